@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""bench.py — distinct states/s and time-to-exhaust of an exhaustive Raft model
+check on MI355X (BASELINE.json metric).
+
+A "step" is one complete exhaustive check of the workload config (BFS from
+Init until the frontier is empty), on inputs resident in HBM (the constants
+are the input; the frontier, fingerprint set and trace records never leave
+the GPU while timed).  `value` = distinct states / seconds-per-check, summed
+over ranks.
+
+Multi-GPU: one process per GPU (torch.distributed.run).  The fingerprint-
+sharded multi-GPU search is not built yet, so N>1 runs N independent replica
+checks ("parallelism": "replicas").
+
+Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raft-tlaplus_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+# name -> (module, cfg path relative to ROOT, BASELINE config index, description)
+WORKLOADS = {
+    "raft_cfg": ("Raft", "configs/Raft.cfg", 1,
+                 "standard-raft Raft.cfg: 3 servers, Value={v1}, MaxElections=2, MaxRestarts=0"),
+    "raft_n3v2e2": ("Raft", "configs/Raft_n3v2e2.cfg", 2,
+                    "standard-raft: 3 servers, Value={v1,v2}, MaxElections=2, MaxRestarts=0"),
+    "raft_n3v1e3": ("Raft", "configs/Raft_n3v1e3.cfg", 2,
+                    "standard-raft: 3 servers, Value={v1}, MaxElections=3, MaxRestarts=0"),
+    "raft_n3v2e3": ("Raft", "configs/Raft_n3v2e3.cfg", 2,
+                    "standard-raft: 3 servers, Value={v1,v2}, MaxElections=3, MaxRestarts=0"),
+}
+DEFAULT_WORKLOAD = "raft_cfg"
+HBM_PEAK = 8.0e12  # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
+
+
+def algorithmic_bytes(res):
+    """Bytes the expand kernel must move per run (SURVEY.md §8d terms it owns):
+    every parent state read once (D*S), one fingerprint-set probe per
+    successor (G*8), one 12-byte candidate record written per successor."""
+    D, G, S = res["distinct"], res["generated"] - 1, res["state_bytes"]
+    return D * S + G * 8 + G * 12
+
+
+def cpu_baseline(module, cfg_path, seconds=20.0):
+    """The C oracle (oracle/_build/rmc_oracle, a port) timed on this host for a
+    bounded wall budget on the same config; returns distinct states/s."""
+    from oracle import run_c
+    from oracle.pyoracle.cfg import load_cfg
+    exe = run_c.BIN
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    cfg = load_cfg(os.path.join(ROOT, cfg_path))
+    threads = max(1, min(16, os.cpu_count() or 1))
+    r = run_c.run(module, cfg["constants"], cfg["invariants"], threads=threads,
+                  extra=["--max-seconds", str(seconds)])
+    return dict(value=r["distinct"] / max(r["seconds"], 1e-9), unit="distinct states/s", cores=threads,
+                kind="port",
+                sample="C oracle (oracle/cengine) BFS of the same cfg for ~%.0fs wall: %d distinct, %d generated, "
+                       "status %s" % (seconds, r["distinct"], r["generated"], r["status"]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default=os.environ.get("RMC_WORKLOAD", DEFAULT_WORKLOAD))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import torch
+    import raftmc
+
+    module, cfg_rel, bcfg, desc = WORKLOADS[args.workload]
+    model = raftmc.Model(os.path.join(ROOT, "configs", module + ".tla"), os.path.join(ROOT, cfg_rel))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        model.check()
+    barrier()
+    t0 = time.perf_counter()
+    results = []
+    for _ in range(args.steps):
+        results.append(model.check())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = results[-1]
+    per_step = elapsed / args.steps
+    value = world * res["distinct"] / per_step
+    exp_bytes = algorithmic_bytes(res)
+    achieved = exp_bytes / (res["expand_ms"] * 1e-3) if res["expand_ms"] > 0 else 0.0
+    if rank == 0:
+        line = {
+            "metric": "distinct states/sec + time-to-exhaust, standard-raft",
+            "value": value,
+            "unit": "distinct states/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": per_step * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: the model constants are the input (no dataset)",
+            "config": {"workload": args.workload, "baseline_config": bcfg, "description": desc,
+                       "spec": module, "cfg": cfg_rel,
+                       "parallelism": "replicas" if world > 1 else "single"},
+            "result": {"generated": res["generated"], "distinct": res["distinct"], "depth": res["depth"],
+                       "status": res["status"], "time_to_exhaust_s": per_step},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "traffic": None,
+                         "kernel": "k_expand", "launches": res["expand_launches"],
+                         "avg_launch_ms": res["expand_ms"] / max(1, res["expand_launches"]),
+                         "bytes_per_launch": exp_bytes / max(1, res["expand_launches"])},
+            "kernel_ms": {"expand": res["expand_ms"], "mark_scan": res["mark_ms"],
+                          "materialize": res["materialize_ms"]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(module, cfg_rel, args.cpu_seconds)
+            except Exception as e:  # report, never hide
+                line["cpu_baseline"] = {"value": None, "error": str(e)}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,91 @@
+/*
+ * rmc.h — C ABI of librmc.so, the MI355X-native explicit-state model checker
+ * for the Raft TLA+ specifications of Vanlightly/raft-tlaplus.
+ *
+ * What it replaces.  The reference has no code of its own on this path: its
+ * specs are run by TLC, invoked as
+ *     java -cp tla2tools.jar tlc2.TLC -deadlock [-workers N] [-config M.cfg] M.tla
+ * (README.md:6 "run all these specifications with the -deadlock argument").
+ * Each entry point below maps to one step of that contract:
+ *   rmc_model_load   <- TLC reading M.tla + M.cfg (SANY parse, constant binding,
+ *                       INIT/NEXT/VIEW/SYMMETRY/INVARIANT), e.g.
+ *                       specifications/standard-raft/Raft.cfg:5-36 bound to
+ *                       specifications/standard-raft/Raft.tla:1-638
+ *   rmc_check        <- the model-checking run (BFS over Init/Next, Raft.tla:213,527),
+ *                       producing TLC's "<G> states generated, <D> distinct states
+ *                       found, <Q> states left on queue" and "depth <d>" lines
+ *   rmc_trace_len /
+ *   rmc_trace_state  <- TLC's "Error: The behavior up to this point is:" block
+ *                       (State k: /\ var = value) after an invariant violation
+ *                       (invariants Raft.tla:588-620, listed at Raft.cfg:34-36)
+ *   rmc_model_free   <- end of run
+ * Plain pointers and sizes only; no torch or HIP types cross this boundary.
+ *
+ * Ownership: the caller owns rmc_options, rmc_result and text buffers; the
+ * library owns the model, device memory and the trace until rmc_model_free.
+ * Errors: a negative return is an API/IO error with a message in `err` (or
+ * rmc_last_error()); model outcomes are reported in rmc_result.status.
+ * Threading: rmc_check is blocking and not re-entrant per model.
+ */
+#ifndef RMC_H
+#define RMC_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rmc_model rmc_model; /* lowered spec + cfg; library-owned */
+
+typedef struct {
+  int n_gpus;          /* GPUs used by this process (1; multi-GPU = one process per GPU) */
+  int cpu_workers;     /* accepted for TLC CLI compatibility (-workers); unused by the GPU path */
+  int deadlock_check;  /* 0 = TLC -deadlock (the reference's mode); 1 is rejected */
+  int fp_bits;         /* 64 (default) */
+  int tlc_order;       /* 1 (default): first successor in TLC order wins per fingerprint */
+  uint64_t hash_slots; /* fingerprint-set capacity (power of two); 0 = auto */
+  uint32_t msg_cap_K;  /* message slots per packed state; 0 = auto */
+  uint64_t frontier_cap; /* max states per BFS level; 0 = auto */
+  uint32_t chunk_parents; /* parents expanded per launch; 0 = auto */
+  int verbose;         /* per-level progress on stderr */
+  int max_depth;       /* stop after this many levels (0 = exhaustive) */
+} rmc_options;
+
+typedef struct {
+  uint64_t generated, distinct, left_on_queue;
+  uint32_t depth;
+  int status; /* 0 ok, 1 invariant violated, 2 evaluation error, 3 capacity overflow, 4 stopped (max_depth) */
+  char violated[64];
+  char message[256];
+  uint64_t hidden_var_collisions; /* reserved */
+  double seconds;
+  /* measurement (filled by rmc_check) */
+  double expand_ms, mark_ms, materialize_ms; /* summed device time per kernel family */
+  uint64_t expand_launches;
+  uint32_t state_bytes; /* packed frontier state size */
+  uint32_t max_msgs;    /* largest |DOMAIN messages| seen */
+  uint64_t hash_capacity;
+} rmc_result;
+
+/* Load M.tla + M.cfg.  tla_path may name a file that does not exist; the module
+ * is then taken from its basename (M.tla -> M).  Returns 0 or a negative error. */
+int rmc_model_load(const char* tla_path, const char* cfg_path, rmc_model** out, char* err, size_t errlen);
+/* Same, from in-memory cfg text and a module name. */
+int rmc_model_load_text(const char* module, const char* cfg_text, rmc_model** out, char* err, size_t errlen);
+void rmc_options_default(rmc_options* o);
+int rmc_check(rmc_model* m, const rmc_options* o, rmc_result* out); /* blocking */
+int rmc_trace_len(const rmc_model* m);                               /* after status 1/2 */
+int rmc_trace_state(const rmc_model* m, int k, char* tla_text, size_t len); /* TLC value syntax */
+int rmc_trace_action(const rmc_model* m, int k, char* text, size_t len);   /* "Initial predicate" / action label */
+/* Print the TLC-format report for a finished check into buf. */
+int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t len);
+void rmc_model_free(rmc_model* m);
+const char* rmc_last_error(void);
+const char* rmc_version(void);
+/* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
+int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RMC_H */

@@ -1,0 +1,1292 @@
+// rmc_oracle — CPU restatement of the four Raft specs under TLC -workers 1
+// semantics.  TEST INFRASTRUCTURE ONLY: this is the checker the HIP path is
+// compared against (and the CPU baseline bench.py times); it shares no code
+// with raft-tlaplus_amd/.
+//
+// Restated from /root/reference/specifications/:
+//   standard-raft/Raft.tla        (Next :527-539, invariants :588-620)
+//   flexible-raft/FlexibleRaft.tla (Next :488-500)
+//   raft-and-fsync/RaftFsync.tla  (Next :522-536)
+//   pull-raft/PullRaft.tla        (Next :542-558)
+// TLC semantics: actions split per constant binding
+// (first bound variable fastest), DOMAIN messages enumerated in TLC value
+// order, FIFO BFS, first successor per fingerprint wins, invariants checked on
+// new states, VIEW hides the aux variables, SYMMETRY = all server permutations.
+//
+// Fingerprints here are EXACT canonical forms (lexicographic minimum of a
+// complete serialisation of the view over every server permutation that can
+// attain it) hashed to 128 bits; the GPU path uses a different construction
+// (min over permutations of a 64-bit additive hash), so agreement between the
+// two is evidence for both.
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+#include <thread>
+#include <atomic>
+
+namespace {
+
+enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3 };
+enum MType : int8_t { RVREQ = 0, RVRESP, AEREQ, AERESP, LNREQ, PEREQ, PERESP };
+enum SState : int8_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
+constexpr int NIL = -1;
+constexpr int MAXN = 8, MAXV = 4, MAXL = 8, MAXMSG = 192;
+
+struct EvalError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// A message record.  Unused fields are 0 so memcmp over the record part is
+// record equality.  `count` is the bag multiplicity (messages[m]).
+struct Msg {
+  int8_t type, term, src, dst;
+  int8_t lastLogTerm, lastLogIndex;  // RequestVoteRequest, PullEntriesRequest
+  int8_t voteGranted;                // RequestVoteResponse
+  int8_t prevLogIndex, prevLogTerm;  // AppendEntriesRequest
+  int8_t nent, eterm, evalue;        // mentries (0 or 1 entry)
+  int8_t commit;                     // mcommitIndex
+  int8_t success, matchIndex;        // AppendEntriesResponse, PullEntriesResponse
+  int8_t lciIndex, lciTerm;          // mlastCommonEntry
+  uint8_t count;
+};
+constexpr size_t REC_BYTES = offsetof(Msg, count);
+inline bool rec_eq(const Msg& a, const Msg& b) { return memcmp(&a, &b, REC_BYTES) == 0; }
+
+struct Entry { int8_t term, value; };
+
+struct State {
+  int16_t nmsg;
+  int8_t electionCtr, restartCtr;
+  int8_t acked[MAXV];  // -1 Nil, 0 FALSE, 1 TRUE
+  int8_t term[MAXN], st[MAXN], voted[MAXN];  // voted = votedFor (Pull: leader)
+  int8_t loglen[MAXN], commit[MAXN], fsync[MAXN];
+  uint8_t votes[MAXN], pending[MAXN];  // bitsets over servers
+  Entry log[MAXN][MAXL];
+  int8_t next[MAXN][MAXN], match[MAXN][MAXN];
+  Msg msgs[MAXMSG];  // DOMAIN messages, sorted in TLC order
+};
+constexpr size_t FIXED_BYTES = offsetof(State, msgs);
+
+struct Config {
+  SpecKind spec = RAFT;
+  int N = 3, V = 1, E = 2, R = 0;
+  int EQ = 0, RQ = 0;                       // FlexibleRaft quorum sizes
+  bool lfae = false, lfiq = true, ffbr = true;  // RaftFsync policy flags
+  bool inv_lhaav = true, inv_nld = true, inv_cerm = false;
+  std::vector<std::string> inv_order;
+};
+Config C;
+
+// ------------------------------------------------------------- TLC ordering
+// TLC compares records by field count, then (sorted) field name and value in
+// turn; sequences by length then elements; model values by name; FALSE<TRUE.
+// We build a byte key with exactly that lexicographic order.
+const char* type_name(int t) {
+  static const char* n[] = {"RequestVoteRequest", "RequestVoteResponse", "AppendEntriesRequest",
+                            "AppendEntriesResponse", "LeaderNotifyRequest", "PullEntriesRequest",
+                            "PullEntriesResponse"};
+  return n[t];
+}
+struct Key {
+  uint8_t b[160];
+  int n = 0;
+  void byte(int v) { b[n++] = (uint8_t)v; }
+  void str(const char* s) { while (*s) b[n++] = (uint8_t)*s++; b[n++] = 0; }
+};
+struct Field { const char* name; int kind; int v0, v1, v2; };
+// kinds: 0 int/bool/server, 1 type name, 2 mentries seq, 3 lastCommonEntry record
+void msg_key(const Msg& m, Key& k) {
+  Field f[8];
+  int nf = 0;
+  auto add = [&](const char* nm, int kind, int a = 0, int b = 0, int c = 0) { f[nf++] = {nm, kind, a, b, c}; };
+  add("mtype", 1, m.type);
+  add("mterm", 0, m.term);
+  add("msource", 0, m.src);
+  add("mdest", 0, m.dst);
+  switch (m.type) {
+    case RVREQ: case PEREQ:
+      add("mlastLogTerm", 0, m.lastLogTerm); add("mlastLogIndex", 0, m.lastLogIndex); break;
+    case RVRESP: add("mvoteGranted", 0, m.voteGranted); break;
+    case AEREQ:
+      add("mprevLogIndex", 0, m.prevLogIndex); add("mprevLogTerm", 0, m.prevLogTerm);
+      add("mentries", 2, m.nent, m.eterm, m.evalue); add("mcommitIndex", 0, m.commit); break;
+    case AERESP: add("msuccess", 0, m.success); add("mmatchIndex", 0, m.matchIndex); break;
+    case LNREQ: break;
+    case PERESP:
+      add("msuccess", 0, m.success);
+      if (m.success) { add("mentries", 2, m.nent, m.eterm, m.evalue); add("mcommitIndex", 0, m.commit); }
+      else add("mlastCommonEntry", 3, m.lciIndex, m.lciTerm);
+      break;
+  }
+  std::sort(f, f + nf, [](const Field& a, const Field& b) { return strcmp(a.name, b.name) < 0; });
+  k.n = 0;
+  k.byte(nf);
+  for (int i = 0; i < nf; i++) {
+    k.str(f[i].name);
+    switch (f[i].kind) {
+      case 0: k.byte(f[i].v0); break;
+      case 1: k.str(type_name(f[i].v0)); break;
+      case 2:  // <<>> or << [term |-> t, value |-> v] >>
+        k.byte(f[i].v0);
+        if (f[i].v0) { k.byte(2); k.str("term"); k.byte(f[i].v1); k.str("value"); k.byte(f[i].v2); }
+        break;
+      case 3: k.byte(2); k.str("index"); k.byte(f[i].v0); k.str("term"); k.byte(f[i].v1); break;
+    }
+  }
+}
+int tlc_cmp(const Msg& a, const Msg& b) {
+  Key ka, kb;
+  msg_key(a, ka);
+  msg_key(b, kb);
+  int n = std::min(ka.n, kb.n);
+  int c = memcmp(ka.b, kb.b, n);
+  if (c) return c;
+  return ka.n - kb.n;
+}
+
+// ------------------------------------------------------------- bag helpers
+int find_msg(const State& s, const Msg& m) {
+  for (int k = 0; k < s.nmsg; k++)
+    if (rec_eq(s.msgs[k], m)) return k;
+  return -1;
+}
+void insert_msg(State& s, Msg m, int count) {  // m not in DOMAIN
+  if (s.nmsg >= MAXMSG) throw EvalError("message capacity exceeded (oracle MAXMSG)");
+  m.count = (uint8_t)count;
+  int pos = s.nmsg;
+  while (pos > 0 && tlc_cmp(s.msgs[pos - 1], m) > 0) {
+    s.msgs[pos] = s.msgs[pos - 1];
+    pos--;
+  }
+  s.msgs[pos] = m;
+  s.nmsg++;
+}
+Msg mk(int type, int term, int src, int dst) {
+  Msg m;
+  memset(&m, 0, sizeof m);
+  m.type = (int8_t)type; m.term = (int8_t)term; m.src = (int8_t)src; m.dst = (int8_t)dst;
+  return m;
+}
+
+// Send variants (Raft.tla:129-155; FlexibleRaft.tla:127-133; RaftFsync.tla:132-134; PullRaft.tla:137-143)
+bool send_once(State& t, const Msg& m) {
+  if (find_msg(t, m) >= 0) return false;
+  insert_msg(t, m, 1);
+  return true;
+}
+void send_norestrict(State& t, const Msg& m) {
+  int k = find_msg(t, m);
+  if (k >= 0) t.msgs[k].count++;
+  else insert_msg(t, m, 1);
+}
+// Reply (Raft.tla:170-176 increments an existing response; the other specs
+// require the response to be absent: FlexibleRaft.tla:148-151 etc.)
+bool reply(State& t, const Msg& response, int req_idx) {
+  if (!(t.msgs[req_idx].count > 0)) return false;
+  int k = find_msg(t, response);
+  if (k >= 0) {
+    if (C.spec != RAFT) return false;
+    t.msgs[req_idx].count--;
+    t.msgs[k].count++;
+    return true;
+  }
+  t.msgs[req_idx].count--;
+  insert_msg(t, response, 1);
+  return true;
+}
+
+// --------------------------------------------------------------- helpers
+inline int Len(const State& s, int i) { return s.loglen[i]; }
+inline const Entry& log_at(const State& s, int i, int idx) {
+  if (idx < 1 || idx > s.loglen[i]) throw EvalError("log[" + std::to_string(i) + "] applied to " + std::to_string(idx));
+  return s.log[i][idx - 1];
+}
+inline int LastTerm(const State& s, int i) { return s.loglen[i] == 0 ? 0 : log_at(s, i, s.loglen[i]).term; }
+inline int popc(unsigned x) { return __builtin_popcount(x); }
+inline bool is_quorum(unsigned set) { return popc(set) * 2 > C.N; }  // Raft.tla:123
+void append(State& t, int i, Entry e) {
+  if (t.loglen[i] >= MAXL) throw EvalError("log capacity exceeded (oracle MAXL)");
+  t.log[i][t.loglen[i]++] = e;
+}
+bool receivable(const State& s, int k, int type, bool equal) {  // Raft.tla:181-187
+  const Msg& m = s.msgs[k];
+  if (!(m.count > 0) || m.type != type) return false;
+  return equal ? m.term == s.term[m.dst] : m.term <= s.term[m.dst];
+}
+
+// Successors are reported with their action id (for labels / stats).
+enum Act {
+  A_RESTART, A_REQUESTVOTE, A_TIMEOUT, A_REQUESTVOTE_IJ, A_BECOMELEADER, A_CLIENTREQUEST,
+  A_ADVANCECOMMIT, A_APPENDENTRIES, A_ADVANCEFSYNC, A_UPDATETERM, A_HRVREQ, A_HRVRESP,
+  A_REJECTAE, A_ACCEPTAE, A_HAERESP, A_REJECTPULL, A_ACCEPTPULL, A_LEARNOFLEADER,
+  A_SENDPULL, A_HSUCCESSPULL, A_HFAILPULL, A_COUNT
+};
+const char* act_name(int a) {
+  static const char* n[] = {"Restart", "RequestVote", "Timeout", "RequestVote", "BecomeLeader",
+                            "ClientRequest", "AdvanceCommitIndex", "AppendEntries", "AdvanceFsyncIndex",
+                            "UpdateTerm", "HandleRequestVoteRequest", "HandleRequestVoteResponse",
+                            "RejectAppendEntriesRequest", "AcceptAppendEntriesRequest",
+                            "HandleAppendEntriesResponse", "RejectPullEntriesRequest",
+                            "AcceptPullEntriesRequest", "LearnOfLeader", "SendPullEntriesRequest",
+                            "HandleSuccessPullEntriesResponse", "HandleFailPullEntriesResponse"};
+  return n[a];
+}
+
+struct Emitter {
+  virtual void emit(const State& t, int act) = 0;
+  virtual ~Emitter() {}
+};
+
+// ----------------------------------------------------------------- actions
+void Restart(const State& s, int i, Emitter& E) {
+  // Raft.tla:226-235, FlexibleRaft.tla:200-208, RaftFsync.tla:203-218, PullRaft.tla:258-265
+  if (!(s.restartCtr < C.R)) return;
+  State t = s;
+  t.st[i] = FOLLOWER;
+  t.votes[i] = 0;
+  for (int j = 0; j < C.N; j++) { t.next[i][j] = 1; t.match[i][j] = 0; }
+  t.pending[i] = 0;
+  t.commit[i] = 0;
+  t.restartCtr++;
+  if (C.spec == FSYNC) {
+    int f = s.fsync[i], L = s.loglen[i];
+    if (f == 0) t.loglen[i] = 0;
+    else if (L > 0 && L > f) t.loglen[i] = (int8_t)f;  // SubSeq(@, 1, fsyncIndex[i])
+  }
+  E.emit(t, A_RESTART);
+}
+
+void RequestVote(const State& s, int i, Emitter& E) {
+  // Raft.tla:242-257 (= FlexibleRaft.tla:215-230; PullRaft.tla:283-298 sets leader[i])
+  if (!(s.electionCtr < C.E)) return;
+  if (!(s.st[i] == FOLLOWER || s.st[i] == CANDIDATE)) return;
+  State t = s;
+  for (int j = 0; j < C.N; j++) {
+    if (j == i) continue;
+    Msg m = mk(RVREQ, s.term[i] + 1, i, j);
+    m.lastLogTerm = (int8_t)LastTerm(s, i);
+    m.lastLogIndex = (int8_t)Len(s, i);
+    if (find_msg(s, m) >= 0) return;  // SendMultipleOnce: all must be new
+    insert_msg(t, m, 1);
+  }
+  t.st[i] = CANDIDATE;
+  t.term[i] = (int8_t)(s.term[i] + 1);
+  t.voted[i] = (int8_t)i;
+  t.votes[i] = (uint8_t)(1u << i);
+  t.electionCtr++;
+  E.emit(t, A_REQUESTVOTE);
+}
+
+void Timeout(const State& s, int i, Emitter& E) {  // RaftFsync.tla:222-230
+  if (!(s.electionCtr < C.E)) return;
+  if (!(s.st[i] == FOLLOWER || s.st[i] == CANDIDATE)) return;
+  State t = s;
+  t.st[i] = CANDIDATE;
+  t.term[i] = (int8_t)(s.term[i] + 1);
+  t.voted[i] = (int8_t)i;
+  t.votes[i] = (uint8_t)(1u << i);
+  t.electionCtr++;
+  E.emit(t, A_TIMEOUT);
+}
+
+void RequestVoteIJ(const State& s, int i, int j, Emitter& E) {  // RaftFsync.tla:234-243
+  if (s.st[i] != CANDIDATE || i == j) return;
+  Msg m = mk(RVREQ, s.term[i], i, j);
+  m.lastLogTerm = (int8_t)LastTerm(s, i);
+  m.lastLogIndex = (int8_t)Len(s, i);
+  State t = s;
+  if (!send_once(t, m)) return;
+  E.emit(t, A_REQUESTVOTE_IJ);
+}
+
+void AppendEntries(const State& s, int i, int j, Emitter& E) {
+  // Raft.tla:263-285; FlexibleRaft.tla:236-256; RaftFsync.tla:249-272
+  if (i == j || s.st[i] != LEADER) return;
+  if (C.spec == RAFT && (s.pending[i] >> j & 1)) return;
+  int nxt = s.next[i][j];
+  int prevLogIndex = nxt - 1;
+  int prevLogTerm = prevLogIndex > 0 ? log_at(s, i, prevLogIndex).term : 0;
+  int lastEntry = std::min(Len(s, i), nxt);
+  if (C.spec == FSYNC && C.lfae && !(s.fsync[i] >= lastEntry)) return;
+  Msg m = mk(AEREQ, s.term[i], i, j);
+  m.prevLogIndex = (int8_t)prevLogIndex;
+  m.prevLogTerm = (int8_t)prevLogTerm;
+  // SubSeq(log[i], nextIndex[i][j], lastEntry): at most one entry
+  int nent = lastEntry - nxt + 1;
+  if (nent < 0) nent = 0;
+  if (nent > 1) throw EvalError("AppendEntries: more than one entry");
+  m.nent = (int8_t)nent;
+  if (nent) { const Entry& e = log_at(s, i, nxt); m.eterm = e.term; m.evalue = e.value; }
+  m.commit = (int8_t)std::min((int)s.commit[i], lastEntry);
+  State t = s;
+  if (C.spec == RAFT) {
+    t.pending[i] |= (uint8_t)(1u << j);
+    if (nent == 0) { if (!send_once(t, m)) return; }  // _SendOnce for empty AE
+    else send_norestrict(t, m);
+  } else {
+    if (!send_once(t, m)) return;
+  }
+  E.emit(t, A_APPENDENTRIES);
+}
+
+void BecomeLeader(const State& s, int i, Emitter& E) {
+  // Raft.tla:289-300; FlexibleRaft.tla:260-269; RaftFsync.tla:276-285; PullRaft.tla:354-366
+  if (s.st[i] != CANDIDATE) return;
+  bool q = C.spec == FLEX ? popc(s.votes[i]) >= C.EQ : is_quorum(s.votes[i]);
+  if (!q) return;
+  State t = s;
+  if (C.spec == PULL) {
+    for (int j = 0; j < C.N; j++) {
+      if (s.votes[i] >> j & 1) continue;
+      Msg m = mk(LNREQ, s.term[i], i, j);
+      if (find_msg(s, m) >= 0) return;
+      insert_msg(t, m, 1);
+    }
+  }
+  t.st[i] = LEADER;
+  for (int j = 0; j < C.N; j++) {
+    if (C.spec != PULL) t.next[i][j] = (int8_t)(Len(s, i) + 1);
+    t.match[i][j] = 0;
+  }
+  if (C.spec == RAFT) t.pending[i] = 0;
+  E.emit(t, A_BECOMELEADER);
+}
+
+void ClientRequest(const State& s, int i, int v, Emitter& E) {  // Raft.tla:304-313
+  if (s.st[i] != LEADER || s.acked[v] != NIL) return;
+  State t = s;
+  append(t, i, Entry{s.term[i], (int8_t)v});
+  t.acked[v] = 0;
+  E.emit(t, A_CLIENTREQUEST);
+}
+
+unsigned agree_set(const State& s, int i, int index, const int8_t* matchrow) {
+  // Raft.tla:323-324; RaftFsync.tla:313-315
+  unsigned ks = 0;
+  for (int k = 0; k < C.N; k++)
+    if (matchrow[k] >= index) ks |= 1u << k;
+  if (C.spec == FSYNC && C.lfiq && index > s.fsync[i]) return ks;
+  return ks | (1u << i);
+}
+bool agree_ok(unsigned set) {
+  return C.spec == FLEX ? popc(set) >= C.RQ : is_quorum(set);  // FlexibleRaft.tla:296
+}
+int new_commit_index(const State& s, int i, const int8_t* matchrow) {
+  int best = 0;
+  for (int index = 1; index <= Len(s, i); index++)
+    if (agree_ok(agree_set(s, i, index, matchrow))) best = index;  // Max(agreeIndexes)
+  if (best > 0 && log_at(s, i, best).term == s.term[i]) return best;
+  return s.commit[i];
+}
+void update_acked(const State& s, State& t, int i, int newCommit) {  // Raft.tla:339-342
+  for (int v = 0; v < C.V; v++) {
+    if (s.acked[v] != 0) continue;
+    bool in = false;
+    for (int idx = s.commit[i] + 1; idx <= newCommit; idx++)
+      if (log_at(s, i, idx).value == v) in = true;
+    t.acked[v] = in ? 1 : 0;
+  }
+}
+
+void AdvanceCommitIndex(const State& s, int i, Emitter& E) {  // Raft.tla:320-344
+  if (s.st[i] != LEADER) return;
+  int nc = new_commit_index(s, i, s.match[i]);
+  if (!(s.commit[i] < nc)) return;
+  State t = s;
+  t.commit[i] = (int8_t)nc;
+  update_acked(s, t, i, nc);
+  E.emit(t, A_ADVANCECOMMIT);
+}
+
+void AdvanceFsyncIndex(const State& s, int i, Emitter& E) {  // RaftFsync.tla:339-343
+  if (!(s.fsync[i] < Len(s, i))) return;
+  State t = s;
+  t.fsync[i]++;
+  E.emit(t, A_ADVANCEFSYNC);
+}
+
+void UpdateTerm(const State& s, Emitter& E) {  // Raft.tla:348-355; PullRaft.tla:269-276
+  for (int k = 0; k < s.nmsg; k++) {
+    const Msg& m = s.msgs[k];
+    if (!(m.term > s.term[m.dst])) continue;
+    State t = s;
+    t.term[m.dst] = m.term;
+    t.st[m.dst] = FOLLOWER;
+    t.voted[m.dst] = NIL;
+    E.emit(t, A_UPDATETERM);
+  }
+}
+
+void HandleRequestVoteRequest(const State& s, Emitter& E) {  // Raft.tla:360-381; PullRaft.tla:306-330
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, RVREQ, false)) continue;
+    const Msg& m = s.msgs[k];
+    int i = m.dst, j = m.src;
+    int lt = LastTerm(s, i);
+    bool logOk = m.lastLogTerm > lt || (m.lastLogTerm == lt && m.lastLogIndex >= Len(s, i));
+    bool grant = m.term == s.term[i] && logOk && (s.voted[i] == NIL || s.voted[i] == j);
+    Msg r = mk(RVRESP, s.term[i], i, j);
+    r.voteGranted = grant;
+    State t = s;
+    if (!reply(t, r, k)) continue;
+    if (grant) t.voted[i] = (int8_t)j;
+    E.emit(t, A_HRVREQ);
+  }
+}
+
+void HandleRequestVoteResponse(const State& s, Emitter& E) {  // Raft.tla:386-401
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, RVRESP, true)) continue;
+    const Msg& m = s.msgs[k];
+    State t = s;
+    if (m.voteGranted) t.votes[m.dst] |= (uint8_t)(1u << m.src);
+    t.msgs[k].count--;  // Discard
+    E.emit(t, A_HRVRESP);
+  }
+}
+
+bool LogOk(const State& s, int i, const Msg& m) {  // Raft.tla:406-410
+  if (m.prevLogIndex == 0) return true;
+  return m.prevLogIndex > 0 && m.prevLogIndex <= Len(s, i) &&
+         m.prevLogTerm == log_at(s, i, m.prevLogIndex).term;
+}
+
+void RejectAppendEntriesRequest(const State& s, Emitter& E) {  // Raft.tla:412-430
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, AEREQ, false)) continue;
+    const Msg& m = s.msgs[k];
+    int i = m.dst, j = m.src;
+    if (!(m.term < s.term[i] || (m.term == s.term[i] && s.st[i] == FOLLOWER && !LogOk(s, i, m)))) continue;
+    Msg r = mk(AERESP, s.term[i], i, j);
+    r.success = 0;
+    r.matchIndex = 0;
+    State t = s;
+    if (!reply(t, r, k)) continue;
+    E.emit(t, A_REJECTAE);
+  }
+}
+
+void AcceptAppendEntriesRequest(const State& s, Emitter& E) {
+  // Raft.tla:454-485; FlexibleRaft.tla:421-450; RaftFsync.tla:449-481
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, AEREQ, true)) continue;
+    const Msg& m = s.msgs[k];
+    int i = m.dst, j = m.src;
+    int index = m.prevLogIndex + 1;
+    if (!(s.st[i] == FOLLOWER || s.st[i] == CANDIDATE)) continue;
+    if (!LogOk(s, i, m)) continue;
+    int L = Len(s, i);
+    bool canAppend = m.nent != 0 && L == m.prevLogIndex;  // Raft.tla:438-440
+    State t = s;
+    if (C.spec == RAFT) {
+      // NeedsTruncation, Raft.tla:445-449; CASE arms :464-470
+      bool needs = (m.nent != 0 && L >= index) || (m.nent == 0 && L > m.prevLogIndex);
+      if (canAppend) append(t, i, Entry{m.eterm, m.evalue});
+      else if (needs && m.nent != 0) { t.loglen[i] = m.prevLogIndex; append(t, i, Entry{m.eterm, m.evalue}); }
+      else if (needs && m.nent == 0) t.loglen[i] = m.prevLogIndex;
+    } else {
+      // NeedsTruncation, FlexibleRaft.tla:413-416: also needs a term mismatch
+      bool needs = m.nent != 0 && L >= index && log_at(s, i, index).term != m.eterm;
+      if (canAppend) append(t, i, Entry{m.eterm, m.evalue});
+      else if (needs) { t.loglen[i] = m.prevLogIndex; append(t, i, Entry{m.eterm, m.evalue}); }
+    }
+    // TruncateLog reads log[i][1..prevLogIndex]; LogOk guarantees prevLogIndex <= Len
+    t.st[i] = FOLLOWER;
+    t.commit[i] = m.commit;
+    if (C.spec == FSYNC && C.ffbr) t.fsync[i] = t.loglen[i];  // RaftFsync.tla:468-470
+    Msg r = mk(AERESP, s.term[i], i, j);
+    r.success = 1;
+    r.matchIndex = (int8_t)(m.prevLogIndex + m.nent);
+    if (!reply(t, r, k)) continue;
+    E.emit(t, A_ACCEPTAE);
+  }
+}
+
+void HandleAppendEntriesResponse(const State& s, Emitter& E) {  // Raft.tla:490-505
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, AERESP, true)) continue;
+    const Msg& m = s.msgs[k];
+    int i = m.dst, j = m.src;
+    State t = s;
+    if (m.success) {
+      t.next[i][j] = (int8_t)(m.matchIndex + 1);
+      t.match[i][j] = m.matchIndex;
+    } else {
+      t.next[i][j] = (int8_t)std::max(s.next[i][j] - 1, 1);
+    }
+    if (C.spec == RAFT) t.pending[i] &= (uint8_t)~(1u << j);
+    t.msgs[k].count--;
+    E.emit(t, A_HAERESP);
+  }
+}
+
+// ---- PullRaft only
+bool ValidPullPosition(const State& s, int i, const Msg& m) {  // PullRaft.tla:192-196
+  if (m.lastLogIndex == 0) return true;
+  return m.lastLogIndex > 0 && m.lastLogIndex <= Len(s, i) &&
+         m.lastLogTerm == log_at(s, i, m.lastLogIndex).term;
+}
+int CompareEntries(int i1, int t1, int i2, int t2) {  // PullRaft.tla:203-207
+  if (t1 > t2) return 1;
+  if (t1 == t2 && i1 > i2) return 1;
+  if (t1 == t2 && i1 == i2) return 0;
+  return -1;
+}
+void LastCommonEntry(const State& s, int i, int lastIndex, int lastTerm, int& idx, int& term) {
+  // PullRaft.tla:211-226
+  idx = 0; term = 0;
+  for (int x = 1; x <= Len(s, i); x++)
+    if (CompareEntries(x, log_at(s, i, x).term, lastIndex, lastTerm) <= 0) idx = x;
+  if (idx) term = log_at(s, i, idx).term;
+}
+
+void LearnOfLeader(const State& s, Emitter& E) {  // PullRaft.tla:383-391
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, LNREQ, true)) continue;
+    State t = s;
+    t.voted[s.msgs[k].dst] = s.msgs[k].src;
+    t.msgs[k].count--;
+    E.emit(t, A_LEARNOFLEADER);
+  }
+}
+
+void SendPullEntriesRequest(const State& s, int i, int j, Emitter& E) {  // PullRaft.tla:396-411
+  if (i == j || s.st[i] != FOLLOWER || s.voted[i] != j) return;
+  int lli = Len(s, i);
+  int llt = lli > 0 ? log_at(s, i, lli).term : 0;
+  Msg m = mk(PEREQ, s.term[i], i, j);
+  m.lastLogIndex = (int8_t)lli;
+  m.lastLogTerm = (int8_t)llt;
+  State t = s;
+  if (!send_once(t, m)) return;
+  E.emit(t, A_SENDPULL);
+}
+
+void RejectPullEntriesRequest(const State& s, Emitter& E) {  // PullRaft.tla:418-436
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, PEREQ, true)) continue;
+    const Msg& m = s.msgs[k];
+    int i = m.dst, j = m.src;
+    if (s.st[i] != LEADER) continue;
+    if (ValidPullPosition(s, i, m)) continue;
+    Msg r = mk(PERESP, s.term[i], i, j);
+    r.success = 0;
+    int a, b;
+    LastCommonEntry(s, i, m.lastLogIndex, m.lastLogTerm, a, b);
+    r.lciIndex = (int8_t)a;
+    r.lciTerm = (int8_t)b;
+    State t = s;
+    if (!reply(t, r, k)) continue;
+    E.emit(t, A_REJECTPULL);
+  }
+}
+
+void AcceptPullEntriesRequest(const State& s, Emitter& E) {  // PullRaft.tla:460-488
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, PEREQ, true)) continue;
+    const Msg& m = s.msgs[k];
+    int i = m.dst, j = m.src;
+    int index = m.lastLogIndex + 1;
+    if (s.st[i] != LEADER) continue;
+    if (!ValidPullPosition(s, i, m)) continue;
+    if (!(index <= Len(s, i))) continue;
+    int8_t nm[MAXN];
+    memcpy(nm, s.match[i], MAXN);
+    nm[j] = m.lastLogIndex;
+    int nc = new_commit_index(s, i, nm);  // NewCommitIndex, PullRaft.tla:446-458
+    State t = s;
+    memcpy(t.match[i], nm, MAXN);
+    t.commit[i] = (int8_t)nc;
+    update_acked(s, t, i, nc);
+    Msg r = mk(PERESP, s.term[i], i, j);
+    r.success = 1;
+    r.nent = 1;
+    const Entry& e = log_at(s, i, index);
+    r.eterm = e.term;
+    r.evalue = e.value;
+    r.commit = (int8_t)std::min(nc, index);
+    if (!reply(t, r, k)) continue;
+    E.emit(t, A_ACCEPTPULL);
+  }
+}
+
+void HandleSuccessPullEntriesResponse(const State& s, Emitter& E) {  // PullRaft.tla:493-503
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, PERESP, true)) continue;
+    const Msg& m = s.msgs[k];
+    if (!m.success) continue;
+    int i = m.dst;
+    State t = s;
+    t.commit[i] = m.commit;
+    append(t, i, Entry{m.eterm, m.evalue});
+    t.msgs[k].count--;
+    E.emit(t, A_HSUCCESSPULL);
+  }
+}
+
+void HandleFailPullEntriesResponse(const State& s, Emitter& E) {  // PullRaft.tla:510-520
+  for (int k = 0; k < s.nmsg; k++) {
+    if (!receivable(s, k, PERESP, true)) continue;
+    const Msg& m = s.msgs[k];
+    if (m.success) continue;
+    int i = m.dst;
+    State t = s;
+    if (m.lciIndex > 0) {  // TruncateLog, PullRaft.tla:185-188
+      for (int x = 1; x <= m.lciIndex; x++) log_at(s, i, x);  // domain check
+      t.loglen[i] = m.lciIndex;
+    } else {
+      t.loglen[i] = 0;
+    }
+    t.msgs[k].count--;
+    E.emit(t, A_HFAILPULL);
+  }
+}
+
+// Next, split into TLC actions in TLC order.  Pairs enumerate with the first
+// bound variable fastest: (n1,n1),(n2,n1),(n3,n1),(n1,n2),...
+void Next(const State& s, Emitter& E) {
+  const int N = C.N;
+  auto pairs = [&](auto f) { for (int j = 0; j < N; j++) for (int i = 0; i < N; i++) f(i, j); };
+  auto clients = [&]() { for (int v = 0; v < C.V; v++) for (int i = 0; i < N; i++) ClientRequest(s, i, v, E); };
+  switch (C.spec) {
+    case RAFT: case FLEX:  // Raft.tla:527-539, FlexibleRaft.tla:488-500
+      for (int i = 0; i < N; i++) Restart(s, i, E);
+      for (int i = 0; i < N; i++) RequestVote(s, i, E);
+      for (int i = 0; i < N; i++) BecomeLeader(s, i, E);
+      clients();
+      for (int i = 0; i < N; i++) AdvanceCommitIndex(s, i, E);
+      pairs([&](int i, int j) { AppendEntries(s, i, j, E); });
+      UpdateTerm(s, E);
+      HandleRequestVoteRequest(s, E);
+      HandleRequestVoteResponse(s, E);
+      RejectAppendEntriesRequest(s, E);
+      AcceptAppendEntriesRequest(s, E);
+      HandleAppendEntriesResponse(s, E);
+      break;
+    case FSYNC:  // RaftFsync.tla:522-536
+      for (int i = 0; i < N; i++) Restart(s, i, E);
+      for (int i = 0; i < N; i++) Timeout(s, i, E);
+      pairs([&](int i, int j) { RequestVoteIJ(s, i, j, E); });
+      for (int i = 0; i < N; i++) BecomeLeader(s, i, E);
+      clients();
+      for (int i = 0; i < N; i++) AdvanceCommitIndex(s, i, E);
+      pairs([&](int i, int j) { AppendEntries(s, i, j, E); });
+      for (int i = 0; i < N; i++) AdvanceFsyncIndex(s, i, E);
+      UpdateTerm(s, E);
+      HandleRequestVoteRequest(s, E);
+      HandleRequestVoteResponse(s, E);
+      RejectAppendEntriesRequest(s, E);
+      AcceptAppendEntriesRequest(s, E);
+      HandleAppendEntriesResponse(s, E);
+      break;
+    case PULL:  // PullRaft.tla:542-558
+      for (int i = 0; i < N; i++) Restart(s, i, E);
+      UpdateTerm(s, E);
+      for (int i = 0; i < N; i++) RequestVote(s, i, E);
+      HandleRequestVoteRequest(s, E);
+      HandleRequestVoteResponse(s, E);
+      for (int i = 0; i < N; i++) BecomeLeader(s, i, E);
+      clients();
+      RejectPullEntriesRequest(s, E);
+      AcceptPullEntriesRequest(s, E);
+      LearnOfLeader(s, E);
+      pairs([&](int i, int j) { SendPullEntriesRequest(s, i, j, E); });
+      HandleSuccessPullEntriesResponse(s, E);
+      HandleFailPullEntriesResponse(s, E);
+      break;
+  }
+}
+
+State Init() {  // Raft.tla:197-218 (and the variants' Init)
+  State s;
+  memset(&s, 0, sizeof s);
+  for (int v = 0; v < C.V; v++) s.acked[v] = NIL;
+  for (int i = 0; i < C.N; i++) {
+    s.term[i] = 1;
+    s.st[i] = FOLLOWER;
+    s.voted[i] = NIL;
+    for (int j = 0; j < C.N; j++) { s.next[i][j] = 1; s.match[i][j] = 0; }
+  }
+  return s;
+}
+
+// -------------------------------------------------------------- invariants
+bool entry_eq(const Entry& a, const Entry& b) { return a.term == b.term && a.value == b.value; }
+bool NoLogDivergence(const State& s) {  // Raft.tla:588-596
+  for (int s2 = 0; s2 < C.N; s2++)
+    for (int s1 = 0; s1 < C.N; s1++) {
+      if (s1 == s2) continue;
+      int c = std::min(s.commit[s1], s.commit[s2]);
+      for (int idx = 1; idx <= c; idx++)
+        if (!entry_eq(log_at(s, s1, idx), log_at(s, s2, idx))) return false;
+    }
+  return true;
+}
+bool LeaderHasAllAckedValues(const State& s) {  // Raft.tla:604-620
+  for (int v = 0; v < C.V; v++) {
+    if (s.acked[v] != 1) continue;
+    for (int i = 0; i < C.N; i++) {
+      if (s.st[i] != LEADER) continue;
+      bool newer = false;
+      for (int l = 0; l < C.N; l++)
+        if (l != i && s.term[l] > s.term[i]) newer = true;
+      if (newer) continue;
+      bool has = false;
+      for (int x = 0; x < s.loglen[i]; x++)
+        if (s.log[i][x].value == v) has = true;
+      if (!has) return false;
+    }
+  }
+  return true;
+}
+bool CommittedEntriesReachMajority(const State& s) {  // Raft.tla:625-636
+  bool any = false;
+  for (int i = 0; i < C.N; i++) if (s.st[i] == LEADER && s.commit[i] > 0) any = true;
+  if (!any) return true;
+  int size = C.N / 2 + 1;
+  for (int i = 0; i < C.N; i++) {
+    if (!(s.st[i] == LEADER && s.commit[i] > 0)) continue;
+    int ci = s.commit[i];
+    for (unsigned q = 0; q < (1u << C.N); q++) {
+      if (popc(q) != size || !(q >> i & 1)) continue;
+      bool ok = true;
+      for (int j = 0; j < C.N && ok; j++) {
+        if (!(q >> j & 1)) continue;
+        if (!(s.loglen[j] >= ci)) { ok = false; break; }
+        if (!entry_eq(log_at(s, j, ci), log_at(s, i, ci))) ok = false;
+      }
+      if (ok) return true;
+    }
+  }
+  return false;
+}
+const char* check_invariants(const State& s) {
+  for (auto& n : C.inv_order) {
+    if (n == "LeaderHasAllAckedValues" && !LeaderHasAllAckedValues(s)) return "LeaderHasAllAckedValues";
+    if (n == "NoLogDivergence" && !NoLogDivergence(s)) return "NoLogDivergence";
+    if (n == "CommittedEntriesReachMajority" && !CommittedEntriesReachMajority(s)) return "CommittedEntriesReachMajority";
+  }
+  return nullptr;
+}
+
+// ------------------------------------------------------- exact canonical form
+// serialisation(pi) = [inv(server at pos 0..N-1)] ++ [relabelled server-valued
+// fields at pos 0..N-1] ++ sorted(relabelled messages) (++ acked for Pull).
+// inv() is permutation-invariant, so a minimal serialisation must sort the
+// servers by inv(); only those permutations are tried.
+struct Ser {
+  uint8_t b[4096];
+  int n = 0;
+  void put(int v) { b[n++] = (uint8_t)v; }
+};
+void server_inv(const State& s, int i, Ser& o) {
+  o.put(s.term[i]); o.put(s.st[i]); o.put(s.loglen[i]);
+  for (int x = 0; x < s.loglen[i]; x++) { o.put(s.log[i][x].term); o.put(s.log[i][x].value); }
+  o.put(s.commit[i]);
+  if (C.spec == FSYNC) o.put(s.fsync[i]);
+}
+void canonical(const State& s, Ser& best) {
+  const int N = C.N;
+  // group servers by invariant bytes
+  Ser inv[MAXN];
+  for (int i = 0; i < N; i++) server_inv(s, i, inv[i]);
+  int order[MAXN];
+  for (int i = 0; i < N; i++) order[i] = i;
+  auto less = [&](int a, int b) {
+    int n = std::min(inv[a].n, inv[b].n);
+    int c = memcmp(inv[a].b, inv[b].b, n);
+    return c ? c < 0 : inv[a].n < inv[b].n;
+  };
+  auto same = [&](int a, int b) { return inv[a].n == inv[b].n && memcmp(inv[a].b, inv[b].b, inv[a].n) == 0; };
+  std::stable_sort(order, order + N, less);
+  // enumerate permutations within tie classes: iterate all permutations of
+  // `order` that keep the inv-sorted property.
+  int cur[MAXN];
+  memcpy(cur, order, sizeof(int) * N);
+  // class boundaries
+  int cls[MAXN];
+  for (int k = 0, c = 0; k < N; k++) { if (k > 0 && !same(order[k - 1], order[k])) c++; cls[k] = c; }
+  bool have = false;
+  uint32_t msgbuf[MAXMSG];
+  while (true) {
+    // cur[pos] = original server placed at position pos; p = inverse map
+    int p[MAXN];
+    for (int pos = 0; pos < N; pos++) p[cur[pos]] = pos;
+    Ser o;
+    for (int pos = 0; pos < N; pos++) { const Ser& v = inv[cur[pos]]; memcpy(o.b + o.n, v.b, v.n); o.n += v.n; }
+    for (int pos = 0; pos < N; pos++) {
+      int i = cur[pos];
+      o.put(s.voted[i] == NIL ? 255 : p[s.voted[i]]);
+      unsigned vg = 0, pd = 0;
+      for (int j = 0; j < N; j++) {
+        if (s.votes[i] >> j & 1) vg |= 1u << p[j];
+        if (s.pending[i] >> j & 1) pd |= 1u << p[j];
+      }
+      o.put(vg);
+      if (C.spec == RAFT) o.put(pd);
+      for (int q = 0; q < N; q++) {
+        int j = cur[q];
+        if (C.spec != PULL) o.put(s.next[i][j]);
+        o.put(s.match[i][j]);
+      }
+    }
+    if (C.spec == PULL) for (int v = 0; v < C.V; v++) o.put(s.acked[v] + 1);
+    // messages: relabel, pack into sortable u64-ish byte strings
+    int nm = s.nmsg;
+    struct MB { uint8_t b[REC_BYTES + 1]; };
+    static thread_local MB mb[MAXMSG];
+    static thread_local int idx[MAXMSG];
+    for (int k = 0; k < nm; k++) {
+      Msg m = s.msgs[k];
+      m.src = (int8_t)p[m.src];
+      m.dst = (int8_t)p[m.dst];
+      memcpy(mb[k].b, &m, REC_BYTES + 1);
+      idx[k] = k;
+    }
+    std::sort(idx, idx + nm, [&](int a, int b) { return memcmp(mb[a].b, mb[b].b, REC_BYTES + 1) < 0; });
+    o.put(nm);
+    for (int k = 0; k < nm; k++) { memcpy(o.b + o.n, mb[idx[k]].b, REC_BYTES + 1); o.n += REC_BYTES + 1; }
+    (void)msgbuf;
+    if (!have || (o.n != best.n ? o.n < best.n : memcmp(o.b, best.b, o.n) < 0)) {
+      best = o;
+      have = true;
+    }
+    // next permutation within classes (lexicographic over positions)
+    bool advanced = false;
+    for (int start = N - 1; start >= 0 && !advanced; ) {
+      int c = cls[start];
+      int lo = start;
+      while (lo > 0 && cls[lo - 1] == c) lo--;
+      if (std::next_permutation(cur + lo, cur + start + 1)) advanced = true;
+      else start = lo - 1;  // this class wrapped around (next_permutation reset it); carry
+    }
+    if (!advanced) break;
+  }
+}
+
+struct Key128 { uint64_t a, b; };
+inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+Key128 hash_ser(const Ser& o) {
+  uint64_t h1 = 0x9E3779B97F4A7C15ULL ^ (uint64_t)o.n, h2 = 0xC2B2AE3D27D4EB4FULL + (uint64_t)o.n * 31;
+  int k = 0;
+  for (; k + 8 <= o.n; k += 8) {
+    uint64_t w;
+    memcpy(&w, o.b + k, 8);
+    h1 = mix64(h1 ^ w) + 0x632BE59BD9B4E019ULL;
+    h2 = mix64(h2 + w * 0xFF51AFD7ED558CCDULL) ^ (h2 >> 17);
+  }
+  uint64_t w = 0;
+  memcpy(&w, o.b + k, o.n - k);
+  h1 = mix64(h1 ^ w ^ 0xA5);
+  h2 = mix64(h2 + w + 0x5A);
+  return {h1, h2 | 1};  // b != 0 marks an occupied slot
+}
+
+// open-addressing set of 128-bit keys, value = (level, hidden)
+struct Slot { uint64_t a, b; uint32_t level; uint32_t hidden; };
+struct FPSet {
+  std::vector<Slot> t;
+  uint64_t mask = 0, count = 0;
+  FPSet() { t.resize(1 << 20); mask = t.size() - 1; memset(t.data(), 0, t.size() * sizeof(Slot)); }
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(t);
+    t.assign(old.size() * 2, Slot{0, 0, 0, 0});
+    mask = t.size() - 1;
+    for (auto& s : old)
+      if (s.b) {
+        uint64_t h = s.a & mask;
+        while (t[h].b) h = (h + 1) & mask;
+        t[h] = s;
+      }
+  }
+  // returns nullptr if inserted, else the existing slot
+  Slot* insert(Key128 k, uint32_t level, uint32_t hidden) {
+    if ((count + 1) * 2 > t.size()) grow();
+    uint64_t h = k.a & mask;
+    while (t[h].b) {
+      if (t[h].a == k.a && t[h].b == k.b) return &t[h];
+      h = (h + 1) & mask;
+    }
+    t[h] = Slot{k.a, k.b, level, hidden};
+    count++;
+    return nullptr;
+  }
+};
+
+uint32_t hidden_of(const State& s) {
+  uint32_t h = (uint32_t)s.electionCtr | ((uint32_t)s.restartCtr << 8);
+  if (C.spec != PULL)
+    for (int v = 0; v < C.V; v++) h |= (uint32_t)(s.acked[v] + 1) << (16 + 2 * v);
+  return h;
+}
+
+// compact storage of frontier states
+struct Arena {
+  std::vector<uint8_t> buf;
+  std::vector<uint64_t> off;
+  void push(const State& s) {
+    off.push_back(buf.size());
+    size_t n = FIXED_BYTES + (size_t)s.nmsg * sizeof(Msg);
+    size_t o = buf.size();
+    buf.resize(o + n);
+    memcpy(buf.data() + o, &s, n);
+  }
+  void get(size_t k, State& s) const {
+    size_t n = (k + 1 < off.size() ? off[k + 1] : buf.size()) - off[k];
+    memcpy(&s, buf.data() + off[k], n);
+  }
+  size_t size() const { return off.size(); }
+  void clear() { buf.clear(); off.clear(); }
+};
+
+// ---------------------------------------------------------------- BFS driver
+struct Stats {
+  uint64_t generated = 0, distinct = 0, left = 0;
+  int depth = 0;
+  std::string status = "ok", violated, error;
+  uint64_t hidden_same = 0, hidden_cross = 0;
+  uint64_t act[A_COUNT] = {0};
+  int max_msgs = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> levels;
+  double seconds = 0;
+};
+
+struct SuccCollect : Emitter {
+  std::vector<State>* out;
+  std::vector<int>* acts;
+  void emit(const State& t, int a) override { out->push_back(t); acts->push_back(a); }
+};
+
+std::string state_json(const State& s);
+
+struct Checker {
+  Stats st;
+  FPSet fps;
+  // trace records (parent global index, ordinal within parent's successors)
+  std::vector<uint64_t> parent;
+  std::vector<uint16_t> ordinal;
+  std::vector<uint8_t> actid;
+  uint64_t max_distinct = 0;
+  double max_seconds = 0;
+  int threads = 1;
+  FILE* fpdump = nullptr;
+  int64_t bad_index = -1;
+
+  void run();
+};
+
+// per-thread expansion buffers for a chunk of parents
+struct Cand {
+  Key128 key;
+  uint32_t hidden;
+  uint32_t parent_local;
+  uint16_t ordinal;
+  uint8_t act;
+};
+
+void expand_range(const Arena& cur, size_t lo, size_t hi, std::vector<Cand>& out, Arena& keep,
+                  std::string& err, size_t& err_parent, int& maxmsg) {
+  std::vector<State> succ;
+  std::vector<int> acts;
+  succ.reserve(128);
+  SuccCollect em;
+  em.out = &succ;
+  em.acts = &acts;
+  State s;
+  for (size_t k = lo; k < hi; k++) {
+    cur.get(k, s);
+    maxmsg = std::max(maxmsg, (int)s.nmsg);
+    succ.clear();
+    acts.clear();
+    try {
+      Next(s, em);
+    } catch (EvalError& e) {
+      err = e.what();
+      err_parent = k;
+      return;
+    }
+    for (size_t q = 0; q < succ.size(); q++) {
+      Ser o;
+      canonical(succ[q], o);
+      Cand c;
+      c.key = hash_ser(o);
+      c.hidden = hidden_of(succ[q]);
+      c.parent_local = (uint32_t)k;
+      c.ordinal = (uint16_t)q;
+      c.act = (uint8_t)acts[q];
+      out.push_back(c);
+      keep.push(succ[q]);
+    }
+  }
+}
+
+void Checker::run() {
+  auto t0 = std::chrono::steady_clock::now();
+  auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+  Arena cur, nxt;
+  State init = Init();
+  st.generated = 1;
+  {
+    Ser o;
+    canonical(init, o);
+    fps.insert(hash_ser(o), 1, hidden_of(init));
+    if (fpdump) { Key128 k = hash_ser(o); fwrite(&k, sizeof k, 1, fpdump); }
+  }
+  parent.push_back(UINT64_MAX);
+  ordinal.push_back(0);
+  actid.push_back(255);
+  cur.push(init);
+  st.levels.push_back({1, 1});
+  st.depth = 1;
+  try {
+    if (const char* bad = check_invariants(init)) { st.status = "violation"; st.violated = bad; bad_index = 0; }
+  } catch (EvalError& e) { st.status = "error"; st.error = e.what(); bad_index = 0; }
+  uint64_t base = 0;  // global index of cur[0]
+  uint32_t level = 1;
+  const int T = std::max(1, threads);
+  const size_t CHUNK = 8192 * (size_t)T;
+  std::vector<std::vector<Cand>> cands(T);
+  std::vector<Arena> keeps(T);
+  while (st.status == "ok" && cur.size() > 0) {
+    size_t F = cur.size();
+    nxt.clear();
+    uint64_t gen_lvl = 0;
+    bool stop = false;
+    for (size_t c0 = 0; c0 < F && !stop; c0 += CHUNK) {
+      size_t c1 = std::min(F, c0 + CHUNK);
+      std::vector<std::string> errs(T);
+      std::vector<size_t> errp(T, 0);
+      std::vector<int> mm(T, 0);
+      std::vector<std::thread> th;
+      for (int w = 0; w < T; w++) {
+        size_t lo = c0 + (c1 - c0) * w / T, hi = c0 + (c1 - c0) * (w + 1) / T;
+        cands[w].clear();
+        keeps[w].clear();
+        if (T == 1) expand_range(cur, lo, hi, cands[w], keeps[w], errs[w], errp[w], mm[w]);
+        else th.emplace_back([&, w, lo, hi]() { expand_range(cur, lo, hi, cands[w], keeps[w], errs[w], errp[w], mm[w]); });
+      }
+      for (auto& x : th) x.join();
+      for (int w = 0; w < T; w++) st.max_msgs = std::max(st.max_msgs, mm[w]);
+      // sequential first-wins insertion in (parent, ordinal) order
+      for (int w = 0; w < T && !stop; w++) {
+        for (size_t q = 0; q < cands[w].size() && !stop; q++) {
+          const Cand& c = cands[w][q];
+          if (!errs[w].empty() && c.parent_local >= errp[w]) break;
+          gen_lvl++;
+          st.generated++;
+          st.act[c.act]++;
+          Slot* old = fps.insert(c.key, level + 1, c.hidden);
+          if (old) {
+            if (old->hidden != c.hidden) {
+              if (old->level == level + 1) st.hidden_same++;
+              else st.hidden_cross++;
+            }
+            continue;
+          }
+          if (fpdump) fwrite(&c.key, sizeof c.key, 1, fpdump);
+          State t;
+          keeps[w].get(q, t);
+          nxt.push(t);
+          parent.push_back(base + c.parent_local);
+          ordinal.push_back(c.ordinal);
+          actid.push_back(c.act);
+          try {
+            if (const char* bad = check_invariants(t)) {
+              st.status = "violation"; st.violated = bad; bad_index = (int64_t)parent.size() - 1; stop = true;
+            }
+          } catch (EvalError& e) {
+            st.status = "error"; st.error = std::string("invariant: ") + e.what();
+            bad_index = (int64_t)parent.size() - 1; stop = true;
+          }
+        }
+        if (!stop && !errs[w].empty()) {
+          st.status = "error";
+          st.error = errs[w];
+          bad_index = (int64_t)(base + errp[w]);
+          stop = true;
+        }
+      }
+    }
+    if (nxt.size() > 0 || gen_lvl > 0) st.levels.push_back({gen_lvl, nxt.size()});
+    if (nxt.size() > 0) st.depth++;
+    base += F;
+    level++;
+    std::swap(cur, nxt);
+    if (st.status != "ok") { st.left = cur.size(); break; }
+    if ((max_distinct && fps.count >= max_distinct) || (max_seconds > 0 && elapsed() > max_seconds)) {
+      st.status = "truncated";
+      st.left = cur.size();
+      break;
+    }
+  }
+  st.distinct = fps.count;
+  st.seconds = elapsed();
+}
+
+// -------------------------------------------------------------- trace / JSON
+std::string state_json(const State& s) {
+  std::string o = "{";
+  char buf[256];
+  auto arr = [&](const char* name, const int8_t* a, int n) {
+    o += std::string("\"") + name + "\":[";
+    for (int i = 0; i < n; i++) { snprintf(buf, sizeof buf, "%s%d", i ? "," : "", a[i]); o += buf; }
+    o += "],";
+  };
+  arr("currentTerm", s.term, C.N);
+  arr("state", s.st, C.N);
+  arr(C.spec == PULL ? "leader" : "votedFor", s.voted, C.N);
+  arr("commitIndex", s.commit, C.N);
+  if (C.spec == FSYNC) arr("fsyncIndex", s.fsync, C.N);
+  arr("acked", s.acked, C.V);
+  o += "\"votesGranted\":[";
+  for (int i = 0; i < C.N; i++) { snprintf(buf, sizeof buf, "%s%d", i ? "," : "", s.votes[i]); o += buf; }
+  o += "],\"log\":[";
+  for (int i = 0; i < C.N; i++) {
+    o += i ? ",[" : "[";
+    for (int x = 0; x < s.loglen[i]; x++) { snprintf(buf, sizeof buf, "%s[%d,%d]", x ? "," : "", s.log[i][x].term, s.log[i][x].value); o += buf; }
+    o += "]";
+  }
+  o += "],\"nextIndex\":[";
+  for (int i = 0; i < C.N; i++) {
+    o += i ? ",[" : "[";
+    for (int j = 0; j < C.N; j++) { snprintf(buf, sizeof buf, "%s%d", j ? "," : "", s.next[i][j]); o += buf; }
+    o += "]";
+  }
+  o += "],\"matchIndex\":[";
+  for (int i = 0; i < C.N; i++) {
+    o += i ? ",[" : "[";
+    for (int j = 0; j < C.N; j++) { snprintf(buf, sizeof buf, "%s%d", j ? "," : "", s.match[i][j]); o += buf; }
+    o += "]";
+  }
+  snprintf(buf, sizeof buf, "],\"pendingResponse\":[%d,%d,%d,%d,%d],\"electionCtr\":%d,\"restartCtr\":%d,\"messages\":[",
+           s.pending[0], s.pending[1], s.pending[2], s.pending[3], s.pending[4], s.electionCtr, s.restartCtr);
+  o += buf;
+  for (int k = 0; k < s.nmsg; k++) {
+    const Msg& m = s.msgs[k];
+    snprintf(buf, sizeof buf,
+             "%s{\"mtype\":\"%s\",\"mterm\":%d,\"msource\":%d,\"mdest\":%d,\"f\":[%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d],\"count\":%d}",
+             k ? "," : "", type_name(m.type), m.term, m.src, m.dst, m.lastLogTerm, m.lastLogIndex, m.voteGranted,
+             m.prevLogIndex, m.prevLogTerm, m.nent, m.eterm, m.evalue, m.commit, m.success, m.matchIndex, m.lciIndex,
+             m.lciTerm, m.count);
+    o += buf;
+  }
+  o += "]}";
+  return o;
+}
+
+struct NthCollect : Emitter {
+  int want, seen = 0;
+  State got;
+  int act = -1;
+  void emit(const State& t, int a) override {
+    if (seen++ == want) { got = t; act = a; }
+  }
+};
+
+std::vector<std::pair<int, State>> rebuild_trace(const Checker& ck, int64_t idx) {
+  std::vector<int64_t> chain;
+  for (int64_t x = idx; x >= 0 && (uint64_t)x != UINT64_MAX; x = (int64_t)(ck.parent[x] == UINT64_MAX ? -1 : (int64_t)ck.parent[x])) {
+    chain.push_back(x);
+    if (ck.parent[x] == UINT64_MAX) break;
+  }
+  std::reverse(chain.begin(), chain.end());
+  std::vector<std::pair<int, State>> out;
+  State s = Init();
+  out.push_back({-1, s});
+  for (size_t k = 1; k < chain.size(); k++) {
+    NthCollect nc;
+    nc.want = ck.ordinal[chain[k]];
+    Next(s, nc);
+    s = nc.got;
+    out.push_back({nc.act, s});
+  }
+  return out;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Checker ck;
+  bool print_trace = false;
+  std::string fpdump;
+  for (int a = 1; a < argc; a++) {
+    std::string k = argv[a];
+    auto val = [&]() { if (a + 1 >= argc) { fprintf(stderr, "missing value for %s\n", k.c_str()); exit(2); } return std::string(argv[++a]); };
+    if (k == "--spec") {
+      std::string v = val();
+      if (v == "Raft") C.spec = RAFT; else if (v == "FlexibleRaft") C.spec = FLEX;
+      else if (v == "RaftFsync") C.spec = FSYNC; else if (v == "PullRaft") C.spec = PULL;
+      else { fprintf(stderr, "unknown spec %s\n", v.c_str()); return 2; }
+    } else if (k == "--servers") C.N = std::stoi(val());
+    else if (k == "--values") C.V = std::stoi(val());
+    else if (k == "--max-elections") C.E = std::stoi(val());
+    else if (k == "--max-restarts") C.R = std::stoi(val());
+    else if (k == "--eq") C.EQ = std::stoi(val());
+    else if (k == "--rq") C.RQ = std::stoi(val());
+    else if (k == "--lfae") C.lfae = std::stoi(val()) != 0;
+    else if (k == "--lfiq") C.lfiq = std::stoi(val()) != 0;
+    else if (k == "--ffbr") C.ffbr = std::stoi(val()) != 0;
+    else if (k == "--inv") {
+      std::string v = val();
+      C.inv_order.clear();
+      size_t p = 0;
+      while (p <= v.size()) {
+        size_t q = v.find(',', p);
+        if (q == std::string::npos) q = v.size();
+        if (q > p) C.inv_order.push_back(v.substr(p, q - p));
+        p = q + 1;
+      }
+    } else if (k == "--max-distinct") ck.max_distinct = std::stoull(val());
+    else if (k == "--max-seconds") ck.max_seconds = std::stod(val());
+    else if (k == "--threads") ck.threads = std::stoi(val());
+    else if (k == "--trace") print_trace = true;
+    else if (k == "--dump-fps") fpdump = val();
+    else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
+  }
+  if (C.inv_order.empty() && argc > 0) C.inv_order = {"LeaderHasAllAckedValues", "NoLogDivergence"};
+  if (C.N < 1 || C.N > MAXN || C.V < 1 || C.V > MAXV) { fprintf(stderr, "bad N/V\n"); return 2; }
+  if (!fpdump.empty()) ck.fpdump = fopen(fpdump.c_str(), "wb");
+  ck.run();
+  if (ck.fpdump) fclose(ck.fpdump);
+  const Stats& s = ck.st;
+  printf("{\"generated\":%llu,\"distinct\":%llu,\"depth\":%d,\"left\":%llu,\"status\":\"%s\",",
+         (unsigned long long)s.generated, (unsigned long long)s.distinct, s.depth, (unsigned long long)s.left,
+         s.status.c_str());
+  printf("\"violated\":\"%s\",\"error\":\"%s\",\"hidden_same_level\":%llu,\"hidden_cross_level\":%llu,",
+         s.violated.c_str(), s.error.c_str(), (unsigned long long)s.hidden_same, (unsigned long long)s.hidden_cross);
+  printf("\"max_msgs\":%d,\"seconds\":%.3f,\"threads\":%d,\"levels\":[", s.max_msgs, s.seconds, ck.threads);
+  for (size_t k = 0; k < s.levels.size(); k++)
+    printf("%s[%llu,%llu]", k ? "," : "", (unsigned long long)s.levels[k].first, (unsigned long long)s.levels[k].second);
+  printf("],\"action_counts\":{");
+  bool first = true;
+  uint64_t merged[A_COUNT] = {0};
+  for (int a = 0; a < A_COUNT; a++) merged[a] = s.act[a];
+  merged[A_REQUESTVOTE] += merged[A_REQUESTVOTE_IJ];
+  for (int a = 0; a < A_COUNT; a++) {
+    if (a == A_REQUESTVOTE_IJ || !merged[a]) continue;
+    printf("%s\"%s\":%llu", first ? "" : ",", act_name(a), (unsigned long long)merged[a]);
+    first = false;
+  }
+  printf("}");
+  if (print_trace && ck.bad_index >= 0) {
+    auto tr = rebuild_trace(ck, ck.bad_index);
+    printf(",\"trace\":[");
+    for (size_t k = 0; k < tr.size(); k++)
+      printf("%s{\"action\":\"%s\",\"state\":%s}", k ? "," : "", tr[k].first < 0 ? "Initial predicate" : act_name(tr[k].first),
+             state_json(tr[k].second).c_str());
+    printf("]");
+  }
+  printf("}\n");
+  return 0;
+}

@@ -1,0 +1,18 @@
+"""Python oracle: literal restatements of the four Raft specs under TLC semantics.
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py may import this package, and only as the
+checker.  The product path (raft-tlaplus_amd/) never imports it.
+"""
+from .cfg import load_cfg, parse_cfg
+from .tlc import bfs, EvalError
+
+
+def make_spec(module, cfg):
+    from .raft import RaftSpec
+    from .variants import FlexibleRaftSpec, RaftFsyncSpec, PullRaftSpec
+    table = {"Raft": RaftSpec, "FlexibleRaft": FlexibleRaftSpec,
+             "RaftFsync": RaftFsyncSpec, "PullRaft": PullRaftSpec}
+    if module not in table:
+        raise ValueError("oracle: unsupported module %r" % module)
+    return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]))

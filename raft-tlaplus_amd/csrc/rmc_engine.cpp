@@ -1,0 +1,1107 @@
+// rmc_engine.cpp — librmc host side: cfg parsing and spec identification
+// (replacing TLC's SANY + cfg binding), the level-synchronous BFS driver over
+// the HIP kernels, trace reconstruction and the TLC-format report, behind the
+// C ABI of include/rmc.h.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <unordered_map>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+#include "../../include/rmc.h"
+#include "rmc_engine.h"
+
+using namespace rmc;
+
+static thread_local std::string g_last_error;
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + \
+                               " at " #x);                                          \
+    }                                                                               \
+  } while (0)
+
+// ------------------------------------------------------------------ cfg
+namespace {
+
+struct CfgVal {
+  enum Kind { INT, BOOL, MV, SET, STR, OP } kind = MV;
+  long long i = 0;
+  bool b = false;
+  std::string s;
+  std::vector<std::string> set;  // set of model values (names)
+};
+
+struct Cfg {
+  std::map<std::string, CfgVal> consts;
+  std::string init, next, spec, view, symmetry;
+  std::vector<std::string> invariants, properties, constraints;
+  int check_deadlock = -1;
+};
+
+std::string strip_comments(const std::string& t) {
+  std::string out;
+  int depth = 0;
+  for (size_t i = 0; i < t.size(); i++) {
+    if (t.compare(i, 2, "(*") == 0) { depth++; i++; continue; }
+    if (depth && t.compare(i, 2, "*)") == 0) { depth--; i++; continue; }
+    if (!depth) out += t[i];
+  }
+  std::string res, line;
+  std::istringstream is(out);
+  while (std::getline(is, line)) {
+    size_t c = line.find("\\*");
+    if (c != std::string::npos) line = line.substr(0, c);
+    res += line + "\n";
+  }
+  return res;
+}
+
+std::vector<std::string> tokenize(const std::string& t) {
+  std::vector<std::string> v;
+  size_t i = 0;
+  while (i < t.size()) {
+    char c = t[i];
+    if (isspace((unsigned char)c)) { i++; continue; }
+    if (c == '<' && i + 1 < t.size() && t[i + 1] == '-') { v.push_back("<-"); i += 2; continue; }
+    if (strchr("{}(),=", c)) { v.push_back(std::string(1, c)); i++; continue; }
+    if (c == '"') {
+      size_t j = t.find('"', i + 1);
+      if (j == std::string::npos) throw std::runtime_error("cfg: unterminated string");
+      v.push_back(t.substr(i, j - i + 1));
+      i = j + 1;
+      continue;
+    }
+    if (isalnum((unsigned char)c) || c == '_' || c == '-') {
+      size_t j = i;
+      while (j < t.size() && (isalnum((unsigned char)t[j]) || t[j] == '_' || t[j] == '!' || (j == i && t[j] == '-')))
+        j++;
+      v.push_back(t.substr(i, j - i));
+      i = j;
+      continue;
+    }
+    throw std::runtime_error(std::string("cfg: unexpected character '") + c + "'");
+  }
+  return v;
+}
+
+bool is_int(const std::string& s) {
+  if (s.empty()) return false;
+  size_t k = s[0] == '-' ? 1 : 0;
+  if (k == s.size()) return false;
+  for (; k < s.size(); k++)
+    if (!isdigit((unsigned char)s[k])) return false;
+  return true;
+}
+
+CfgVal parse_value(const std::vector<std::string>& tk, size_t& k) {
+  CfgVal v;
+  const std::string& t = tk.at(k);
+  if (t == "{") {
+    v.kind = CfgVal::SET;
+    k++;
+    while (tk.at(k) != "}") {
+      CfgVal e = parse_value(tk, k);
+      if (e.kind != CfgVal::MV) throw std::runtime_error("cfg: only sets of model values are supported");
+      v.set.push_back(e.s);
+      if (tk.at(k) == ",") k++;
+    }
+    k++;
+    return v;
+  }
+  k++;
+  if (t == "TRUE" || t == "FALSE") { v.kind = CfgVal::BOOL; v.b = t == "TRUE"; return v; }
+  if (is_int(t)) { v.kind = CfgVal::INT; v.i = std::stoll(t); return v; }
+  if (t[0] == '"') { v.kind = CfgVal::STR; v.s = t.substr(1, t.size() - 2); return v; }
+  v.kind = CfgVal::MV;  // bare identifier: an untyped model value (Raft.cfg:6-9 quirk)
+  v.s = t;
+  return v;
+}
+
+Cfg parse_cfg(const std::string& text) {
+  static const std::set<std::string> kw = {"CONSTANT", "CONSTANTS", "INIT", "NEXT", "SPECIFICATION", "INVARIANT",
+                                           "INVARIANTS", "PROPERTY", "PROPERTIES", "VIEW", "SYMMETRY", "CONSTRAINT",
+                                           "CONSTRAINTS", "ACTION_CONSTRAINT", "ACTION_CONSTRAINTS",
+                                           "CHECK_DEADLOCK", "POSTCONDITION", "ALIAS"};
+  Cfg c;
+  auto tk = tokenize(strip_comments(text));
+  std::string sec;
+  size_t k = 0;
+  while (k < tk.size()) {
+    const std::string t = tk[k];
+    if (kw.count(t)) {
+      sec = t;
+      k++;
+      if (sec == "INIT") c.init = tk.at(k++);
+      else if (sec == "NEXT") c.next = tk.at(k++);
+      else if (sec == "SPECIFICATION") c.spec = tk.at(k++);
+      else if (sec == "VIEW") c.view = tk.at(k++);
+      else if (sec == "SYMMETRY") c.symmetry = tk.at(k++);
+      else if (sec == "ALIAS") k++;
+      else if (sec == "CHECK_DEADLOCK") { CfgVal v = parse_value(tk, k); c.check_deadlock = v.b; }
+      continue;
+    }
+    if (sec == "CONSTANT" || sec == "CONSTANTS") {
+      if (k + 1 >= tk.size()) throw std::runtime_error("cfg: dangling constant " + t);
+      if (tk[k + 1] == "=") {
+        k += 2;
+        c.consts[t] = parse_value(tk, k);
+      } else if (tk[k + 1] == "<-") {
+        CfgVal v;
+        v.kind = CfgVal::OP;
+        v.s = tk.at(k + 2);
+        c.consts[t] = v;
+        k += 3;
+      } else {
+        throw std::runtime_error("cfg: bad constant assignment near " + t);
+      }
+      continue;
+    }
+    if (sec == "INVARIANT" || sec == "INVARIANTS") c.invariants.push_back(t);
+    else if (sec == "PROPERTY" || sec == "PROPERTIES") c.properties.push_back(t);
+    else if (sec.find("CONSTRAINT") != std::string::npos) c.constraints.push_back(t);
+    else throw std::runtime_error("cfg: token '" + t + "' outside any section");
+    k++;
+  }
+  return c;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- model
+struct rmc_model {
+  std::string module, tla_text;
+  Model M;
+  int fp_aux = 0;  // reserved: no VIEW -> aux vars would join the fingerprint
+  std::vector<std::string> server_names, value_names, inv_names;
+  std::vector<std::string> var_order;
+  // results of the last check
+  std::vector<std::pair<unsigned long long, unsigned long long>> levels;
+  std::vector<std::vector<uint32_t>> trace_states;
+  std::vector<std::string> trace_actions;
+  uint32_t kmax_user = 0;
+};
+
+namespace {
+
+int spec_of_module(const std::string& m) {
+  if (m == "Raft") return RAFT;
+  if (m == "FlexibleRaft") return FLEX;
+  if (m == "RaftFsync") return FSYNC;
+  if (m == "PullRaft") return PULL;
+  return -1;
+}
+
+const char* act_label(int a) {
+  static const char* n[] = {"Restart", "RequestVote", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
+                            "AdvanceCommitIndex", "AppendEntries", "AdvanceFsyncIndex", "UpdateTerm",
+                            "HandleRequestVoteRequest", "HandleRequestVoteResponse", "RejectAppendEntriesRequest",
+                            "AcceptAppendEntriesRequest", "HandleAppendEntriesResponse", "RejectPullEntriesRequest",
+                            "AcceptPullEntriesRequest", "LearnOfLeader", "SendPullEntriesRequest",
+                            "HandleSuccessPullEntriesResponse", "HandleFailPullEntriesResponse"};
+  return (a >= 0 && a < A_NUM) ? n[a] : "?";
+}
+
+void build_actions(Model& M) {
+  struct E { int id, kind; };
+  std::vector<E> t;
+  switch (M.spec) {
+    case RAFT: case FLEX:  // Raft.tla:527-539; FlexibleRaft.tla:488-500
+      t = {{A_RESTART, K_I}, {A_REQUESTVOTE, K_I}, {A_BECOMELEADER, K_I}, {A_CLIENT, K_IV}, {A_ADVCOMMIT, K_I},
+           {A_APPENDENTRIES, K_IJ}, {A_UPDATETERM, K_MSG}, {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG},
+           {A_REJAE, K_MSG}, {A_ACCAE, K_MSG}, {A_HAERESP, K_MSG}};
+      break;
+    case FSYNC:  // RaftFsync.tla:522-536
+      t = {{A_RESTART, K_I}, {A_TIMEOUT, K_I}, {A_RVIJ, K_IJ}, {A_BECOMELEADER, K_I}, {A_CLIENT, K_IV},
+           {A_ADVCOMMIT, K_I}, {A_APPENDENTRIES, K_IJ}, {A_ADVFSYNC, K_I}, {A_UPDATETERM, K_MSG},
+           {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG}, {A_REJAE, K_MSG}, {A_ACCAE, K_MSG}, {A_HAERESP, K_MSG}};
+      break;
+    case PULL:  // PullRaft.tla:542-558
+      t = {{A_RESTART, K_I}, {A_UPDATETERM, K_MSG}, {A_REQUESTVOTE, K_I}, {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG},
+           {A_BECOMELEADER, K_I}, {A_CLIENT, K_IV}, {A_REJPULL, K_MSG}, {A_ACCPULL, K_MSG}, {A_LEARN, K_MSG},
+           {A_SENDPULL, K_IJ}, {A_HSUCC, K_MSG}, {A_HFAIL, K_MSG}};
+      break;
+  }
+  M.nact = (int)t.size();
+  int off = 0, nf = 0;
+  for (int a = 0; a < A_NUM; a++) M.msg_act_slot[a] = 0;
+  for (int s = 0; s < M.nact; s++) {
+    M.act_id[s] = t[s].id;
+    M.act_kind[s] = t[s].kind;
+    M.act_off[s] = off;
+    int size = t[s].kind == K_I ? M.N : t[s].kind == K_IV ? M.N * M.V : t[s].kind == K_IJ ? M.N * M.N : M.kmax;
+    if (t[s].kind == K_MSG) M.msg_act_slot[t[s].id] = s;
+    else
+      for (int x = 0; x < size; x++) {
+        if (nf >= MAXFIXED) throw std::runtime_error("too many fixed bindings");
+        M.fb_act[nf] = (uint8_t)s;
+        M.fb_x[nf] = (uint8_t)x;
+        nf++;
+      }
+    off += size;
+  }
+  M.nfixed = nf;
+  M.ordinal_limit = off;
+  if (off >= 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");
+}
+
+void build_perms(Model& M, bool symmetry) {
+  std::vector<int> p(M.N);
+  for (int i = 0; i < M.N; i++) p[i] = i;
+  M.nperm = 0;
+  do {
+    uint32_t P = 0;
+    for (int j = 0; j < M.N; j++) P |= (uint32_t)p[j] << (3 * j);
+    M.perm[M.nperm++] = P;
+    if (!symmetry) break;
+  } while (std::next_permutation(p.begin(), p.end()));
+}
+
+rmc_model* load_model(const std::string& module, const std::string& cfg_text, const std::string& tla_text) {
+  auto m = new rmc_model();
+  try {
+    m->module = module;
+    m->tla_text = tla_text;
+    int spec = spec_of_module(module);
+    if (spec < 0)
+      throw std::runtime_error("unsupported module '" + module +
+                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft)");
+    if (!tla_text.empty() && tla_text.find("MODULE " + module) == std::string::npos)
+      throw std::runtime_error("the .tla file does not declare MODULE " + module);
+    Cfg c = parse_cfg(cfg_text);
+    if (!c.spec.empty()) throw std::runtime_error("SPECIFICATION is not supported; use INIT Init / NEXT Next");
+    if (c.init != "Init" || c.next != "Next")
+      throw std::runtime_error("cfg must bind INIT Init and NEXT Next (got '" + c.init + "', '" + c.next + "')");
+    if (!c.properties.empty()) throw std::runtime_error("PROPERTY checking (liveness) is not supported");
+    if (!c.constraints.empty()) throw std::runtime_error("CONSTRAINT is not supported");
+    if (c.view != "view") throw std::runtime_error("cfg must set VIEW view (the reference cfgs do)");
+    if (!c.symmetry.empty() && c.symmetry != "symmServers")
+      throw std::runtime_error("only SYMMETRY symmServers is supported");
+    auto need = [&](const std::string& n) -> CfgVal& {
+      auto it = c.consts.find(n);
+      if (it == c.consts.end()) throw std::runtime_error("cfg: constant " + n + " is not assigned");
+      return it->second;
+    };
+    Model& M = m->M;
+    memset(&M, 0, sizeof M);
+    M.spec = spec;
+    CfgVal& S = need("Server");
+    CfgVal& Vv = need("Value");
+    if (S.kind != CfgVal::SET || Vv.kind != CfgVal::SET) throw std::runtime_error("Server and Value must be sets");
+    m->server_names = S.set;
+    m->value_names = Vv.set;
+    std::sort(m->server_names.begin(), m->server_names.end());  // TLC orders model values by name
+    std::sort(m->value_names.begin(), m->value_names.end());
+    M.N = (int)S.set.size();
+    M.V = (int)Vv.set.size();
+    if (M.N < 2 || M.N > 5) throw std::runtime_error("|Server| must be 2..5");
+    if (M.V < 1 || M.V > MAXV) throw std::runtime_error("|Value| must be 1..4");
+    auto geti = [&](const char* n) {
+      CfgVal& v = need(n);
+      if (v.kind != CfgVal::INT) throw std::runtime_error(std::string("constant ") + n + " must be an integer");
+      return (int)v.i;
+    };
+    auto getb = [&](const char* n) {
+      CfgVal& v = need(n);
+      if (v.kind != CfgVal::BOOL) throw std::runtime_error(std::string("constant ") + n + " must be TRUE/FALSE");
+      return (int)v.b;
+    };
+    M.E = geti("MaxElections");
+    M.R = geti("MaxRestarts");
+    if (M.E < 0 || M.E > 14 || M.R < 0 || M.R > 15) throw std::runtime_error("MaxElections/MaxRestarts out of range");
+    if (spec == FLEX) { M.EQ = geti("ElectionQuorumSize"); M.RQ = geti("ReplicationQuorumSize"); }
+    if (spec == FSYNC) {
+      M.lfae = getb("LeaderFsyncBeforeAppendEntries");
+      M.lfiq = getb("LeaderFsyncBeforeIncludeInQuorum");
+      M.ffbr = getb("FollowerFsyncBeforeReply");
+    }
+    M.ninv = 0;
+    for (auto& n : c.invariants) {
+      int id = n == "LeaderHasAllAckedValues" ? 0 : n == "NoLogDivergence" ? 1
+                                               : n == "CommittedEntriesReachMajority" ? 2
+                                               : n == "TestInv" ? -2 : -1;
+      if (id == -2) continue;  // TestInv == TRUE
+      if (id < 0) throw std::runtime_error("unsupported invariant " + n);
+      if (M.ninv >= 3) throw std::runtime_error("too many invariants");
+      M.inv[M.ninv++] = id;
+      m->inv_names.push_back(n);
+    }
+    build_perms(M, !c.symmetry.empty());
+    switch (spec) {
+      case RAFT:
+        m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "votedFor", "log",
+                        "commitIndex", "votesGranted", "nextIndex", "matchIndex", "pendingResponse"};
+        break;
+      case FLEX:
+        m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "votedFor", "log",
+                        "commitIndex", "votesGranted", "nextIndex", "matchIndex"};
+        break;
+      case FSYNC:
+        m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "votedFor", "log",
+                        "commitIndex", "fsyncIndex", "votesGranted", "nextIndex", "matchIndex"};
+        break;
+      case PULL:
+        m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "leader", "log",
+                        "commitIndex", "votesGranted", "matchIndex"};
+        break;
+    }
+  } catch (std::exception& e) {
+    delete m;
+    throw;
+  }
+  return m;
+}
+
+void finalize_model(rmc_model* m, uint32_t kmax) {
+  Model& M = m->M;
+  M.kmax = (int)kmax;
+  M.words = 1 + 4 * M.N + M.kmax;
+  build_actions(M);
+}
+
+uint32_t default_kmax(const Model& M) {
+  int k = 8 * M.N + 8 * M.V + 4 * M.E;
+  k = ((k + 7) / 8) * 8;
+  return (uint32_t)std::min(std::max(k, 24), 120);
+}
+
+std::vector<uint32_t> init_state(const Model& M) {
+  std::vector<uint32_t> S(M.words, 0u);
+  S[0] = 0;  // nmsg 0, counters 0, acked all Nil (Raft.tla:209-213)
+  for (int i = 0; i < M.N; i++) {
+    uint32_t a = 1u | (FOLLOWER << 4) | ((uint32_t)NILS << 6);  // currentTerm 1, Follower, votedFor Nil
+    S[1 + 4 * i] = a;
+    S[2 + 4 * i] = 0;
+    S[3 + 4 * i] = M.spec == PULL ? 0u : all_rows(M.N, 1);  // nextIndex = 1
+    S[4 + 4 * i] = 0;                                        // matchIndex = 0
+  }
+  return S;
+}
+
+// ------------------------------------------------------------ formatting
+std::string fmt_state(const rmc_model* m, const uint32_t* S) {
+  const Model& M = m->M;
+  auto sv = [&](int i) { return i == NILS ? std::string("Nil") : m->server_names.at(i); };
+  auto fn = [&](auto val) {
+    std::string o = "(";
+    for (int i = 0; i < M.N; i++) o += (i ? " @@ " : "") + m->server_names[i] + " :> " + val(i);
+    return o + ")";
+  };
+  auto entry = [&](int t, int v) {
+    return "[term |-> " + std::to_string(t) + ", value |-> " + m->value_names.at(v) + "]";
+  };
+  std::string o;
+  int nm = h_nmsg(S[0]);
+  for (auto& var : m->var_order) {
+    std::string val;
+    if (var == "messages") {
+      if (nm == 0) val = "<< >>";
+      else {
+        val = "(";
+        for (int k = 0; k < nm; k++) {
+          MsgF f = M.spec == PULL ? msg_decode<PULL>(S[1 + 4 * M.N + k]) : msg_decode<RAFT>(S[1 + 4 * M.N + k]);
+          std::string r;
+          auto B = [](int x) { return std::string(x ? "TRUE" : "FALSE"); };
+          auto ents = [&](int n, int t, int v) { return n ? "<<" + entry(t, v) + ">>" : std::string("<<>>"); };
+          switch (f.type) {
+            case RVREQ:
+              r = "[mdest |-> " + sv(f.dst) + ", mlastLogIndex |-> " + std::to_string(f.lli) + ", mlastLogTerm |-> " +
+                  std::to_string(f.llt) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                  ", mtype |-> RequestVoteRequest]";
+              break;
+            case PEREQ:
+              r = "[mdest |-> " + sv(f.dst) + ", mlastLogIndex |-> " + std::to_string(f.lli) + ", mlastLogTerm |-> " +
+                  std::to_string(f.llt) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                  ", mtype |-> PullEntriesRequest]";
+              break;
+            case RVRESP:
+              r = "[mdest |-> " + sv(f.dst) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                  ", mtype |-> RequestVoteResponse, mvoteGranted |-> " + B(f.granted) + "]";
+              break;
+            case AEREQ:
+              r = "[mcommitIndex |-> " + std::to_string(f.commit) + ", mdest |-> " + sv(f.dst) + ", mentries |-> " +
+                  ents(f.nent, f.eterm, f.evalue) + ", mprevLogIndex |-> " + std::to_string(f.pli) +
+                  ", mprevLogTerm |-> " + std::to_string(f.plt) + ", msource |-> " + sv(f.src) + ", mterm |-> " +
+                  std::to_string(f.term) + ", mtype |-> AppendEntriesRequest]";
+              break;
+            case AERESP:
+              r = "[mdest |-> " + sv(f.dst) + ", mmatchIndex |-> " + std::to_string(f.midx) + ", msource |-> " +
+                  sv(f.src) + ", msuccess |-> " + B(f.success) + ", mterm |-> " + std::to_string(f.term) +
+                  ", mtype |-> AppendEntriesResponse]";
+              break;
+            case LNREQ:
+              r = "[mdest |-> " + sv(f.dst) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                  ", mtype |-> LeaderNotifyRequest]";
+              break;
+            case PERESP:
+              if (f.success)
+                r = "[mcommitIndex |-> " + std::to_string(f.commit) + ", mdest |-> " + sv(f.dst) + ", mentries |-> " +
+                    ents(f.nent, f.eterm, f.evalue) + ", msource |-> " + sv(f.src) + ", msuccess |-> TRUE, mterm |-> " +
+                    std::to_string(f.term) + ", mtype |-> PullEntriesResponse]";
+              else
+                r = "[mdest |-> " + sv(f.dst) + ", mlastCommonEntry |-> [index |-> " + std::to_string(f.lci) +
+                    ", term |-> " + std::to_string(f.lct) + "], msource |-> " + sv(f.src) +
+                    ", msuccess |-> FALSE, mterm |-> " + std::to_string(f.term) + ", mtype |-> PullEntriesResponse]";
+              break;
+          }
+          val += (k ? " @@\n  " : "") + r + " :> " + std::to_string(f.count);
+        }
+        val += ")";
+      }
+    } else if (var == "acked") {
+      val = "(";
+      for (int v = 0; v < M.V; v++) {
+        int a = h_acked(S[0], v);
+        val += (v ? " @@ " : "") + m->value_names[v] + " :> " + (a == 0 ? "Nil" : a == 1 ? "FALSE" : "TRUE");
+      }
+      val += ")";
+    } else if (var == "electionCtr") val = std::to_string(h_ectr(S[0]));
+    else if (var == "restartCtr") val = std::to_string(h_rctr(S[0]));
+    else if (var == "currentTerm") val = fn([&](int i) { return std::to_string(a_term(S[1 + 4 * i])); });
+    else if (var == "state")
+      val = fn([&](int i) {
+        int st = a_st(S[1 + 4 * i]);
+        return std::string(st == FOLLOWER ? "Follower" : st == CANDIDATE ? "Candidate" : "Leader");
+      });
+    else if (var == "votedFor" || var == "leader") val = fn([&](int i) { return sv(a_voted(S[1 + 4 * i])); });
+    else if (var == "log")
+      val = fn([&](int i) {
+        uint32_t a = S[1 + 4 * i], b = S[2 + 4 * i];
+        std::string o2 = "<<";
+        for (int x = 0; x < a_len(a); x++) o2 += (x ? ", " : "") + entry(e_term(b, x), e_value(b, x));
+        return o2 + ">>";
+      });
+    else if (var == "commitIndex") val = fn([&](int i) { return std::to_string(a_commit(S[1 + 4 * i])); });
+    else if (var == "fsyncIndex") val = fn([&](int i) { return std::to_string(a_fsync(S[1 + 4 * i])); });
+    else if (var == "votesGranted")
+      val = fn([&](int i) {
+        int vg = a_votes(S[1 + 4 * i]);
+        std::string o2 = "{";
+        bool first = true;
+        for (int j = 0; j < M.N; j++)
+          if ((vg >> j) & 1) { o2 += (first ? "" : ", ") + m->server_names[j]; first = false; }
+        return o2 + "}";
+      });
+    else if (var == "nextIndex" || var == "matchIndex" || var == "pendingResponse")
+      val = fn([&](int i) {
+        std::string o2 = "(";
+        for (int j = 0; j < M.N; j++) {
+          std::string x;
+          if (var == "nextIndex") x = std::to_string(row_get(S[3 + 4 * i], j));
+          else if (var == "matchIndex") x = std::to_string(row_get(S[4 + 4 * i], j));
+          else x = ((a_pending(S[1 + 4 * i]) >> j) & 1) ? "TRUE" : "FALSE";
+          o2 += (j ? " @@ " : "") + m->server_names[j] + " :> " + x;
+        }
+        return o2 + ")";
+      });
+    o += "/\\ " + var + " = " + val + "\n";
+  }
+  return o;
+}
+
+std::string binding_label(const rmc_model* m, int b, int act) {
+  const Model& M = m->M;
+  std::string name = act_label(act);
+  if (b < M.nfixed) {
+    int slot = M.fb_act[b], x = M.fb_x[b];
+    int kind = M.act_kind[slot];
+    int i = x % M.N, jv = x / M.N;
+    if (kind == K_I) return name + "(" + m->server_names[i] + ")";
+    if (kind == K_IV) return name + "(" + m->server_names[i] + ", " + m->value_names[jv] + ")";
+    return name + "(" + m->server_names[i] + ", " + m->server_names[jv] + ")";
+  }
+  return name;
+}
+
+// line of an operator definition in the module text, for TLC-style labels
+std::string def_location(const rmc_model* m, const std::string& op) {
+  if (m->tla_text.empty()) return "";
+  std::istringstream is(m->tla_text);
+  std::string line;
+  int ln = 0;
+  while (std::getline(is, line)) {
+    ln++;
+    if (line.compare(0, op.size(), op) == 0) {
+      size_t p = op.size();
+      while (p < line.size() && line[p] != '=' && line[p] != '\n') p++;
+      if (line.find("==", op.size()) != std::string::npos) return " line " + std::to_string(ln);
+    }
+  }
+  return "";
+}
+
+}  // namespace
+
+// ----------------------------------------------------------- BFS driver
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void alloc(size_t b) {
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    bytes = b;
+    if (b) HIPCHK(hipMalloc(&p, b));
+  }
+  void grow_copy(size_t b, size_t keep) {
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, b));
+    if (p && keep) HIPCHK(hipMemcpy(q, p, keep, hipMemcpyDeviceToDevice));
+    if (p) HIPCHK(hipFree(p));
+    p = q;
+    bytes = b;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+struct EventTimer {
+  hipEvent_t a, b;
+  EventTimer() { HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b)); }
+  ~EventTimer() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
+};
+
+int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
+  auto t0 = std::chrono::steady_clock::now();
+  Model& M = m->M;
+  if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
+  if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("only 64-bit fingerprints are supported");
+  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : default_kmax(M));
+  if (kmax > 120) kmax = 120;
+  finalize_model(m, kmax);
+  HIPCHK(upload_model(M));
+  hipStream_t stream;
+  HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  const size_t W = (size_t)M.words;
+  res->state_bytes = (uint32_t)(W * 4);
+
+  // ---- sizing
+  size_t freeb = 0, totalb = 0;
+  HIPCHK(hipMemGetInfo(&freeb, &totalb));
+  unsigned long long slots = opt->hash_slots;
+  if (!slots) {
+    slots = 1ULL << 26;  // 1 GiB table; grown on demand
+  }
+  if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
+  unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : (1ULL << 22);
+  const int maxsucc = M.nfixed + M.kmax;
+  unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 20);
+  const unsigned long long cand_cap = chunk * (unsigned long long)std::min(maxsucc, 256);
+
+  DevBuf table, fa, fb, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp, trp, trb;
+  table.alloc(slots * 16);
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, table.bytes, stream));
+  fa.alloc(fcap * W * 4);
+  fb.alloc(fcap * W * 4);
+  cslot.alloc(cand_cap * 8);
+  cob.alloc(cand_cap * 4);
+  cwin.alloc(cand_cap);
+  poff.alloc(chunk * 4);
+  pn.alloc(chunk * 4);
+  pwin.alloc(chunk * 4);
+  ppos.alloc(chunk * 4);
+  counters.alloc(64);
+  stbuf.alloc(sizeof(DevStatus));
+  size_t stb = scan_temp_bytes(chunk);
+  scantmp.alloc(stb ? stb : 16);
+  unsigned long long trcap = fcap * 4;
+  trp.alloc(trcap * 8);
+  trb.alloc(trcap * 2);
+
+  DevStatus hst;
+  auto reset_status = [&]() {
+    hst.err_key = hst.inv_err_key = hst.viol_key = ~0ULL;
+    hst.cap_flags = 0;
+    hst.pad = 0;
+    HIPCHK(hipMemcpyAsync(stbuf.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
+  };
+  reset_status();
+
+  // ---- level 1: Init (Raft.tla:213-218)
+  std::vector<uint32_t> init = init_state(M);
+  HIPCHK(hipMemcpyAsync(fa.p, init.data(), W * 4, hipMemcpyHostToDevice, stream));
+  {
+    unsigned long long fp = host_fingerprint(M, init.data());
+    if (fp == ~0ULL) fp--;
+    unsigned long long slot = (fp ^ (fp >> 29)) & (slots - 1);
+    unsigned long long ent[2] = {fp, (1ULL << 48)};
+    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + 2 * slot, ent, 16, hipMemcpyHostToDevice, stream));
+    unsigned long long root = ~0ULL;
+    uint16_t zero = 0;
+    HIPCHK(hipMemcpyAsync(trp.p, &root, 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(trb.p, &zero, 2, hipMemcpyHostToDevice, stream));
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  m->levels.clear();
+  m->trace_states.clear();
+  m->trace_actions.clear();
+  unsigned long long generated = 1, distinct = 1, cur_n = 1, cur_base = 0;
+  unsigned depth = 1;
+  m->levels.push_back({1, 1});
+  int status = 0;
+  std::string message;
+  unsigned long long bad_state = ~0ULL;  // global index of the violating / erroring state, if materialized
+  unsigned long long bad_key = ~0ULL;
+  bool bad_is_parent_key = false;
+  {
+    int err = 0;
+    int bad = host_check_invariants(M, init.data(), &err);
+    if (err) { status = 2; message = "evaluation error in an invariant on the initial state"; bad_state = 0; }
+    else if (bad >= 0) { status = 1; snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str()); bad_state = 0; }
+  }
+  EventTimer te, tm, tz;
+  double expand_ms = 0, mark_ms = 0, mat_ms = 0;
+  unsigned long long expand_launches = 0;
+  uint32_t* cur = fa.as<uint32_t>();
+  uint32_t* nxt = fb.as<uint32_t>();
+  unsigned long long entries_hint = 1;
+  while (status == 0 && cur_n > 0) {
+    if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
+    unsigned level = depth + 1;
+    if (level >= 0xFFFF) throw std::runtime_error("too many levels");
+    unsigned long long next_n = 0, gen_lvl = 0;
+    for (unsigned long long c0 = 0; c0 < cur_n; c0 += chunk) {
+      unsigned long long n = std::min(chunk, cur_n - c0);
+      // grow the table before it passes 1/2 load (worst case: every candidate new)
+      if ((entries_hint + n * (unsigned long long)maxsucc) * 2 > slots) {
+        // rehash into a larger table on the host side: copy out, reinsert by kernel-free path
+        unsigned long long nslots = slots;
+        while ((entries_hint + n * (unsigned long long)maxsucc) * 2 > nslots) nslots <<= 1;
+        if (opt->hash_slots) throw std::runtime_error("fingerprint set full (raise hash_slots)");
+        DevBuf nt;
+        nt.alloc(nslots * 16);
+        HIPCHK(hipMemsetAsync(nt.p, 0xFF, nt.bytes, stream));
+        launch_rehash(table.as<unsigned long long>(), slots, nt.as<unsigned long long>(), nslots - 1,
+                      stbuf.as<DevStatus>(), stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(stream));
+        std::swap(table.p, nt.p);
+        std::swap(table.bytes, nt.bytes);
+        slots = nslots;
+      }
+      LevelArgs a;
+      memset(&a, 0, sizeof a);
+      a.frontier = cur + c0 * W;
+      a.nparents = n;
+      a.pbase = cur_base + c0;
+      a.level = level;
+      a.table = table.as<unsigned long long>();
+      a.mask = slots - 1;
+      a.cand_slot = cslot.as<unsigned long long>();
+      a.cand_ob = cob.as<uint32_t>();
+      a.cand_win = cwin.as<uint8_t>();
+      a.par_off = poff.as<uint32_t>();
+      a.par_n = pn.as<uint32_t>();
+      a.par_win = pwin.as<uint32_t>();
+      a.par_pos = ppos.as<uint32_t>();
+      a.counters = counters.as<unsigned long long>();
+      a.cand_cap = cand_cap;
+      a.st = stbuf.as<DevStatus>();
+      HIPCHK(hipMemsetAsync(counters.p, 0, 64, stream));
+      HIPCHK(hipEventRecord(te.a, stream));
+      launch_expand(M.spec, M.N, a, stream);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(te.b, stream));
+      launch_mark(a, stream);
+      HIPCHK(hipGetLastError());
+      launch_scan(scantmp.p, scantmp.bytes, a.par_win, a.par_pos, n, stream);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(tm.b, stream));
+      unsigned long long ncand = 0;
+      uint32_t lastpos = 0, lastwin = 0;
+      HIPCHK(hipMemcpyAsync(&ncand, counters.p, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&lastpos, a.par_pos + (n - 1), 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&lastwin, a.par_win + (n - 1), 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&hst, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
+      expand_ms += ms;
+      expand_launches++;
+      HIPCHK(hipEventElapsedTime(&ms, te.b, tm.b));
+      mark_ms += ms;
+      if (hst.cap_flags) {
+        int e = 0;
+        while (!((hst.cap_flags >> e) & 1)) e++;
+        if (e == E_CAP_MSG && !opt->msg_cap_K && kmax < 120) {
+          // the caller re-runs with a larger message capacity
+          m->kmax_user = std::min(120u, kmax * 2);
+          HIPCHK(hipStreamDestroy(stream));
+          return 1;
+        }
+        static const char* names[] = {"", "", "log longer than the packed layout (5 entries)",
+                                      "message capacity msg_cap_K exceeded", "message multiplicity > 7",
+                                      "term > 15", "index field > 7", "successor buffer", "fingerprint set full",
+                                      "frontier capacity"};
+        status = 3;
+        message = std::string("capacity overflow: ") + names[e];
+        break;
+      }
+      unsigned long long W_chunk = (unsigned long long)lastpos + lastwin;
+      gen_lvl += ncand;
+      if (next_n + W_chunk > fcap) {
+        // grow both frontier buffers (keep what is already written)
+        unsigned long long nf = fcap;
+        while (next_n + W_chunk > nf) nf *= 2;
+        size_t cur_off_words = (size_t)(cur - (cur == fa.as<uint32_t>() ? fa.as<uint32_t>() : fb.as<uint32_t>()));
+        (void)cur_off_words;
+        bool cur_is_a = cur == fa.as<uint32_t>();
+        DevBuf& cb = cur_is_a ? fa : fb;
+        DevBuf& nb = cur_is_a ? fb : fa;
+        cb.grow_copy(nf * W * 4, cur_n * W * 4);
+        nb.grow_copy(nf * W * 4, next_n * W * 4);
+        cur = cb.as<uint32_t>();
+        nxt = nb.as<uint32_t>();
+        a.frontier = cur + c0 * W;
+        fcap = nf;
+      }
+      if (distinct + next_n + W_chunk > trcap) {
+        unsigned long long nt = trcap;
+        while (distinct + next_n + W_chunk > nt) nt *= 2;
+        trp.grow_copy(nt * 8, (distinct + next_n) * 8);
+        trb.grow_copy(nt * 2, (distinct + next_n) * 2);
+        trcap = nt;
+      }
+      a.out = nxt + next_n * W;
+      a.out_base_global = distinct + next_n;
+      a.tr_parent = trp.as<unsigned long long>();
+      a.tr_bind = trb.as<uint16_t>();
+      // positions from the scan are chunk-local; shift by next_n via out pointer
+      HIPCHK(hipEventRecord(tz.a, stream));
+      launch_materialize(M.spec, M.N, a, stream);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(tz.b, stream));
+      HIPCHK(hipMemcpyAsync(&hst, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      HIPCHK(hipEventElapsedTime(&ms, tz.a, tz.b));
+      mat_ms += ms;
+      next_n += W_chunk;
+      entries_hint += W_chunk;
+      if (hst.cap_flags) {
+        status = 3;
+        message = "capacity overflow while materializing";
+        break;
+      }
+      if (hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL) break;
+    }
+    generated += gen_lvl;
+    distinct += next_n;
+    if (next_n || gen_lvl) m->levels.push_back({gen_lvl, next_n});
+    if (next_n) depth++;
+    if (status) break;
+    if (hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL) {
+      // TLC stops at the first problem in its exploration order
+      unsigned long long k_err = std::min(hst.err_key, hst.inv_err_key);
+      if (k_err < hst.viol_key) {
+        status = 2;
+        bad_key = k_err;
+        bad_is_parent_key = hst.err_key <= hst.inv_err_key;
+        message = bad_is_parent_key ? "evaluation error in the next-state relation (a sequence applied outside its domain)"
+                                    : "evaluation error while checking an invariant";
+      } else {
+        status = 1;
+        bad_key = hst.viol_key;
+      }
+      cur_base += cur_n;
+      cur_n = next_n;
+      std::swap(cur, nxt);
+      break;
+    }
+    cur_base += cur_n;
+    cur_n = next_n;
+    std::swap(cur, nxt);
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated\n", depth, next_n, distinct, generated);
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  // ---- trace reconstruction: walk parent records, replay bindings on the host
+  if (status == 1 || status == 2) {
+    std::vector<std::pair<unsigned long long, int>> chain;  // (global state index or parent, binding)
+    unsigned long long parent_g = ~0ULL;
+    int last_b = -1;
+    if (bad_key != ~0ULL) {
+      parent_g = bad_key >> 20;
+      last_b = (int)(bad_key & 0x3FF);
+    } else if (bad_state != ~0ULL) {
+      parent_g = bad_state;
+    }
+    std::vector<int> binds;
+    unsigned long long g = parent_g;
+    while (g != ~0ULL && g != 0) {
+      unsigned long long pp;
+      uint16_t bb;
+      HIPCHK(hipMemcpy(&pp, trp.as<unsigned long long>() + g, 8, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&bb, trb.as<uint16_t>() + g, 2, hipMemcpyDeviceToHost));
+      binds.push_back(bb);
+      g = pp;
+    }
+    std::reverse(binds.begin(), binds.end());
+    std::vector<uint32_t> s = init;
+    m->trace_states.push_back(s);
+    m->trace_actions.push_back("Initial predicate");
+    auto step = [&](int b) {
+      std::vector<uint32_t> t(W, 0);
+      int ordv = 0, act = -1, err = 0;
+      int en = host_eval_apply(M, s.data(), b, t.data(), &ordv, &act, &err);
+      if (en != 1) throw std::runtime_error("trace replay: binding not enabled");
+      std::string lbl = binding_label(m, b, act);
+      if (err) return lbl;  // the erroring step: no successor state
+      s = t;
+      m->trace_states.push_back(s);
+      m->trace_actions.push_back(lbl);
+      return std::string();
+    };
+    for (int b : binds) step(b);
+    if (last_b >= 0) {
+      std::string e = step(last_b);
+      if (!e.empty()) message += " in action " + e;
+    }
+    if (status == 1 && !m->trace_states.empty()) {
+      int err = 0;
+      int bad = host_check_invariants(M, m->trace_states.back().data(), &err);
+      if (bad >= 0) snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str());
+    }
+  }
+  HIPCHK(hipStreamDestroy(stream));
+  res->generated = generated;
+  res->distinct = distinct;
+  res->left_on_queue = (status == 0) ? 0 : cur_n;
+  res->depth = depth;
+  res->status = status;
+  snprintf(res->message, sizeof res->message, "%s", message.c_str());
+  res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  res->expand_ms = expand_ms;
+  res->mark_ms = mark_ms;
+  res->materialize_ms = mat_ms;
+  res->expand_launches = expand_launches;
+  res->hash_capacity = slots;
+  res->max_msgs = 0;
+  return 0;
+}
+
+std::string read_file(const std::string& p, bool& ok) {
+  std::ifstream f(p);
+  if (!f) { ok = false; return ""; }
+  ok = true;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+void set_err(char* err, size_t len, const std::string& msg) {
+  g_last_error = msg;
+  if (err && len) snprintf(err, len, "%s", msg.c_str());
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char* rmc_version(void) { return "raftmc 0.1 (gfx950)"; }
+const char* rmc_last_error(void) { return g_last_error.c_str(); }
+
+void rmc_options_default(rmc_options* o) {
+  memset(o, 0, sizeof *o);
+  o->n_gpus = 1;
+  o->fp_bits = 64;
+  o->tlc_order = 1;
+}
+
+int rmc_model_load_text(const char* module, const char* cfg_text, rmc_model** out, char* err, size_t errlen) {
+  if (!module || !cfg_text || !out) { set_err(err, errlen, "null argument"); return -1; }
+  try {
+    *out = load_model(module, cfg_text, "");
+    return 0;
+  } catch (std::exception& e) {
+    set_err(err, errlen, e.what());
+    return -2;
+  }
+}
+
+int rmc_model_load(const char* tla_path, const char* cfg_path, rmc_model** out, char* err, size_t errlen) {
+  if (!tla_path || !out) { set_err(err, errlen, "null argument"); return -1; }
+  std::string tp = tla_path;
+  std::string base = tp.substr(tp.find_last_of('/') == std::string::npos ? 0 : tp.find_last_of('/') + 1);
+  std::string module = base.size() > 4 && base.substr(base.size() - 4) == ".tla" ? base.substr(0, base.size() - 4) : base;
+  bool ok = false;
+  std::string tla = read_file(tp, ok);
+  std::string cp = cfg_path ? std::string(cfg_path) : (tp.size() > 4 && tp.substr(tp.size() - 4) == ".tla" ? tp.substr(0, tp.size() - 4) : tp) + ".cfg";
+  bool cok = false;
+  std::string cfg = read_file(cp, cok);
+  if (!cok) { set_err(err, errlen, "cannot read cfg file " + cp); return -3; }
+  try {
+    *out = load_model(module, cfg, ok ? tla : "");
+    return 0;
+  } catch (std::exception& e) {
+    set_err(err, errlen, e.what());
+    return -2;
+  }
+}
+
+int rmc_check(rmc_model* m, const rmc_options* o, rmc_result* out) {
+  if (!m || !out) { g_last_error = "null argument"; return -1; }
+  rmc_options def;
+  rmc_options_default(&def);
+  if (!o) o = &def;
+  memset(out, 0, sizeof *out);
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+      g_last_error = "no HIP device available: the raftmc GPU path requires an MI355X (gfx950)";
+      return -4;
+    }
+    m->kmax_user = 0;
+    int rc;
+    while ((rc = check_impl(m, o, out)) == 1) memset(out, 0, sizeof *out);
+    return rc;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -5;
+  }
+}
+
+int rmc_trace_len(const rmc_model* m) { return m ? (int)m->trace_states.size() : -1; }
+
+int rmc_trace_state(const rmc_model* m, int k, char* buf, size_t len) {
+  if (!m || k < 0 || k >= (int)m->trace_states.size()) return -1;
+  std::string s = fmt_state(m, m->trace_states[k].data());
+  if (buf && len) snprintf(buf, len, "%s", s.c_str());
+  return (int)s.size();
+}
+
+int rmc_trace_action(const rmc_model* m, int k, char* buf, size_t len) {
+  if (!m || k < 0 || k >= (int)m->trace_actions.size()) return -1;
+  const std::string& s = m->trace_actions[k];
+  if (buf && len) snprintf(buf, len, "%s", s.c_str());
+  return (int)s.size();
+}
+
+int rmc_levels(const rmc_model* m, uint64_t* pairs, int cap) {
+  if (!m) return -1;
+  int n = (int)m->levels.size();
+  for (int k = 0; k < n && k < cap; k++) {
+    pairs[2 * k] = m->levels[k].first;
+    pairs[2 * k + 1] = m->levels[k].second;
+  }
+  return n;
+}
+
+int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t len) {
+  if (!m || !r) return -1;
+  std::string o;
+  char line[512];
+  if (r->status == 1) {
+    o += std::string("Error: Invariant ") + r->violated + " is violated.\n";
+  } else if (r->status == 2) {
+    o += std::string("Error: TLC threw an unexpected exception.\n") + r->message + "\n";
+  } else if (r->status == 3) {
+    o += std::string("Error: ") + r->message + "\n";
+  }
+  if ((r->status == 1 || r->status == 2) && !m->trace_states.empty()) {
+    o += "Error: The behavior up to this point is:\n";
+    for (size_t k = 0; k < m->trace_states.size(); k++) {
+      std::string act = m->trace_actions[k];
+      std::string op = act.substr(0, act.find('('));
+      if (k == 0) snprintf(line, sizeof line, "State %zu: <Initial predicate>\n", k + 1);
+      else snprintf(line, sizeof line, "State %zu: <%s%s of module %s>\n", k + 1, act.c_str(),
+                    def_location(m, op).c_str(), m->module.c_str());
+      o += line;
+      o += fmt_state(m, m->trace_states[k].data());
+      o += "\n";
+    }
+  }
+  if (r->status == 0) o += "Model checking completed. No error has been found.\n";
+  snprintf(line, sizeof line, "%llu states generated, %llu distinct states found, %llu states left on queue.\n",
+           (unsigned long long)r->generated, (unsigned long long)r->distinct, (unsigned long long)r->left_on_queue);
+  o += line;
+  snprintf(line, sizeof line, "The depth of the complete state graph search is %u.\n", r->depth);
+  o += line;
+  if (buf && len) snprintf(buf, len, "%s", o.c_str());
+  return (int)o.size();
+}
+
+void rmc_model_free(rmc_model* m) { delete m; }
+
+// Test hook only (never called by rmc_check): sequential host BFS over the same
+// lowered actions and fingerprints the kernels use, in TLC order, so the CPU
+// test suite can pin the lowering against the oracle without a GPU.
+int rmc_selftest_host_bfs(rmc_model* m, uint32_t kmax, uint64_t max_distinct, uint64_t* out3, uint64_t* levels,
+                          int level_cap) {
+  try {
+    finalize_model(m, kmax ? kmax : default_kmax(m->M));
+    const Model& M = m->M;
+    const size_t W = (size_t)M.words;
+    std::unordered_map<unsigned long long, char> seen;
+    std::vector<uint32_t> cur = init_state(M), nxt;
+    seen[host_fingerprint(M, cur.data())] = 1;
+    uint64_t gen = 1, distinct = 1, depth = 1;
+    int nl = 0;
+    auto push_level = [&](uint64_t g, uint64_t d) {
+      if (nl < level_cap) { levels[2 * nl] = g; levels[2 * nl + 1] = d; }
+      nl++;
+    };
+    push_level(1, 1);
+    size_t ncur = 1;
+    std::vector<std::pair<int, std::vector<uint32_t>>> succ;
+    while (ncur) {
+      nxt.clear();
+      size_t nn = 0;
+      uint64_t gl = 0;
+      for (size_t p = 0; p < ncur; p++) {
+        const uint32_t* S = cur.data() + p * W;
+        int B = M.nfixed + h_nmsg(S[0]);
+        succ.clear();
+        for (int b = 0; b < B; b++) {
+          std::vector<uint32_t> t(W, 0);
+          int ord = 0, act = 0, err = 0;
+          if (host_eval_apply(M, S, b, t.data(), &ord, &act, &err) != 1) continue;
+          if (err) { out3[0] = gen; out3[1] = distinct; out3[2] = depth; return -10 - err; }
+          succ.push_back({ord, t});
+        }
+        std::stable_sort(succ.begin(), succ.end(), [](auto& x, auto& y) { return x.first < y.first; });
+        for (auto& sc : succ) {
+          gen++;
+          gl++;
+          unsigned long long fp = host_fingerprint(M, sc.second.data());
+          if (seen.count(fp)) continue;
+          seen[fp] = 1;
+          distinct++;
+          nxt.insert(nxt.end(), sc.second.begin(), sc.second.end());
+          nn++;
+          int err = 0;
+          if (host_check_invariants(M, sc.second.data(), &err) >= 0 || err) {
+            out3[0] = gen; out3[1] = distinct; out3[2] = depth + 1;
+            return err ? -3 : 1;
+          }
+        }
+      }
+      if (nn || gl) push_level(gl, nn);
+      if (nn) depth++;
+      std::swap(cur, nxt);
+      ncur = nn;
+      if (max_distinct && distinct >= max_distinct) break;
+    }
+    out3[0] = gen; out3[1] = distinct; out3[2] = depth;
+    return nl;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// rmc_engine.h — interface between the host driver (rmc_engine.cpp) and the
+// HIP kernels (rmc_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "rmc_spec.h"
+
+namespace rmc {
+
+struct DevStatus {
+  unsigned long long err_key;      // first (TLC order) evaluation error in Next
+  unsigned long long inv_err_key;  // first evaluation error inside an invariant
+  unsigned long long viol_key;     // first new state violating an invariant
+  unsigned cap_flags;              // bit e set: capacity overflow ErrCode e
+  unsigned pad;
+};
+
+struct LevelArgs {
+  const uint32_t* frontier;
+  unsigned long long nparents, pbase;
+  unsigned level;  // level of the successors (parents are level-1)
+  unsigned long long* table;
+  unsigned long long mask;
+  unsigned long long* cand_slot;
+  uint32_t* cand_ob;
+  uint8_t* cand_win;
+  uint32_t *par_off, *par_n, *par_win, *par_pos;
+  unsigned long long* counters;
+  unsigned long long cand_cap;
+  uint32_t* out;
+  unsigned long long out_base_global;
+  unsigned long long* tr_parent;
+  uint16_t* tr_bind;
+  DevStatus* st;
+};
+
+void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s);
+void launch_mark(const LevelArgs& a, hipStream_t s);
+void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s);
+void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
+                   unsigned long long nmask, DevStatus* st, hipStream_t s);
+size_t scan_temp_bytes(unsigned long long n);
+void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
+                 hipStream_t s);
+hipError_t upload_model(const Model& m);
+
+// host-side (rmc_host.cpp): replay + formatting use the same action code
+int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,
+                    int* err);
+unsigned long long host_fingerprint(const Model& M, const uint32_t* S);
+int host_check_invariants(const Model& M, const uint32_t* S, int* err);
+
+}  // namespace rmc

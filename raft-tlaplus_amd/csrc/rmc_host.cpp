@@ -1,0 +1,126 @@
+// rmc_host.cpp — host instantiations of the shared action code (rmc_spec.h):
+// initial-state fingerprint, trace replay and invariant re-checks.  Compiled
+// by hipcc as host code; no device work happens here.
+#include "rmc_engine.h"
+
+namespace rmc {
+
+template <int SPEC, int N>
+static int eval_apply_t(const Model& M, const uint32_t* parent, int b, uint32_t* out, int* ordinal, int* act,
+                        int* err) {
+  PState<SPEC, N> s{parent};
+  Delta d;
+  bool en = eval_binding<SPEC, N>(s, M, b, d);
+  if (!en) return 0;
+  if (ordinal) *ordinal = d.ordinal;
+  if (act) *act = d.act;
+  if (err) *err = d.err;
+  if (d.err) return 1;
+  int e = apply_delta<SPEC, N>(s, M, d, out);
+  if (e && err) *err = e;
+  return 1;
+}
+
+template <int SPEC, int N>
+static unsigned long long fp_t(const Model& M, const uint32_t* S) {
+  PState<SPEC, N> s{S};
+  unsigned long long best = ~0ULL;
+  for (int p = 0; p < M.nperm; p++) {
+    uint32_t P = M.perm[p];
+    unsigned long long h = 0;
+    for (int i = 0; i < N; i++) h += h_server<SPEC, N>(P, i, s.A(i), s.B(i), s.Cw(i), s.Dw(i));
+    for (int k = 0; k < s.nmsg(); k++) h += h_msg<SPEC>(P, s.msg(k));
+    if (SPEC == PULL) h += h_acked_view(s.hdr());
+    unsigned long long f = mix64(h);
+    if (f < best) best = f;
+  }
+  return best;
+}
+
+template <int SPEC, int N>
+static int inv_t(const Model& M, const uint32_t* S, int* err) {
+  PState<SPEC, N> s{S};
+  int e = 0;
+  int r = check_invariants<SPEC, N>(s, M, e);
+  if (err) *err = e;
+  return r;
+}
+
+#define RMC_DISPATCH(FN, ...)                                    \
+  switch (M.spec * 8 + M.N) {                                    \
+    case RAFT * 8 + 2: return FN<RAFT, 2>(__VA_ARGS__);          \
+    case RAFT * 8 + 3: return FN<RAFT, 3>(__VA_ARGS__);          \
+    case RAFT * 8 + 4: return FN<RAFT, 4>(__VA_ARGS__);          \
+    case RAFT * 8 + 5: return FN<RAFT, 5>(__VA_ARGS__);          \
+    case FLEX * 8 + 2: return FN<FLEX, 2>(__VA_ARGS__);          \
+    case FLEX * 8 + 3: return FN<FLEX, 3>(__VA_ARGS__);          \
+    case FLEX * 8 + 4: return FN<FLEX, 4>(__VA_ARGS__);          \
+    case FLEX * 8 + 5: return FN<FLEX, 5>(__VA_ARGS__);          \
+    case FSYNC * 8 + 2: return FN<FSYNC, 2>(__VA_ARGS__);        \
+    case FSYNC * 8 + 3: return FN<FSYNC, 3>(__VA_ARGS__);        \
+    case FSYNC * 8 + 4: return FN<FSYNC, 4>(__VA_ARGS__);        \
+    case FSYNC * 8 + 5: return FN<FSYNC, 5>(__VA_ARGS__);        \
+    case PULL * 8 + 2: return FN<PULL, 2>(__VA_ARGS__);          \
+    case PULL * 8 + 3: return FN<PULL, 3>(__VA_ARGS__);          \
+    case PULL * 8 + 4: return FN<PULL, 4>(__VA_ARGS__);          \
+    case PULL * 8 + 5: return FN<PULL, 5>(__VA_ARGS__);          \
+  }
+
+int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,
+                    int* err) {
+  RMC_DISPATCH(eval_apply_t, M, parent, binding, out, ordinal, act, err);
+  return -1;
+}
+unsigned long long host_fingerprint(const Model& M, const uint32_t* S) {
+  RMC_DISPATCH(fp_t, M, S);
+  return 0;
+}
+int host_check_invariants(const Model& M, const uint32_t* S, int* err) {
+  RMC_DISPATCH(inv_t, M, S, err);
+  return -1;
+}
+
+}  // namespace rmc
+
+// ---------------------------------------------------------------------------
+// Test hooks (never reached from rmc_check / raftmc): a sequential host BFS
+// over the SAME lowered action code and fingerprint as the kernels, so the
+// CPU test suite can check the lowering against the oracle without a GPU,
+// and message-codec probes for the layout tests.
+#include <unordered_map>
+#include <vector>
+#include <string>
+#include <cstring>
+#include "../../include/rmc.h"
+
+namespace rmc {
+std::vector<uint32_t> selftest_init_state(const Model& M) {
+  std::vector<uint32_t> S(M.words, 0u);
+  for (int i = 0; i < M.N; i++) {
+    S[1 + 4 * i] = 1u | ((uint32_t)NILS << 6);
+    S[3 + 4 * i] = M.spec == PULL ? 0u : all_rows(M.N, 1);
+  }
+  return S;
+}
+}  // namespace rmc
+
+extern "C" int rmc_selftest_encode_msg(int spec, const int* f, uint32_t* out) {
+  using namespace rmc;
+  MsgF m = msg_zero();
+  m.type = f[0]; m.term = f[1]; m.src = f[2]; m.dst = f[3]; m.lli = f[4]; m.llt = f[5]; m.granted = f[6];
+  m.pli = f[7]; m.plt = f[8]; m.nent = f[9]; m.eterm = f[10]; m.evalue = f[11]; m.commit = f[12];
+  m.success = f[13]; m.midx = f[14]; m.lci = f[15]; m.lct = f[16]; m.count = f[17];
+  *out = spec == PULL ? msg_encode<PULL>(m) : msg_encode<RAFT>(m);
+  MsgF d = spec == PULL ? msg_decode<PULL>(*out) : msg_decode<RAFT>(*out);
+  int sp, dp;
+  if (spec == PULL) msg_srcdst_pos<PULL>(*out, sp, dp); else msg_srcdst_pos<RAFT>(*out, sp, dp);
+  int term = spec == PULL ? msg_term<PULL>(*out) : msg_term<RAFT>(*out);
+  int type = spec == PULL ? msg_type<PULL>(*out) : msg_type<RAFT>(*out);
+  int ok = d.type == m.type && d.term == m.term && d.src == m.src && d.dst == m.dst && d.lli == m.lli &&
+           d.llt == m.llt && d.granted == m.granted && d.pli == m.pli && d.plt == m.plt && d.nent == m.nent &&
+           d.eterm == m.eterm && d.evalue == m.evalue && d.commit == m.commit && d.success == m.success &&
+           d.midx == m.midx && d.lci == m.lci && d.lct == m.lct && d.count == m.count &&
+           (int)((*out >> sp) & 7u) == m.src && (int)((*out >> dp) & 7u) == m.dst && term == m.term &&
+           type == m.type;
+  return ok ? 0 : 1;
+}

@@ -1,0 +1,365 @@
+// rmc_kernels.hip — level-synchronous BFS kernels for gfx950 (MI355X).
+//
+// Per BFS level, per chunk of parents:
+//   k_expand       one wavefront per parent: stage the packed parent in LDS,
+//                  compute H_pi(parent) for every server permutation (lanes
+//                  split the items, wave reduction per pi), evaluate every
+//                  binding of Next in parallel (one lane per binding), ballot
+//                  the enabled ones, and for each successor compute its
+//                  canonical fingerprint incrementally from the parent's H_pi
+//                  and the successor delta, then insert it into the HBM
+//                  fingerprint set with first-in-TLC-order-wins semantics
+//                  (atomicMin on (level, parent, ordinal)).
+//   k_mark         one thread per parent: which of its candidates won.
+//   (scan)         exclusive scan of winners per parent -> output positions.
+//   k_materialize  one wavefront per parent: regenerate each winning successor
+//                  from parent + binding, write it to the next frontier in TLC
+//                  order, check the cfg's invariants, write the trace record.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include "rmc_spec.h"
+#include "rmc_engine.h"
+
+namespace rmc {
+
+__constant__ Model cM;
+
+constexpr int WAVE = 64;
+constexpr int WAVES_PER_BLOCK = 4;
+constexpr int MAXW = 1 + 4 * MAXN + 128;  // words per state staged in LDS
+constexpr int MAXROUNDS = 4;              // up to 256 bindings per state
+constexpr unsigned long long EMPTY = ~0ULL;
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+    lo = __shfl_xor(lo, o, WAVE);
+    hi = __shfl_xor(hi, o, WAVE);
+    v += ((unsigned long long)hi << 32) | lo;
+  }
+  return v;
+}
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  int l = lane_id();
+  return l ? (~0ULL >> (64 - l)) : 0ULL;
+}
+
+// first-in-TLC-order error / violation keys: (parent_global << 20) | (ordinal << 10) | binding
+__device__ __forceinline__ unsigned long long order_key(unsigned long long pg, int ordinal, int b) {
+  return (pg << 20) | ((unsigned long long)ordinal << 10) | (unsigned long long)b;
+}
+
+// Insert fp with value val; returns the slot.  val = (level << 48) | rank.
+__device__ __forceinline__ unsigned long long table_insert(unsigned long long* T, unsigned long long mask,
+                                                           unsigned long long fp, unsigned long long val,
+                                                           unsigned level, DevStatus* st) {
+  if (fp == EMPTY) fp = EMPTY - 1;
+  unsigned long long slot = (fp ^ (fp >> 29)) & mask;
+  for (unsigned long long probe = 0; probe <= mask; probe++) {
+    unsigned long long* e = T + 2 * slot;
+    unsigned long long k = e[0];
+    if (k == EMPTY) {
+      unsigned long long prev = atomicCAS(e, EMPTY, fp);
+      if (prev == EMPTY || prev == fp) {
+        atomicMin(e + 1, val);
+        return slot;
+      }
+      k = prev;
+    } else if (k == fp) {
+      unsigned long long v = e[1];
+      if ((unsigned)(v >> 48) < level) return slot;  // seen in an earlier level
+      atomicMin(e + 1, val);
+      return slot;
+    }
+    slot = (slot + 1) & mask;
+  }
+  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+  return 0;
+}
+
+template <int SPEC, int N>
+__device__ __forceinline__ unsigned long long successor_fp(const PState<SPEC, N>& s, const Delta& d,
+                                                           const unsigned long long* Hp, int nperm) {
+  unsigned long long best = EMPTY;
+  unsigned long long aux = 0;
+  if (SPEC == PULL && ((d.hdr ^ s.hdr()) & 0x00FF0000u)) aux = h_acked_view(d.hdr) - h_acked_view(s.hdr());
+  for (int p = 0; p < nperm; p++) {
+    uint32_t P = cM.perm[p];
+    unsigned long long h = Hp[p] + aux;
+    if (d.srv >= 0) {
+      int i = d.srv;
+      h += h_server<SPEC, N>(P, i, d.w[0], d.w[1], d.w[2], d.w[3]);
+      h -= h_server<SPEC, N>(P, i, s.A(i), s.B(i), s.Cw(i), s.Dw(i));
+    }
+#pragma unroll
+    for (int q = 0; q < MAXOPS; q++) {
+      if (q >= d.nops) break;
+      h += h_msg<SPEC>(P, d.opc[q]);
+      if (d.opk[q] >= 0) h -= h_msg<SPEC>(P, s.msg(d.opk[q]));
+    }
+    unsigned long long f = mix64(h);
+    best = f < best ? f : best;
+  }
+  return best;
+}
+
+template <int SPEC, int N>
+__global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+                                                unsigned long long pbase, unsigned level,
+                                                unsigned long long* __restrict__ table, unsigned long long mask,
+                                                unsigned long long* __restrict__ cand_slot,
+                                                uint32_t* __restrict__ cand_ob, uint32_t* __restrict__ par_off,
+                                                uint32_t* __restrict__ par_n,
+                                                unsigned long long* __restrict__ counters, unsigned long long cand_cap,
+                                                DevStatus* st) {
+  __shared__ uint32_t sS[WAVES_PER_BLOCK][MAXW];
+  __shared__ unsigned long long sH[WAVES_PER_BLOCK][MAXPERM];
+  const int w = threadIdx.x / WAVE, lane = lane_id();
+  const unsigned long long p = (unsigned long long)blockIdx.x * WAVES_PER_BLOCK + w;
+  if (p >= nparents) return;
+  const int words = cM.words, nperm = cM.nperm;
+  uint32_t* S = sS[w];
+  const uint32_t* src = frontier + p * (unsigned long long)words;
+  for (int q = lane; q < words; q += WAVE) S[q] = src[q];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  PState<SPEC, N> s{S};
+  const int nm = s.nmsg();
+  // ---- H_pi(parent) for all pi: items = N servers + nm messages (+ acked for Pull)
+  const int nitems = N + nm;
+  for (int pi = 0; pi < nperm; pi++) {
+    uint32_t P = cM.perm[pi];
+    unsigned long long acc = 0;
+    for (int it = lane; it < nitems; it += WAVE) {
+      if (it < N) acc += h_server<SPEC, N>(P, it, s.A(it), s.B(it), s.Cw(it), s.Dw(it));
+      else acc += h_msg<SPEC>(P, s.msg(it - N));
+    }
+    acc = wave_sum_u64(acc);
+    if (SPEC == PULL) acc += h_acked_view(s.hdr());
+    if (lane == 0) sH[w][pi] = acc;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // ---- enabled bindings
+  const int B = cM.nfixed + nm;
+  const int rounds = (B + WAVE - 1) / WAVE;
+  if (rounds > MAXROUNDS) {
+    if (lane == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
+    return;
+  }
+  unsigned long long masks[MAXROUNDS] = {0, 0, 0, 0};
+  int total = 0;
+  const unsigned long long pg = pbase + p;
+#pragma unroll
+  for (int r = 0; r < MAXROUNDS; r++) {
+    if (r >= rounds) break;
+    int b = r * WAVE + lane;
+    Delta d;
+    bool en = false;
+    if (b < B) {
+      en = eval_binding<SPEC, N>(s, cM, b, d);
+      if (en && d.err) {
+        if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pg, d.ordinal, b));
+        else atomicOr(&st->cap_flags, 1u << d.err);
+      }
+      if (en && !d.err) {
+        // capacity: the successor must fit in kmax message slots
+        int adds = 0;
+#pragma unroll
+        for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
+        if (nm + adds > cM.kmax) { atomicOr(&st->cap_flags, 1u << E_CAP_MSG); }
+      }
+    }
+    masks[r] = __ballot(en);
+    total += __popcll(masks[r]);
+  }
+  unsigned long long off = 0;
+  if (lane == 0 && total) off = atomicAdd(&counters[0], (unsigned long long)total);
+  off = __shfl(off, 0, WAVE);
+  if (lane == 0) {
+    par_off[p] = (uint32_t)off;
+    par_n[p] = (uint32_t)total;
+  }
+  if (off + total > cand_cap) {
+    if (lane == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
+    return;
+  }
+  // ---- fingerprints + inserts
+  int before = 0;
+  const unsigned long long* Hp = sH[w];
+#pragma unroll
+  for (int r = 0; r < MAXROUNDS; r++) {
+    if (r >= rounds) break;
+    if ((masks[r] >> lane) & 1ULL) {
+      int b = r * WAVE + lane;
+      Delta d;
+      eval_binding<SPEC, N>(s, cM, b, d);
+      unsigned long long t = off + before + __popcll(masks[r] & lanemask_lt());
+      unsigned long long slot = 0;
+      if (!d.err) {
+        unsigned long long fp = successor_fp<SPEC, N>(s, d, Hp, nperm);
+        unsigned long long val = ((unsigned long long)level << 48) | (pg << 10) | (unsigned long long)d.ordinal;
+        slot = table_insert(table, mask, fp, val, level, st);
+      }
+      cand_slot[t] = slot;
+      cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? 0x8000u : 0u);
+    }
+    before += __popcll(masks[r]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsigned long long pbase, unsigned level,
+                                              const unsigned long long* __restrict__ table,
+                                              const unsigned long long* __restrict__ cand_slot,
+                                              const uint32_t* __restrict__ cand_ob,
+                                              const uint32_t* __restrict__ par_off, const uint32_t* __restrict__ par_n,
+                                              uint8_t* __restrict__ cand_win, uint32_t* __restrict__ par_win) {
+  unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nparents) return;
+  uint32_t off = par_off[p], n = par_n[p];
+  uint32_t cnt = 0;
+  unsigned long long base = ((unsigned long long)level << 48) | ((pbase + p) << 10);
+  for (uint32_t t = off; t < off + n; t++) {
+    uint32_t ob = cand_ob[t];
+    uint8_t win = 0;
+    if (!(ob & 0x8000u)) {
+      unsigned long long mine = base | (ob >> 16);
+      win = table[2 * cand_slot[t] + 1] == mine;
+    }
+    cand_win[t] = win;
+    cnt += win;
+  }
+  par_win[p] = cnt;
+}
+
+template <int SPEC, int N>
+__global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+                                                     unsigned long long pbase, const uint32_t* __restrict__ cand_ob,
+                                                     const uint8_t* __restrict__ cand_win,
+                                                     const uint32_t* __restrict__ par_off,
+                                                     const uint32_t* __restrict__ par_n,
+                                                     const uint32_t* __restrict__ par_pos, uint32_t* __restrict__ out,
+                                                     unsigned long long out_base_global,
+                                                     unsigned long long* __restrict__ tr_parent,
+                                                     uint16_t* __restrict__ tr_bind, DevStatus* st) {
+  __shared__ uint32_t sS[WAVES_PER_BLOCK][MAXW];
+  __shared__ uint32_t sOrd[WAVES_PER_BLOCK][MAXROUNDS * WAVE];
+  const int w = threadIdx.x / WAVE, lane = lane_id();
+  const unsigned long long p = (unsigned long long)blockIdx.x * WAVES_PER_BLOCK + w;
+  if (p >= nparents) return;
+  const uint32_t n = par_n[p], off = par_off[p];
+  const int words = cM.words;
+  uint32_t* S = sS[w];
+  const uint32_t* src = frontier + p * (unsigned long long)words;
+  for (int q = lane; q < words; q += WAVE) S[q] = src[q];
+  // winners' ordinals (0xFFFF for losers) so each winner can find its rank in TLC order
+  for (uint32_t t = lane; t < n; t += WAVE)
+    sOrd[w][t] = cand_win[off + t] ? (cand_ob[off + t] >> 16) : 0xFFFFu;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  PState<SPEC, N> s{S};
+  const unsigned long long pg = pbase + p;
+  const uint32_t pos0 = par_pos[p];
+  for (uint32_t t = lane; t < n; t += WAVE) {
+    uint32_t my = sOrd[w][t];
+    if (my == 0xFFFFu) continue;
+    uint32_t rank = 0;
+    for (uint32_t u = 0; u < n; u++) rank += sOrd[w][u] < my;
+    int b = (int)(cand_ob[off + t] & 0x3FFu);
+    Delta d;
+    eval_binding<SPEC, N>(s, cM, b, d);
+    unsigned long long dst = (unsigned long long)pos0 + rank;
+    uint32_t* o = out + dst * (unsigned long long)words;
+    int e = apply_delta<SPEC, N>(s, cM, d, o);
+    if (e) atomicOr(&st->cap_flags, 1u << e);
+    tr_parent[out_base_global + dst] = pg;
+    tr_bind[out_base_global + dst] = (uint16_t)b;
+    PState<SPEC, N> ns{o};
+    int err = 0;
+    int bad = check_invariants<SPEC, N>(ns, cM, err);
+    if (err) atomicMin(&st->inv_err_key, order_key(pg, (int)my, b));
+    else if (bad >= 0) atomicMin(&st->viol_key, order_key(pg, (int)my, b));
+  }
+}
+
+// ------------------------------------------------------------ host driver
+struct Launch {
+  template <int SPEC, int N>
+  static void expand(const LevelArgs& a, hipStream_t s) {
+    unsigned long long blocks = (a.nparents + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), 0, s, a.frontier, a.nparents, a.pbase,
+                       a.level, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
+                       a.st);
+  }
+  template <int SPEC, int N>
+  static void materialize(const LevelArgs& a, hipStream_t s) {
+    unsigned long long blocks = (a.nparents + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(256), 0, s, a.frontier, a.nparents,
+                       a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
+                       a.tr_parent, a.tr_bind, a.st);
+  }
+};
+
+template <int SPEC>
+static void dispatch_n(int N, bool expand, const LevelArgs& a, hipStream_t s) {
+  switch (N) {
+    case 2: expand ? Launch::expand<SPEC, 2>(a, s) : Launch::materialize<SPEC, 2>(a, s); break;
+    case 3: expand ? Launch::expand<SPEC, 3>(a, s) : Launch::materialize<SPEC, 3>(a, s); break;
+    case 4: expand ? Launch::expand<SPEC, 4>(a, s) : Launch::materialize<SPEC, 4>(a, s); break;
+    case 5: expand ? Launch::expand<SPEC, 5>(a, s) : Launch::materialize<SPEC, 5>(a, s); break;
+  }
+}
+static void dispatch(int spec, int N, bool expand, const LevelArgs& a, hipStream_t s) {
+  switch (spec) {
+    case RAFT: dispatch_n<RAFT>(N, expand, a, s); break;
+    case FLEX: dispatch_n<FLEX>(N, expand, a, s); break;
+    case FSYNC: dispatch_n<FSYNC>(N, expand, a, s); break;
+    case PULL: dispatch_n<PULL>(N, expand, a, s); break;
+  }
+}
+
+void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, true, a, s); }
+void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, false, a, s); }
+void launch_mark(const LevelArgs& a, hipStream_t s) {
+  unsigned long long blocks = (a.nparents + 255) / 256;
+  hipLaunchKernelGGL(k_mark, dim3((unsigned)blocks), dim3(256), 0, s, a.nparents, a.pbase, a.level, a.table,
+                     a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.cand_win, a.par_win);
+}
+// Move every entry of the old fingerprint set into a larger one (values kept).
+__global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __restrict__ old, unsigned long long nold,
+                                                unsigned long long* __restrict__ nt, unsigned long long mask,
+                                                DevStatus* st) {
+  unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nold) return;
+  unsigned long long k = old[2 * e];
+  if (k == EMPTY) return;
+  unsigned long long slot = (k ^ (k >> 29)) & mask;
+  for (unsigned long long probe = 0; probe <= mask; probe++) {
+    unsigned long long prev = atomicCAS(nt + 2 * slot, EMPTY, k);
+    if (prev == EMPTY) {
+      nt[2 * slot + 1] = old[2 * e + 1];
+      return;
+    }
+    slot = (slot + 1) & mask;
+  }
+  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+}
+void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
+                   unsigned long long nmask, DevStatus* st, hipStream_t s) {
+  unsigned long long blocks = (nold + 255) / 256;
+  hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, s, old, nold, nt, nmask, st);
+}
+size_t scan_temp_bytes(unsigned long long n) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  return bytes;
+}
+void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
+                 hipStream_t s) {
+  hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
+}
+hipError_t upload_model(const Model& m) { return hipMemcpyToSymbol(HIP_SYMBOL(cM), &m, sizeof(Model)); }
+
+}  // namespace rmc

@@ -1,0 +1,962 @@
+// rmc_spec.h — packed state layout and the four Raft specs' Next actions as
+// __host__ __device__ functions over it.  Shared by the HIP kernels and the
+// host-side trace replay of librmc.  (The CPU oracle in oracle/ is a separate,
+// independent restatement and does not include this file.)
+//
+// Packed state (u32 words; all specs):
+//   S[0]            header: nmsg 0-7 | electionCtr 8-11 | restartCtr 12-15 |
+//                   acked[v] 16+2v (0 Nil, 1 FALSE, 2 TRUE)
+//   S[1+4i+0] (A)   server i: currentTerm 0-3 | state 4-5 | votedFor/leader 6-8
+//                   (7 = Nil) | Len(log) 9-11 | commitIndex 12-14 |
+//                   fsyncIndex 15-17 | votesGranted 18-24 | pendingResponse 25-31
+//   S[1+4i+1] (B)   log: entry x (0-based) at 6x: term 0-3 | value 4-5
+//   S[1+4i+2] (C)   nextIndex[i][j] at 3j
+//   S[1+4i+3] (D)   matchIndex[i][j] at 3j
+//   S[1+4N+k]       DOMAIN messages, ascending = TLC's value order; record in
+//                   bits 3-31 (layouts below), count (messages[m]) in bits 0-2.
+//
+// Message records are laid out MSB-first in exactly the order TLC compares
+// them (RecordValue.compareTo: field count, then sorted field names with
+// their values), so unsigned comparison of two words IS TLC's order and a
+// sorted word array IS TLC's DOMAIN enumeration order (SURVEY.md §7 hard part
+// 3, Appendix A.4).  Field-name orders:
+//   Raft.tla:251-256 RVReq  {mdest, mlastLogIndex, mlastLogTerm, msource, mterm, mtype}
+//   Raft.tla:374-378 RVResp {mdest, msource, mterm, mtype, mvoteGranted}
+//   Raft.tla:277-284 AEReq  {mcommitIndex, mdest, mentries, mprevLogIndex, mprevLogTerm, msource, mterm, mtype}
+//   Raft.tla:422-427 AEResp {mdest, mmatchIndex, msource, msuccess, mterm, mtype}
+//   PullRaft.tla:361-364 LeaderNotify {mdest, msource, mterm, mtype}
+//   PullRaft.tla:405-410 PullReq {same names as RVReq}
+//   PullRaft.tla:426-433 PullResp fail {mdest, mlastCommonEntry, msource, msuccess, mterm, mtype}
+//   PullRaft.tla:480-486 PullResp ok   {mcommitIndex, mdest, mentries, msource, msuccess, mterm, mtype}
+#pragma once
+#include <stdint.h>
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RMC_HD __host__ __device__ __forceinline__
+#else
+#define RMC_HD static inline
+#endif
+
+namespace rmc {
+
+enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3 };
+enum SrvState { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
+enum MType { RVREQ = 0, RVRESP = 1, AEREQ = 2, AERESP = 3, LNREQ = 4, PEREQ = 5, PERESP = 6 };
+enum ActId {
+  A_RESTART = 0, A_REQUESTVOTE, A_TIMEOUT, A_RVIJ, A_BECOMELEADER, A_CLIENT, A_ADVCOMMIT,
+  A_APPENDENTRIES, A_ADVFSYNC, A_UPDATETERM, A_HRVREQ, A_HRVRESP, A_REJAE, A_ACCAE, A_HAERESP,
+  A_REJPULL, A_ACCPULL, A_LEARN, A_SENDPULL, A_HSUCC, A_HFAIL, A_NUM
+};
+enum ActKind { K_I = 0, K_IV = 1, K_IJ = 2, K_MSG = 3 };
+enum ErrCode {
+  E_NONE = 0,
+  E_DOMAIN = 1,     // TLC evaluation error: sequence applied outside its domain
+  E_CAP_LOG = 2,    // log longer than the packed layout holds
+  E_CAP_MSG = 3,    // more messages than msg_cap_K
+  E_CAP_COUNT = 4,  // message multiplicity > 7
+  E_CAP_TERM = 5,   // term > 15
+  E_CAP_FIELD = 6,  // an index field > 7
+  E_CAP_SUCC = 7,   // more successors for one state than the candidate buffer holds
+  E_CAP_TABLE = 8,  // fingerprint set full
+  E_CAP_FRONTIER = 9
+};
+constexpr int NILS = 7;
+constexpr int MAXN = 7, MAXV = 4, MAXLOG = 5, MAXOPS = 7, MAXPERM = 120, MAXACT = 16, MAXFIXED = 192;
+
+struct Model {
+  int spec, N, V, E, R, EQ, RQ, lfae, lfiq, ffbr;
+  int kmax, words;  // words = 1 + 4N + kmax
+  int nperm;
+  uint32_t perm[MAXPERM];  // permutation p maps server j -> (perm[p] >> 3j) & 7
+  int ninv, inv[3];        // invariant ids in cfg order: 0 LHAAV, 1 NLD, 2 CERM
+  int nact, act_id[MAXACT], act_kind[MAXACT], act_off[MAXACT];
+  int nfixed;
+  uint8_t fb_act[MAXFIXED], fb_x[MAXFIXED];  // fixed binding -> (action slot, binding index)
+  int msg_act_slot[A_NUM];                   // action slot of each message action
+  int ordinal_limit;
+};
+
+// ------------------------------------------------------------- bit helpers
+RMC_HD uint32_t getb(uint32_t w, int pos, int width) { return (w >> pos) & ((1u << width) - 1u); }
+RMC_HD uint32_t setb(uint32_t w, int pos, int width, uint32_t v) {
+  uint32_t m = ((1u << width) - 1u) << pos;
+  return (w & ~m) | ((v << pos) & m);
+}
+// header
+RMC_HD int h_nmsg(uint32_t h) { return (int)(h & 0xFF); }
+RMC_HD int h_ectr(uint32_t h) { return (int)getb(h, 8, 4); }
+RMC_HD int h_rctr(uint32_t h) { return (int)getb(h, 12, 4); }
+RMC_HD int h_acked(uint32_t h, int v) { return (int)getb(h, 16 + 2 * v, 2); }
+// server word A
+RMC_HD int a_term(uint32_t a) { return (int)getb(a, 0, 4); }
+RMC_HD int a_st(uint32_t a) { return (int)getb(a, 4, 2); }
+RMC_HD int a_voted(uint32_t a) { return (int)getb(a, 6, 3); }
+RMC_HD int a_len(uint32_t a) { return (int)getb(a, 9, 3); }
+RMC_HD int a_commit(uint32_t a) { return (int)getb(a, 12, 3); }
+RMC_HD int a_fsync(uint32_t a) { return (int)getb(a, 15, 3); }
+RMC_HD int a_votes(uint32_t a) { return (int)getb(a, 18, 7); }
+RMC_HD int a_pending(uint32_t a) { return (int)getb(a, 25, 7); }
+// log word B
+RMC_HD int e_term(uint32_t b, int x) { return (int)getb(b, 6 * x, 4); }
+RMC_HD int e_value(uint32_t b, int x) { return (int)getb(b, 6 * x + 4, 2); }
+RMC_HD uint32_t e_pack(int term, int value) { return (uint32_t)(term | (value << 4)); }
+// C/D rows
+RMC_HD int row_get(uint32_t w, int j) { return (int)getb(w, 3 * j, 3); }
+RMC_HD uint32_t row_set(uint32_t w, int j, int v) { return setb(w, 3 * j, 3, (uint32_t)v); }
+
+// ------------------------------------------------------------ messages
+struct MsgF {
+  int type, term, src, dst;
+  int lli, llt;               // mlastLogIndex, mlastLogTerm
+  int granted;                // mvoteGranted
+  int pli, plt;               // mprevLogIndex, mprevLogTerm
+  int nent, eterm, evalue;    // mentries
+  int commit;                 // mcommitIndex
+  int success, midx;          // msuccess, mmatchIndex
+  int lci, lct;               // mlastCommonEntry.index/.term
+  int count;
+};
+RMC_HD MsgF msg_zero() {
+  MsgF f;
+  f.type = f.term = f.src = f.dst = f.lli = f.llt = f.granted = f.pli = f.plt = 0;
+  f.nent = f.eterm = f.evalue = f.commit = f.success = f.midx = f.lci = f.lct = f.count = 0;
+  return f;
+}
+struct Bits {
+  uint32_t v;
+  int pos;
+  RMC_HD void put(int x, int w) { pos -= w; v |= ((uint32_t)x & ((1u << w) - 1u)) << pos; }
+};
+struct Rd {
+  uint32_t v;
+  int pos;
+  RMC_HD int get(int w) { pos -= w; return (int)((v >> pos) & ((1u << w) - 1u)); }
+};
+template <int SPEC>
+RMC_HD uint32_t msg_encode(const MsgF& f) {
+  Bits b{0u, 32};
+  if (SPEC != PULL) {
+    switch (f.type) {
+      case RVRESP: b.put(0, 2); b.put(f.dst, 3); b.put(f.src, 3); b.put(f.term, 4); b.put(f.granted, 1); break;
+      case RVREQ: b.put(1, 2); b.put(f.dst, 3); b.put(0, 1); b.put(f.lli, 3); b.put(f.llt, 4); b.put(f.src, 3); b.put(f.term, 4); break;
+      case AERESP: b.put(1, 2); b.put(f.dst, 3); b.put(1, 1); b.put(f.midx, 3); b.put(f.src, 3); b.put(f.success, 1); b.put(f.term, 4); break;
+      default: /* AEREQ */
+        b.put(2, 2); b.put(f.commit, 3); b.put(f.dst, 3); b.put(f.nent, 1); b.put(f.eterm, 4); b.put(f.evalue, 2);
+        b.put(f.pli, 3); b.put(f.plt, 4); b.put(f.src, 3); b.put(f.term, 4); break;
+    }
+  } else {
+    switch (f.type) {
+      case LNREQ: b.put(0, 2); b.put(f.dst, 3); b.put(f.src, 3); b.put(f.term, 4); break;
+      case RVRESP: b.put(1, 2); b.put(f.dst, 3); b.put(f.src, 3); b.put(f.term, 4); b.put(f.granted, 1); break;
+      case RVREQ: case PEREQ:
+        b.put(2, 2); b.put(f.dst, 3); b.put(1, 1); b.put(f.lli, 3); b.put(f.llt, 4); b.put(f.src, 3); b.put(f.term, 4);
+        b.put(f.type == RVREQ ? 1 : 0, 1); break;
+      default: /* PERESP */
+        if (!f.success) {
+          b.put(2, 2); b.put(f.dst, 3); b.put(0, 1); b.put(f.lci, 3); b.put(f.lct, 4); b.put(f.src, 3); b.put(0, 1); b.put(f.term, 4);
+        } else {
+          b.put(3, 2); b.put(f.commit, 3); b.put(f.dst, 3); b.put(f.nent, 1); b.put(f.eterm, 4); b.put(f.evalue, 2);
+          b.put(f.src, 3); b.put(1, 1); b.put(f.term, 4);
+        }
+        break;
+    }
+  }
+  return b.v | ((uint32_t)f.count & 7u);
+}
+template <int SPEC>
+RMC_HD MsgF msg_decode(uint32_t w) {
+  MsgF f = msg_zero();
+  Rd r{w, 32};
+  f.count = (int)(w & 7u);
+  int cls = r.get(2);
+  if (SPEC != PULL) {
+    if (cls == 0) { f.type = RVRESP; f.dst = r.get(3); f.src = r.get(3); f.term = r.get(4); f.granted = r.get(1); }
+    else if (cls == 1) {
+      f.dst = r.get(3);
+      if (r.get(1) == 0) { f.type = RVREQ; f.lli = r.get(3); f.llt = r.get(4); f.src = r.get(3); f.term = r.get(4); }
+      else { f.type = AERESP; f.midx = r.get(3); f.src = r.get(3); f.success = r.get(1); f.term = r.get(4); }
+    } else {
+      f.type = AEREQ; f.commit = r.get(3); f.dst = r.get(3); f.nent = r.get(1); f.eterm = r.get(4); f.evalue = r.get(2);
+      f.pli = r.get(3); f.plt = r.get(4); f.src = r.get(3); f.term = r.get(4);
+    }
+  } else {
+    if (cls == 0) { f.type = LNREQ; f.dst = r.get(3); f.src = r.get(3); f.term = r.get(4); }
+    else if (cls == 1) { f.type = RVRESP; f.dst = r.get(3); f.src = r.get(3); f.term = r.get(4); f.granted = r.get(1); }
+    else if (cls == 2) {
+      f.dst = r.get(3);
+      if (r.get(1) == 0) { f.type = PERESP; f.success = 0; f.lci = r.get(3); f.lct = r.get(4); f.src = r.get(3); r.get(1); f.term = r.get(4); }
+      else { f.lli = r.get(3); f.llt = r.get(4); f.src = r.get(3); f.term = r.get(4); f.type = r.get(1) ? RVREQ : PEREQ; }
+    } else {
+      f.type = PERESP; f.success = 1; f.commit = r.get(3); f.dst = r.get(3); f.nent = r.get(1); f.eterm = r.get(4);
+      f.evalue = r.get(2); f.src = r.get(3); r.get(1); f.term = r.get(4);
+    }
+  }
+  return f;
+}
+// Bit positions (LSB index) of msource / mdest / mterm within a message word,
+// from the MSB-first layouts of msg_encode (checked against msg_decode by the
+// CPU test tests/test_layout.py):
+//   Raft  cls0 RVResp  dst27 src24 term20 | cls1 RVReq dst27 src16 term12 |
+//         cls1 AEResp  dst27 src20 term15 | cls2 AEReq dst24 src7  term3
+//   Pull  cls0 LN      dst27 src24 term20 | cls1 RVResp dst27 src24 term20 |
+//         cls2 fail    dst27 src16 term11 | cls2 req   dst27 src16 term12 (isRV at 11) |
+//         cls3 ok      dst24 src14 term9
+template <int SPEC>
+RMC_HD void msg_srcdst_pos(uint32_t w, int& sp, int& dp) {
+  int cls = (int)(w >> 30);
+  if (SPEC != PULL) {
+    if (cls == 0) { dp = 27; sp = 24; }
+    else if (cls == 1) { dp = 27; sp = ((w >> 26) & 1u) ? 20 : 16; }
+    else { dp = 24; sp = 7; }
+  } else {
+    if (cls <= 1) { dp = 27; sp = 24; }
+    else if (cls == 2) { dp = 27; sp = 16; }
+    else { dp = 24; sp = 14; }
+  }
+}
+template <int SPEC>
+RMC_HD int msg_type(uint32_t w) {
+  int cls = (int)(w >> 30);
+  if (SPEC != PULL) {
+    if (cls == 0) return RVRESP;
+    if (cls == 1) return ((w >> 26) & 1u) ? AERESP : RVREQ;
+    return AEREQ;
+  }
+  if (cls == 0) return LNREQ;
+  if (cls == 1) return RVRESP;
+  if (cls == 2) return ((w >> 26) & 1u) ? (((w >> 11) & 1u) ? RVREQ : PEREQ) : PERESP;
+  return PERESP;
+}
+template <int SPEC>
+RMC_HD int msg_term(uint32_t w) {
+  int cls = (int)(w >> 30);
+  int pos;
+  if (SPEC != PULL) {
+    if (cls == 0) pos = 20;
+    else if (cls == 1) pos = ((w >> 26) & 1u) ? 15 : 12;
+    else pos = 3;
+  } else {
+    if (cls <= 1) pos = 20;
+    else if (cls == 2) pos = ((w >> 26) & 1u) ? 12 : 11;
+    else pos = 9;
+  }
+  return (int)((w >> pos) & 15u);
+}
+template <int SPEC>
+RMC_HD int msg_dst(uint32_t w) {
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  return (int)((w >> dp) & 7u);
+}
+RMC_HD uint32_t msg_rec(uint32_t w) { return w >> 3; }
+RMC_HD int msg_count(uint32_t w) { return (int)(w & 7u); }
+
+// ------------------------------------------------------------------ delta
+// A successor = parent + (one server's words replaced) + (message ops) +
+// (new header).  Every Next disjunct of the four specs changes at most one
+// server's variables, so this is exact.
+struct Delta {
+  int srv;
+  uint32_t w[4];
+  int nops;
+  int opk[MAXOPS];       // parent DOMAIN index modified in place, or -1 = insert
+  uint32_t opc[MAXOPS];  // resulting message word (record | count)
+  uint32_t hdr;
+  int ordinal;
+  int act;
+  int err;
+};
+
+template <int SPEC, int N>
+struct PState {
+  const uint32_t* S;
+  RMC_HD uint32_t hdr() const { return S[0]; }
+  RMC_HD uint32_t A(int i) const { return S[1 + 4 * i]; }
+  RMC_HD uint32_t B(int i) const { return S[2 + 4 * i]; }
+  RMC_HD uint32_t Cw(int i) const { return S[3 + 4 * i]; }
+  RMC_HD uint32_t Dw(int i) const { return S[4 + 4 * i]; }
+  RMC_HD int nmsg() const { return h_nmsg(S[0]); }
+  RMC_HD uint32_t msg(int k) const { return S[1 + 4 * N + k]; }
+  RMC_HD int term(int i) const { return a_term(A(i)); }
+  RMC_HD int st(int i) const { return a_st(A(i)); }
+  RMC_HD int len(int i) const { return a_len(A(i)); }
+  // index of the message with the same record as w, or -1 (binary search:
+  // DOMAIN is sorted by record)
+  RMC_HD int find(uint32_t w) const {
+    int lo = 0, hi = nmsg() - 1;
+    uint32_t r = msg_rec(w);
+    while (lo <= hi) {
+      int mid = (lo + hi) >> 1;
+      uint32_t x = msg_rec(msg(mid));
+      if (x == r) return mid;
+      if (x < r) lo = mid + 1; else hi = mid - 1;
+    }
+    return -1;
+  }
+};
+
+// log helpers (1-based TLA+ indices; out of domain -> E_DOMAIN)
+RMC_HD int log_term_at(uint32_t a, uint32_t b, int idx, int& err) {
+  if (idx < 1 || idx > a_len(a)) { err = E_DOMAIN; return 0; }
+  return e_term(b, idx - 1);
+}
+RMC_HD int log_value_at(uint32_t a, uint32_t b, int idx, int& err) {
+  if (idx < 1 || idx > a_len(a)) { err = E_DOMAIN; return 0; }
+  return e_value(b, idx - 1);
+}
+RMC_HD int last_term(uint32_t a, uint32_t b) { int L = a_len(a); return L ? e_term(b, L - 1) : 0; }
+RMC_HD void log_append(uint32_t& a, uint32_t& b, int term, int value, int& err) {
+  int L = a_len(a);
+  if (L >= MAXLOG) { err = E_CAP_LOG; return; }
+  b = setb(b, 6 * L, 6, e_pack(term, value));
+  a = setb(a, 9, 3, (uint32_t)(L + 1));
+}
+RMC_HD void log_truncate(uint32_t& a, uint32_t& b, int n) {  // keep entries 1..n (n <= Len)
+  a = setb(a, 9, 3, (uint32_t)n);
+  b &= (n >= 5) ? 0x3FFFFFFFu : ((1u << (6 * n)) - 1u);
+}
+RMC_HD int popc7(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popc(x);
+#else
+  return __builtin_popcount(x);
+#endif
+}
+
+// Emitting message ops into the delta.  Written with compile-time indices so
+// the Delta stays in registers (a runtime-indexed array would go to scratch).
+RMC_HD void push_op(Delta& d, int k, uint32_t c) {
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++)
+    if (q == d.nops) { d.opk[q] = k; d.opc[q] = c; }
+  d.nops++;
+}
+RMC_HD bool ops_have_rec(const Delta& d, uint32_t w) {
+  bool hit = false;
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++)
+    if (q < d.nops && msg_rec(d.opc[q]) == msg_rec(w)) hit = true;
+  return hit;
+}
+template <int SPEC, int N>
+RMC_HD bool op_send_once(const PState<SPEC, N>& s, Delta& d, uint32_t rec1) {
+  // rec1 = record with count 1; disabled if the record is already in DOMAIN
+  if (s.find(rec1) >= 0) return false;
+  if (ops_have_rec(d, rec1)) return false;
+  push_op(d, -1, rec1);
+  return true;
+}
+template <int SPEC, int N>
+RMC_HD void op_send_any(const PState<SPEC, N>& s, Delta& d, uint32_t rec1) {  // _SendNoRestriction
+  int k = s.find(rec1);
+  if (k < 0) { push_op(d, -1, rec1); return; }
+  uint32_t w = s.msg(k);
+  if (msg_count(w) >= 7) { d.err = E_CAP_COUNT; return; }
+  push_op(d, k, w + 1u);
+}
+template <int SPEC, int N>
+RMC_HD bool op_reply(const PState<SPEC, N>& s, Delta& d, uint32_t resp1, int req_k) {
+  // Raft.tla:170-176 (Raft increments an existing response);
+  // FlexibleRaft.tla:148-151, RaftFsync.tla:149-152, PullRaft.tla:158-161 (response must be new)
+  uint32_t req = s.msg(req_k);
+  if (!(msg_count(req) > 0)) return false;
+  int k = s.find(resp1);
+  if (k >= 0 && SPEC != RAFT) return false;
+  push_op(d, req_k, req - 1u);
+  if (k >= 0) {
+    uint32_t w = s.msg(k);
+    if (msg_count(w) >= 7) { d.err = E_CAP_COUNT; return true; }
+    push_op(d, k, w + 1u);
+  } else {
+    push_op(d, -1, resp1);
+  }
+  return true;
+}
+template <int SPEC, int N>
+RMC_HD void op_discard(const PState<SPEC, N>& s, Delta& d, int k) {  // Raft.tla:164-167 (count > 0 checked by caller)
+  push_op(d, k, s.msg(k) - 1u);
+}
+
+template <int SPEC, int N>
+RMC_HD void begin_srv(const PState<SPEC, N>& s, Delta& d, int i) {
+  d.srv = i; d.w[0] = s.A(i); d.w[1] = s.B(i); d.w[2] = s.Cw(i); d.w[3] = s.Dw(i);
+}
+
+RMC_HD uint32_t all_rows(int N, int v) {
+  uint32_t w = 0;
+  for (int j = 0; j < N; j++) w |= (uint32_t)v << (3 * j);
+  return w;
+}
+
+// ---------------------------------------------------------------- actions
+// Each returns true iff the action is enabled for the binding; d receives the
+// successor.  Citations are to /root/reference/specifications/.
+
+template <int SPEC, int N>
+RMC_HD bool act_restart(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {
+  // Raft.tla:226-235; FlexibleRaft.tla:200-208; RaftFsync.tla:203-218; PullRaft.tla:258-265
+  if (!(h_rctr(s.hdr()) < M.R)) return false;
+  begin_srv(s, d, i);
+  uint32_t a = d.w[0];
+  a = setb(a, 4, 2, FOLLOWER);
+  a = setb(a, 18, 7, 0);   // votesGranted[i] = {}
+  a = setb(a, 25, 7, 0);   // pendingResponse[i] = [j |-> FALSE]
+  a = setb(a, 12, 3, 0);   // commitIndex[i] = 0
+  if (SPEC != PULL) d.w[2] = all_rows(N, 1);
+  d.w[3] = 0;
+  if (SPEC == FSYNC) {
+    int f = a_fsync(a), L = a_len(a);
+    if (f == 0) log_truncate(a, d.w[1], 0);
+    else if (L > 0 && L > f) log_truncate(a, d.w[1], f);
+  }
+  d.w[0] = a;
+  int r = h_rctr(s.hdr()) + 1;
+  if (r > 15) { d.err = E_CAP_FIELD; }
+  d.hdr = setb(s.hdr(), 12, 4, (uint32_t)r);
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_requestvote(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {
+  // Raft.tla:242-257 (FlexibleRaft.tla:215-230; PullRaft.tla:283-298 sets leader[i])
+  int ec = h_ectr(s.hdr());
+  if (!(ec < M.E)) return false;
+  int st = s.st(i);
+  if (!(st == FOLLOWER || st == CANDIDATE)) return false;
+  int t1 = s.term(i) + 1;
+  if (t1 > 15) { d.err = E_CAP_TERM; return true; }
+  uint32_t a = s.A(i), b = s.B(i);
+  MsgF m = msg_zero();
+  m.type = RVREQ; m.term = t1; m.llt = last_term(a, b); m.lli = a_len(a); m.src = i; m.count = 1;
+  for (int j = 0; j < N; j++) {
+    if (j == i) continue;
+    m.dst = j;
+    if (!op_send_once(s, d, msg_encode<SPEC>(m))) return false;  // SendMultipleOnce / SendMultiple
+  }
+  begin_srv(s, d, i);
+  a = setb(a, 4, 2, CANDIDATE);
+  a = setb(a, 0, 4, (uint32_t)t1);
+  a = setb(a, 6, 3, (uint32_t)i);
+  a = setb(a, 18, 7, 1u << i);
+  d.w[0] = a;
+  d.hdr = setb(s.hdr(), 8, 4, (uint32_t)(ec + 1));
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_timeout(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {  // RaftFsync.tla:222-230
+  int ec = h_ectr(s.hdr());
+  if (!(ec < M.E)) return false;
+  int st = s.st(i);
+  if (!(st == FOLLOWER || st == CANDIDATE)) return false;
+  int t1 = s.term(i) + 1;
+  if (t1 > 15) { d.err = E_CAP_TERM; return true; }
+  begin_srv(s, d, i);
+  uint32_t a = d.w[0];
+  a = setb(a, 4, 2, CANDIDATE);
+  a = setb(a, 0, 4, (uint32_t)t1);
+  a = setb(a, 6, 3, (uint32_t)i);
+  a = setb(a, 18, 7, 1u << i);
+  d.w[0] = a;
+  d.hdr = setb(s.hdr(), 8, 4, (uint32_t)(ec + 1));
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_rvij(const PState<SPEC, N>& s, const Model& M, int i, int j, Delta& d) {  // RaftFsync.tla:234-243
+  if (s.st(i) != CANDIDATE || i == j) return false;
+  uint32_t a = s.A(i), b = s.B(i);
+  MsgF m = msg_zero();
+  m.type = RVREQ; m.term = a_term(a); m.llt = last_term(a, b); m.lli = a_len(a); m.src = i; m.dst = j; m.count = 1;
+  return op_send_once(s, d, msg_encode<SPEC>(m));
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_appendentries(const PState<SPEC, N>& s, const Model& M, int i, int j, Delta& d) {
+  // Raft.tla:263-285; FlexibleRaft.tla:236-256; RaftFsync.tla:249-272
+  if (i == j || s.st(i) != LEADER) return false;
+  uint32_t a = s.A(i), b = s.B(i);
+  if (SPEC == RAFT && ((a_pending(a) >> j) & 1)) return false;
+  int nxt = row_get(s.Cw(i), j);
+  int prevLogIndex = nxt - 1;
+  int prevLogTerm = prevLogIndex > 0 ? log_term_at(a, b, prevLogIndex, d.err) : 0;
+  if (d.err) return true;
+  int L = a_len(a);
+  int lastEntry = L < nxt ? L : nxt;  // Min({Len(log[i]), nextIndex[i][j]})
+  if (SPEC == FSYNC && M.lfae && !(a_fsync(a) >= lastEntry)) return false;
+  int nent = lastEntry - nxt + 1;   // SubSeq(log[i], nextIndex[i][j], lastEntry)
+  if (nent < 0) nent = 0;
+  MsgF m = msg_zero();
+  m.type = AEREQ; m.term = a_term(a); m.pli = prevLogIndex; m.plt = prevLogTerm; m.nent = nent;
+  if (nent) { m.eterm = log_term_at(a, b, nxt, d.err); m.evalue = log_value_at(a, b, nxt, d.err); }
+  int ci = a_commit(a);
+  m.commit = ci < lastEntry ? ci : lastEntry;
+  m.src = i; m.dst = j; m.count = 1;
+  if (prevLogIndex > 7) { d.err = E_CAP_FIELD; return true; }
+  uint32_t w = msg_encode<SPEC>(m);
+  if (SPEC == RAFT) {
+    if (nent == 0) { if (!op_send_once(s, d, w)) return false; }  // _SendOnce (Raft.tla:146-148)
+    else op_send_any(s, d, w);                                     // _SendNoRestriction
+    begin_srv(s, d, i);
+    d.w[0] = setb(d.w[0], 25 + j, 1, 1);  // pendingResponse[i][j] = TRUE
+  } else {
+    if (!op_send_once(s, d, w)) return false;
+  }
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_becomeleader(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {
+  // Raft.tla:289-300; FlexibleRaft.tla:260-269; RaftFsync.tla:276-285; PullRaft.tla:354-366
+  if (s.st(i) != CANDIDATE) return false;
+  uint32_t a = s.A(i);
+  int vg = a_votes(a);
+  bool q = SPEC == FLEX ? popc7((uint32_t)vg) >= M.EQ : popc7((uint32_t)vg) * 2 > N;
+  if (!q) return false;
+  if (SPEC == PULL) {
+    MsgF m = msg_zero();
+    m.type = LNREQ; m.term = a_term(a); m.src = i; m.count = 1;
+    for (int j = 0; j < N; j++) {
+      if ((vg >> j) & 1) continue;
+      m.dst = j;
+      if (!op_send_once(s, d, msg_encode<SPEC>(m))) return false;
+    }
+  }
+  begin_srv(s, d, i);
+  d.w[0] = setb(d.w[0], 4, 2, LEADER);
+  if (SPEC == RAFT) d.w[0] = setb(d.w[0], 25, 7, 0);
+  if (SPEC != PULL) {
+    int nx = a_len(a) + 1;
+    if (nx > 7) { d.err = E_CAP_FIELD; return true; }
+    d.w[2] = all_rows(N, nx);
+  }
+  d.w[3] = 0;
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_client(const PState<SPEC, N>& s, const Model& M, int i, int v, Delta& d) {  // Raft.tla:304-313
+  if (s.st(i) != LEADER || h_acked(s.hdr(), v) != 0) return false;
+  begin_srv(s, d, i);
+  log_append(d.w[0], d.w[1], s.term(i), v, d.err);
+  d.hdr = setb(s.hdr(), 16 + 2 * v, 2, 1);  // acked[v] = FALSE
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD int new_commit_index(const PState<SPEC, N>& s, const Model& M, int i, uint32_t matchrow, int& err) {
+  // Raft.tla:322-335 / RaftFsync.tla:313-327 / FlexibleRaft.tla:296 / PullRaft.tla:446-458
+  uint32_t a = s.A(i), b = s.B(i);
+  int best = 0;
+  for (int index = 1; index <= a_len(a); index++) {
+    uint32_t set = 0;
+    for (int k = 0; k < N; k++)
+      if (row_get(matchrow, k) >= index) set |= 1u << k;
+    if (!(SPEC == FSYNC && M.lfiq && index > a_fsync(a))) set |= 1u << i;
+    int c = popc7(set);
+    bool q = SPEC == FLEX ? c >= M.RQ : c * 2 > N;
+    if (q) best = index;
+  }
+  if (best > 0 && log_term_at(a, b, best, err) == a_term(a)) return best;
+  return a_commit(a);
+}
+
+template <int SPEC, int N>
+RMC_HD uint32_t acked_after_commit(const PState<SPEC, N>& s, const Model& M, int i, int newCommit, int& err) {
+  // acked' = [v |-> IF acked[v] = FALSE THEN v \in {log[i][k].value : k \in commitIndex[i]+1..new} ELSE acked[v]]
+  uint32_t h = s.hdr();
+  uint32_t a = s.A(i), b = s.B(i);
+  for (int v = 0; v < M.V; v++) {
+    if (h_acked(s.hdr(), v) != 1) continue;
+    bool in = false;
+    for (int k = a_commit(a) + 1; k <= newCommit; k++)
+      if (log_value_at(a, b, k, err) == v) in = true;
+    h = setb(h, 16 + 2 * v, 2, in ? 2u : 1u);
+  }
+  return h;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_advcommit(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {  // Raft.tla:320-344
+  if (s.st(i) != LEADER) return false;
+  int nc = new_commit_index(s, M, i, s.Dw(i), d.err);
+  if (d.err) return true;
+  if (!(a_commit(s.A(i)) < nc)) return false;
+  d.hdr = acked_after_commit(s, M, i, nc, d.err);
+  begin_srv(s, d, i);
+  d.w[0] = setb(d.w[0], 12, 3, (uint32_t)nc);
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_advfsync(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {  // RaftFsync.tla:339-343
+  uint32_t a = s.A(i);
+  if (!(a_fsync(a) < a_len(a))) return false;
+  begin_srv(s, d, i);
+  d.w[0] = setb(a, 15, 3, (uint32_t)(a_fsync(a) + 1));
+  return true;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_sendpull(const PState<SPEC, N>& s, const Model& M, int i, int j, Delta& d) {  // PullRaft.tla:396-411
+  uint32_t a = s.A(i), b = s.B(i);
+  if (i == j || a_st(a) != FOLLOWER || a_voted(a) != j) return false;
+  int lli = a_len(a);
+  int llt = lli > 0 ? log_term_at(a, b, lli, d.err) : 0;
+  MsgF m = msg_zero();
+  m.type = PEREQ; m.term = a_term(a); m.lli = lli; m.llt = llt; m.src = i; m.dst = j; m.count = 1;
+  return op_send_once(s, d, msg_encode<SPEC>(m));
+}
+
+// ---- message-bound actions: exactly one can be enabled per DOMAIN element
+template <int SPEC, int N>
+RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
+  uint32_t w = s.msg(k);
+  MsgF m = msg_decode<SPEC>(w);
+  int i = m.dst, j = m.src;
+  uint32_t a = s.A(i), b = s.B(i);
+  int cur = a_term(a);
+  if (m.term > cur) {
+    // UpdateTerm: Raft.tla:348-355 / PullRaft.tla:269-276 (count not required)
+    d.act = A_UPDATETERM;
+    begin_srv(s, d, i);
+    uint32_t x = setb(a, 0, 4, (uint32_t)m.term);
+    x = setb(x, 4, 2, FOLLOWER);
+    x = setb(x, 6, 3, NILS);
+    d.w[0] = x;
+    return true;
+  }
+  if (!(m.count > 0)) return false;  // ReceivableMessage: messages[m] > 0 (Raft.tla:182)
+  int st = a_st(a);
+  switch (m.type) {
+    case RVREQ: {
+      // HandleRequestVoteRequest: Raft.tla:360-381; PullRaft.tla:306-330 (mterm <= currentTerm)
+      d.act = A_HRVREQ;
+      int lt = last_term(a, b);
+      bool logOk = m.llt > lt || (m.llt == lt && m.lli >= a_len(a));
+      int vf = a_voted(a);
+      bool grant = m.term == cur && logOk && (vf == NILS || vf == j);
+      MsgF r = msg_zero();
+      r.type = RVRESP; r.term = cur; r.granted = grant; r.src = i; r.dst = j; r.count = 1;
+      if (!op_reply(s, d, msg_encode<SPEC>(r), k)) return false;
+      if (grant) { begin_srv(s, d, i); d.w[0] = setb(a, 6, 3, (uint32_t)j); }
+      return true;
+    }
+    case RVRESP: {
+      // HandleRequestVoteResponse: Raft.tla:386-401 (EqualTerm)
+      if (m.term != cur) return false;
+      d.act = A_HRVRESP;
+      if (m.granted) { begin_srv(s, d, i); d.w[0] = setb(a, 18 + j, 1, 1); }
+      op_discard(s, d, k);
+      return true;
+    }
+    case AEREQ: {
+      // LogOk: Raft.tla:406-410
+      bool logOk;
+      if (m.pli == 0) logOk = true;
+      else logOk = m.pli > 0 && m.pli <= a_len(a) && m.plt == e_term(b, m.pli - 1);
+      if (m.term < cur || (m.term == cur && st == FOLLOWER && !logOk)) {
+        // RejectAppendEntriesRequest: Raft.tla:412-430
+        d.act = A_REJAE;
+        MsgF r = msg_zero();
+        r.type = AERESP; r.term = cur; r.success = 0; r.midx = 0; r.src = i; r.dst = j; r.count = 1;
+        return op_reply(s, d, msg_encode<SPEC>(r), k);
+      }
+      if (m.term != cur || !(st == FOLLOWER || st == CANDIDATE) || !logOk) return false;
+      // AcceptAppendEntriesRequest: Raft.tla:454-485; FlexibleRaft.tla:421-450; RaftFsync.tla:449-481
+      d.act = A_ACCAE;
+      int L = a_len(a);
+      int index = m.pli + 1;
+      bool canAppend = m.nent != 0 && L == m.pli;
+      uint32_t na = a, nb = b;
+      if (SPEC == RAFT) {
+        bool needs = (m.nent != 0 && L >= index) || (m.nent == 0 && L > m.pli);
+        if (canAppend) log_append(na, nb, m.eterm, m.evalue, d.err);
+        else if (needs && m.nent != 0) { log_truncate(na, nb, m.pli); log_append(na, nb, m.eterm, m.evalue, d.err); }
+        else if (needs && m.nent == 0) log_truncate(na, nb, m.pli);
+      } else {
+        bool needs = m.nent != 0 && L >= index && e_term(b, index - 1) != m.eterm;
+        if (canAppend) log_append(na, nb, m.eterm, m.evalue, d.err);
+        else if (needs) { log_truncate(na, nb, m.pli); log_append(na, nb, m.eterm, m.evalue, d.err); }
+      }
+      na = setb(na, 4, 2, FOLLOWER);
+      na = setb(na, 12, 3, (uint32_t)m.commit);
+      if (SPEC == FSYNC && M.ffbr) na = setb(na, 15, 3, (uint32_t)a_len(na));
+      MsgF r = msg_zero();
+      r.type = AERESP; r.term = cur; r.success = 1; r.midx = m.pli + m.nent; r.src = i; r.dst = j; r.count = 1;
+      if (r.midx > 7) { d.err = E_CAP_FIELD; return true; }
+      if (!op_reply(s, d, msg_encode<SPEC>(r), k)) return false;
+      d.srv = i; d.w[0] = na; d.w[1] = nb; d.w[2] = s.Cw(i); d.w[3] = s.Dw(i);
+      return true;
+    }
+    case AERESP: {
+      // HandleAppendEntriesResponse: Raft.tla:490-505 (EqualTerm)
+      if (m.term != cur) return false;
+      d.act = A_HAERESP;
+      begin_srv(s, d, i);
+      if (m.success) {
+        if (m.midx + 1 > 7) { d.err = E_CAP_FIELD; return true; }
+        d.w[2] = row_set(d.w[2], j, m.midx + 1);
+        d.w[3] = row_set(d.w[3], j, m.midx);
+      } else {
+        int nx = row_get(d.w[2], j) - 1;
+        d.w[2] = row_set(d.w[2], j, nx > 1 ? nx : 1);
+      }
+      if (SPEC == RAFT) d.w[0] = setb(d.w[0], 25 + j, 1, 0);
+      op_discard(s, d, k);
+      return true;
+    }
+    case LNREQ: {
+      // LearnOfLeader: PullRaft.tla:383-391 (EqualTerm)
+      if (m.term != cur) return false;
+      d.act = A_LEARN;
+      begin_srv(s, d, i);
+      d.w[0] = setb(a, 6, 3, (uint32_t)j);
+      op_discard(s, d, k);
+      return true;
+    }
+    case PEREQ: {
+      if (m.term != cur || st != LEADER) return false;
+      // ValidPullPosition: PullRaft.tla:192-196
+      bool valid;
+      if (m.lli == 0) valid = true;
+      else valid = m.lli > 0 && m.lli <= a_len(a) && m.llt == e_term(b, m.lli - 1);
+      if (!valid) {
+        // RejectPullEntriesRequest: PullRaft.tla:418-436, LastCommonEntry :211-226
+        d.act = A_REJPULL;
+        int idx = 0;
+        for (int x = 1; x <= a_len(a); x++) {
+          int t = e_term(b, x - 1);
+          int cmp = t > m.llt ? 1 : (t == m.llt && x > m.lli) ? 1 : (t == m.llt && x == m.lli) ? 0 : -1;
+          if (cmp <= 0) idx = x;
+        }
+        MsgF r = msg_zero();
+        r.type = PERESP; r.term = cur; r.success = 0; r.lci = idx; r.lct = idx ? e_term(b, idx - 1) : 0;
+        r.src = i; r.dst = j; r.count = 1;
+        return op_reply(s, d, msg_encode<SPEC>(r), k);
+      }
+      int index = m.lli + 1;
+      if (!(index <= a_len(a))) return false;
+      // AcceptPullEntriesRequest: PullRaft.tla:460-488
+      d.act = A_ACCPULL;
+      uint32_t nm = row_set(s.Dw(i), j, m.lli);
+      int nc = new_commit_index(s, M, i, nm, d.err);
+      uint32_t hdr = acked_after_commit(s, M, i, nc, d.err);
+      MsgF r = msg_zero();
+      r.type = PERESP; r.term = cur; r.success = 1; r.nent = 1;
+      r.eterm = e_term(b, index - 1); r.evalue = e_value(b, index - 1);
+      r.commit = nc < index ? nc : index;
+      r.src = i; r.dst = j; r.count = 1;
+      if (!op_reply(s, d, msg_encode<SPEC>(r), k)) return false;
+      d.hdr = hdr;
+      begin_srv(s, d, i);
+      d.w[3] = nm;
+      d.w[0] = setb(d.w[0], 12, 3, (uint32_t)nc);
+      return true;
+    }
+    case PERESP: {
+      if (m.term != cur) return false;
+      begin_srv(s, d, i);
+      if (m.success) {
+        // HandleSuccessPullEntriesResponse: PullRaft.tla:493-503
+        d.act = A_HSUCC;
+        d.w[0] = setb(d.w[0], 12, 3, (uint32_t)m.commit);
+        log_append(d.w[0], d.w[1], m.eterm, m.evalue, d.err);
+      } else {
+        // HandleFailPullEntriesResponse: PullRaft.tla:510-520, TruncateLog :185-188
+        d.act = A_HFAIL;
+        if (m.lci > a_len(a)) { d.err = E_DOMAIN; return true; }
+        log_truncate(d.w[0], d.w[1], m.lci);
+      }
+      op_discard(s, d, k);
+      return true;
+    }
+  }
+  return false;
+}
+
+// Evaluate binding b (fixed bindings first, then one per DOMAIN element).
+template <int SPEC, int N>
+RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta& d) {
+  d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
+  if (b < M.nfixed) {
+    int slot = M.fb_act[b], x = M.fb_x[b];
+    int act = M.act_id[slot];
+    d.act = act;
+    d.ordinal = M.act_off[slot] + x;
+    int i = x % N, jv = x / N;  // first bound variable fastest
+    switch (act) {
+      case A_RESTART: return act_restart(s, M, i, d);
+      case A_REQUESTVOTE: return act_requestvote(s, M, i, d);
+      case A_TIMEOUT: return act_timeout(s, M, i, d);
+      case A_RVIJ: return act_rvij(s, M, i, jv, d);
+      case A_BECOMELEADER: return act_becomeleader(s, M, i, d);
+      case A_CLIENT: return act_client(s, M, i, jv, d);
+      case A_ADVCOMMIT: return act_advcommit(s, M, i, d);
+      case A_APPENDENTRIES: return act_appendentries(s, M, i, jv, d);
+      case A_ADVFSYNC: return act_advfsync(s, M, i, d);
+      case A_SENDPULL: return act_sendpull(s, M, i, jv, d);
+    }
+    return false;
+  }
+  int k = b - M.nfixed;
+  d.act = -1;
+  bool en = act_message(s, M, k, d);
+  if (en) d.ordinal = M.act_off[M.msg_act_slot[d.act]] + k;
+  return en;
+}
+
+// Apply a delta: out = successor words (M.words), messages re-sorted.
+template <int SPEC, int N>
+RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d, uint32_t* out) {
+  const int W0 = 1 + 4 * N;
+  for (int q = 0; q < W0; q++) out[q] = s.S[q];
+  if (d.srv >= 0) for (int t = 0; t < 4; t++) out[1 + 4 * d.srv + t] = d.w[t];
+  int n = s.nmsg();
+  uint32_t* mo = out + W0;
+  for (int k = 0; k < n; k++) mo[k] = s.msg(k);
+  int nn = n;
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++)
+    if (q < d.nops && d.opk[q] >= 0) mo[d.opk[q]] = d.opc[q];
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++) {
+    if (q >= d.nops || d.opk[q] >= 0) continue;
+    if (nn >= M.kmax) return E_CAP_MSG;
+    uint32_t w = d.opc[q];
+    int p = nn;
+    while (p > 0 && mo[p - 1] > w) { mo[p] = mo[p - 1]; p--; }
+    mo[p] = w;
+    nn++;
+  }
+  for (int k = nn; k < M.kmax; k++) mo[k] = 0;
+  out[0] = (d.hdr & ~0xFFu) | (uint32_t)nn;
+  return E_NONE;
+}
+
+// ------------------------------------------------------------- invariants
+template <int SPEC, int N>
+RMC_HD bool inv_no_log_divergence(const PState<SPEC, N>& s, int& err) {  // Raft.tla:588-596
+  for (int s2 = 0; s2 < N; s2++)
+    for (int s1 = 0; s1 < N; s1++) {
+      if (s1 == s2) continue;
+      uint32_t a1 = s.A(s1), a2 = s.A(s2);
+      int c = a_commit(a1) < a_commit(a2) ? a_commit(a1) : a_commit(a2);
+      for (int idx = 1; idx <= c; idx++) {
+        if (idx > a_len(a1) || idx > a_len(a2)) { err = E_DOMAIN; return true; }
+        if (((s.B(s1) >> (6 * (idx - 1))) & 63u) != ((s.B(s2) >> (6 * (idx - 1))) & 63u)) return false;
+      }
+    }
+  return true;
+}
+template <int SPEC, int N>
+RMC_HD bool inv_leader_has_all_acked(const PState<SPEC, N>& s, const Model& M) {  // Raft.tla:604-620
+  for (int v = 0; v < M.V; v++) {
+    if (h_acked(s.hdr(), v) != 2) continue;
+    for (int i = 0; i < N; i++) {
+      uint32_t a = s.A(i);
+      if (a_st(a) != LEADER) continue;
+      bool newer = false;
+      for (int l = 0; l < N; l++)
+        if (l != i && s.term(l) > a_term(a)) newer = true;
+      if (newer) continue;
+      bool has = false;
+      for (int x = 0; x < a_len(a); x++)
+        if (e_value(s.B(i), x) == v) has = true;
+      if (!has) return false;
+    }
+  }
+  return true;
+}
+template <int SPEC, int N>
+RMC_HD bool inv_committed_majority(const PState<SPEC, N>& s, int& err) {  // Raft.tla:625-636
+  bool any = false;
+  for (int i = 0; i < N; i++) if (s.st(i) == LEADER && a_commit(s.A(i)) > 0) any = true;
+  if (!any) return true;
+  int size = N / 2 + 1;
+  for (int i = 0; i < N; i++) {
+    uint32_t ai = s.A(i);
+    if (!(a_st(ai) == LEADER && a_commit(ai) > 0)) continue;
+    int ci = a_commit(ai);
+    for (uint32_t q = 0; q < (1u << N); q++) {
+      if (popc7(q) != size || !((q >> i) & 1u)) continue;
+      bool ok = true;
+      for (int j = 0; j < N && ok; j++) {
+        if (!((q >> j) & 1u)) continue;
+        if (!(a_len(s.A(j)) >= ci)) { ok = false; break; }
+        if (ci > a_len(ai)) { err = E_DOMAIN; return true; }
+        if (((s.B(j) >> (6 * (ci - 1))) & 63u) != ((s.B(i) >> (6 * (ci - 1))) & 63u)) ok = false;
+      }
+      if (ok) return true;
+    }
+  }
+  return false;
+}
+// returns -1 if all hold, else the position (in cfg order) of the violated one
+template <int SPEC, int N>
+RMC_HD int check_invariants(const PState<SPEC, N>& s, const Model& M, int& err) {
+  for (int q = 0; q < M.ninv; q++) {
+    bool ok = true;
+    switch (M.inv[q]) {
+      case 0: ok = inv_leader_has_all_acked(s, M); break;
+      case 1: ok = inv_no_log_divergence(s, err); break;
+      case 2: ok = inv_committed_majority(s, err); break;
+    }
+    if (err) return -2;
+    if (!ok) return q;
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------- hashing
+// fp(s) = min over server permutations pi of mix(H_pi(s)), where H_pi is a sum
+// of per-server and per-message 64-bit hashes of pi(s)'s view.  H_pi is an
+// additive (multiset) hash, so a successor's H_pi is the parent's plus the
+// delta's contribution; min over all of S_N makes fp a function of the view
+// orbit (VIEW + SYMMETRY, Raft.tla:115-116).
+RMC_HD uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+RMC_HD int perm_of(uint32_t P, int j) { return (int)((P >> (3 * j)) & 7u); }
+
+template <int N>
+RMC_HD uint32_t relabel_set(uint32_t set, uint32_t P) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < N; j++)
+    if ((set >> j) & 1u) o |= 1u << perm_of(P, j);
+  return o;
+}
+template <int N>
+RMC_HD uint32_t relabel_row(uint32_t row, uint32_t P) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < N; j++) o |= ((row >> (3 * j)) & 7u) << (3 * perm_of(P, j));
+  return o;
+}
+template <int SPEC, int N>
+RMC_HD uint64_t h_server(uint32_t P, int i, uint32_t a, uint32_t b, uint32_t c, uint32_t dd) {
+  int v = a_voted(a);
+  uint32_t a2 = setb(a, 6, 3, v == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v));
+  a2 = setb(a2, 18, 7, relabel_set<N>(a_votes(a), P));
+  a2 = setb(a2, 25, 7, relabel_set<N>(a_pending(a), P));
+  uint64_t lo = (uint64_t)a2 | ((uint64_t)b << 32);
+  uint64_t hi = (uint64_t)relabel_row<N>(c, P) | ((uint64_t)relabel_row<N>(dd, P) << 32);
+  int pos = perm_of(P, i);
+  return mix64(mix64(lo + 0x9E3779B97F4A7C15ULL * (uint64_t)(pos + 1)) ^ hi);
+}
+template <int SPEC>
+RMC_HD uint64_t h_msg(uint32_t P, uint32_t w) {
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  uint32_t s = (w >> sp) & 7u, d = (w >> dp) & 7u;
+  uint32_t w2 = (w & ~((7u << sp) | (7u << dp))) | ((uint32_t)perm_of(P, (int)s) << sp) | ((uint32_t)perm_of(P, (int)d) << dp);
+  return mix64((uint64_t)w2 * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
+}
+RMC_HD uint64_t h_acked_view(uint32_t hdr) {  // PullRaft's view includes acked (PullRaft.tla:123)
+  return mix64(((uint64_t)(hdr >> 16) & 0xFFu) + 0xE7037ED1A0B428DBULL);
+}
+
+}  // namespace rmc

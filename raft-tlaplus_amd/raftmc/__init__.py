@@ -1,0 +1,179 @@
+"""raftmc — Python binding of librmc (ctypes over include/rmc.h).
+
+Mirrors the reference's operator interface for this path, which is TLC's
+command line: `tlc2.TLC -deadlock [-workers N] [-config M.cfg] M.tla`
+(/root/reference/README.md:6).  `check(tla, cfg)` returns TLC's three counts
+(states generated, distinct states, depth), the states left on the queue,
+and on an invariant violation the invariant name and the behaviour (a list of
+(action label, TLA+ state text)) as TLC prints it.
+
+The HIP path is the only path: if librmc.so is missing or no GPU is present,
+calls fail loudly (RaftmcError); there is no CPU fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "librmc.so")
+
+STATUS = {0: "ok", 1: "violation", 2: "error", 3: "capacity", 4: "stopped"}
+
+
+class RaftmcError(RuntimeError):
+    pass
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("n_gpus", ctypes.c_int), ("cpu_workers", ctypes.c_int),
+                ("deadlock_check", ctypes.c_int), ("fp_bits", ctypes.c_int),
+                ("tlc_order", ctypes.c_int), ("hash_slots", ctypes.c_uint64),
+                ("msg_cap_K", ctypes.c_uint32), ("frontier_cap", ctypes.c_uint64),
+                ("chunk_parents", ctypes.c_uint32), ("verbose", ctypes.c_int),
+                ("max_depth", ctypes.c_int)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("generated", ctypes.c_uint64), ("distinct", ctypes.c_uint64),
+                ("left_on_queue", ctypes.c_uint64), ("depth", ctypes.c_uint32),
+                ("status", ctypes.c_int), ("violated", ctypes.c_char * 64),
+                ("message", ctypes.c_char * 256),
+                ("hidden_var_collisions", ctypes.c_uint64), ("seconds", ctypes.c_double),
+                ("expand_ms", ctypes.c_double), ("mark_ms", ctypes.c_double),
+                ("materialize_ms", ctypes.c_double), ("expand_launches", ctypes.c_uint64),
+                ("state_bytes", ctypes.c_uint32), ("max_msgs", ctypes.c_uint32),
+                ("hash_capacity", ctypes.c_uint64)]
+
+
+# every entry point include/rmc.h declares (checked by tests/test_abi.py)
+EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_check",
+           "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
+           "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels"]
+
+_lib = None
+
+
+def lib():
+    """Load librmc.so (built in-tree by `make -C raft-tlaplus_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RaftmcError("librmc.so not built: run `make -C raft-tlaplus_amd` (expected %s)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, c_int, c_size_t = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    L.rmc_model_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(P), ctypes.c_char_p, c_size_t]
+    L.rmc_model_load_text.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(P), ctypes.c_char_p, c_size_t]
+    L.rmc_options_default.argtypes = [ctypes.POINTER(Options)]
+    L.rmc_check.argtypes = [P, ctypes.POINTER(Options), ctypes.POINTER(Result)]
+    L.rmc_trace_len.argtypes = [P]
+    L.rmc_trace_state.argtypes = [P, c_int, ctypes.c_char_p, c_size_t]
+    L.rmc_trace_action.argtypes = [P, c_int, ctypes.c_char_p, c_size_t]
+    L.rmc_format_report.argtypes = [P, ctypes.POINTER(Result), ctypes.c_char_p, c_size_t]
+    L.rmc_model_free.argtypes = [P]
+    L.rmc_last_error.restype = ctypes.c_char_p
+    L.rmc_version.restype = ctypes.c_char_p
+    L.rmc_levels.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), c_int]
+    L.rmc_selftest_host_bfs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64,
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), c_int]
+    L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
+    _lib = L
+    return L
+
+
+class Model:
+    """A spec + cfg loaded into librmc (TLC's parse/bind step)."""
+
+    def __init__(self, tla_path=None, cfg_path=None, module=None, cfg_text=None):
+        L = lib()
+        err = ctypes.create_string_buffer(512)
+        h = ctypes.c_void_p()
+        if cfg_text is not None:
+            rc = L.rmc_model_load_text(module.encode(), cfg_text.encode(), ctypes.byref(h), err, 512)
+        else:
+            rc = L.rmc_model_load(tla_path.encode(), cfg_path.encode() if cfg_path else None,
+                                  ctypes.byref(h), err, 512)
+        if rc != 0:
+            raise RaftmcError(err.value.decode())
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rmc_model_free(self._h)
+            self._h = None
+
+    def check(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
+              chunk_parents=0, verbose=False, max_depth=0, workers=0):
+        """Run the model check on the GPU; returns a dict of TLC's results."""
+        L = lib()
+        o = Options()
+        L.rmc_options_default(ctypes.byref(o))
+        o.deadlock_check = 1 if deadlock else 0
+        o.hash_slots, o.msg_cap_K, o.frontier_cap = hash_slots, msg_cap_K, frontier_cap
+        o.chunk_parents, o.verbose, o.max_depth, o.cpu_workers = chunk_parents, int(verbose), max_depth, workers
+        r = Result()
+        rc = L.rmc_check(self._h, ctypes.byref(o), ctypes.byref(r))
+        if rc != 0:
+            raise RaftmcError(L.rmc_last_error().decode())
+        levels = (ctypes.c_uint64 * 2048)()
+        nl = L.rmc_levels(self._h, levels, 1024)
+        out = dict(generated=r.generated, distinct=r.distinct, depth=r.depth,
+                   left=r.left_on_queue, status=STATUS.get(r.status, str(r.status)),
+                   violated=r.violated.decode(), message=r.message.decode(),
+                   seconds=r.seconds, expand_ms=r.expand_ms, mark_ms=r.mark_ms,
+                   materialize_ms=r.materialize_ms, expand_launches=r.expand_launches,
+                   state_bytes=r.state_bytes, hash_capacity=r.hash_capacity,
+                   levels=[[levels[2 * k], levels[2 * k + 1]] for k in range(min(nl, 1024))])
+        self._last = r
+        if r.status in (1, 2):
+            out["trace"] = self.trace()
+        return out
+
+    def trace(self):
+        L = lib()
+        n = L.rmc_trace_len(self._h)
+        buf = ctypes.create_string_buffer(1 << 20)
+        tr = []
+        for k in range(max(n, 0)):
+            L.rmc_trace_action(self._h, k, buf, len(buf))
+            act = buf.value.decode()
+            L.rmc_trace_state(self._h, k, buf, len(buf))
+            tr.append((act, buf.value.decode()))
+        return tr
+
+    def report(self):
+        L = lib()
+        buf = ctypes.create_string_buffer(1 << 22)
+        L.rmc_format_report(self._h, ctypes.byref(self._last), buf, len(buf))
+        return buf.value.decode()
+
+    def selftest_host_bfs(self, kmax=0, max_distinct=0):
+        """TEST HOOK: sequential host BFS over the same lowered actions (not a product path)."""
+        L = lib()
+        out3 = (ctypes.c_uint64 * 3)()
+        levels = (ctypes.c_uint64 * 4096)()
+        rc = L.rmc_selftest_host_bfs(self._h, kmax, max_distinct, out3, levels, 2048)
+        if rc == -1:
+            raise RaftmcError(L.rmc_last_error().decode())
+        res = dict(generated=out3[0], distinct=out3[1], depth=out3[2], rc=rc)
+        if rc > 0:
+            res["levels"] = [[levels[2 * k], levels[2 * k + 1]] for k in range(min(rc, 2048))]
+        return res
+
+
+def check(tla_path, cfg_path=None, **kw):
+    """TLC-equivalent run: check(M.tla, M.cfg) -> dict (generated, distinct, depth, ...)."""
+    return Model(tla_path, cfg_path).check(**kw)
+
+
+def check_text(module, cfg_text, **kw):
+    return Model(module=module, cfg_text=cfg_text).check(**kw)
+
+
+def encode_msg(spec, **f):
+    """TEST HOOK: the packed word for a message record + codec self-consistency flag."""
+    names = ["type", "term", "src", "dst", "lli", "llt", "granted", "pli", "plt", "nent", "eterm",
+             "evalue", "commit", "success", "midx", "lci", "lct", "count"]
+    arr = (ctypes.c_int * 18)(*[int(f.get(n, 0)) for n in names])
+    out = ctypes.c_uint32()
+    ok = lib().rmc_selftest_encode_msg(spec, arr, ctypes.byref(out))
+    return out.value, ok == 0

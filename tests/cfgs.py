@@ -1,0 +1,53 @@
+"""cfg texts for the parity cases (TLC .cfg syntax, same grammar as the reference cfgs)."""
+
+FSYNC_FLAGS = dict(LeaderFsyncBeforeAppendEntries=False, LeaderFsyncBeforeIncludeInQuorum=True,
+                   FollowerFsyncBeforeReply=True)
+
+
+def cfg_text(module, n=3, v=1, E=2, R=0, inv=("LeaderHasAllAckedValues", "NoLogDivergence"),
+             symmetry=True, **extra):
+    lines = ["CONSTANTS"]
+    lines += ["    n%d = n%d" % (i, i) for i in range(1, n + 1)]
+    lines += ["    v%d = v%d" % (i, i) for i in range(1, v + 1)]
+    lines.append("    Server = {%s}" % ", ".join("n%d" % i for i in range(1, n + 1)))
+    lines.append("    Value = {%s}" % ", ".join("v%d" % i for i in range(1, v + 1)))
+    for k in ("Follower", "Candidate", "Leader", "Nil", "EqualTerm", "LessOrEqualTerm"):
+        lines.append("    %s = %s" % (k, k))
+    lines.append("    MaxElections = %d" % E)
+    lines.append("    MaxRestarts = %d" % R)
+    if module == "RaftFsync":
+        for k, val in dict(FSYNC_FLAGS, **extra).items():
+            lines.append("    %s = %s" % (k, "TRUE" if val else "FALSE"))
+    elif module == "FlexibleRaft":
+        lines.append("    ElectionQuorumSize = %d" % extra.get("ElectionQuorumSize", n // 2 + 1))
+        lines.append("    ReplicationQuorumSize = %d" % extra.get("ReplicationQuorumSize", n // 2 + 1))
+    lines += ["INIT Init", "NEXT Next", "VIEW view"]
+    if symmetry:
+        lines.append("SYMMETRY symmServers")
+    lines.append("INVARIANT")
+    lines += list(inv)
+    return "\n".join(lines) + "\n"
+
+
+# (name, module, kwargs): small parity cases (oracle seconds), covering every spec
+SMALL = [
+    ("raft_n3v1e1", "Raft", dict(n=3, v=1, E=1)),
+    ("raft_n2v1e2", "Raft", dict(n=2, v=1, E=2)),
+    ("raft_n3v1e1r1", "Raft", dict(n=3, v=1, E=1, R=1)),
+    ("raft_n2v2e2", "Raft", dict(n=2, v=2, E=2)),
+    ("pull_n3v1e1", "PullRaft", dict(n=3, v=1, E=1)),
+    ("pull_n3v2e1", "PullRaft", dict(n=3, v=2, E=1)),
+    ("pull_n2v1e2r1", "PullRaft", dict(n=2, v=1, E=2, R=1)),
+    ("fsync_n3v1e1", "RaftFsync", dict(n=3, v=1, E=1)),
+    ("fsync_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1)),
+    ("flex_n3v1e1", "FlexibleRaft", dict(n=3, v=1, E=1, ElectionQuorumSize=2, ReplicationQuorumSize=2)),
+    ("flex_n2v1e2", "FlexibleRaft", dict(n=2, v=1, E=2, ElectionQuorumSize=2, ReplicationQuorumSize=1)),
+]
+
+# medium cases: C oracle only (too slow for the literal Python oracle)
+MEDIUM = [
+    ("flex_n4v1e1", "FlexibleRaft", dict(n=4, v=1, E=1, ElectionQuorumSize=3, ReplicationQuorumSize=2)),
+    ("pull_n3v1e2r1", "PullRaft", dict(n=3, v=1, E=2, R=1)),
+    ("fsync_n3v1e2_unsafe", "RaftFsync", dict(n=3, v=1, E=2, R=1, FollowerFsyncBeforeReply=False)),
+    ("raft_n4v1e1", "Raft", dict(n=4, v=1, E=1)),
+]

@@ -1,0 +1,86 @@
+"""Generate the committed golden fixtures (tests/golden/*.json).
+
+Run in the build container (needs oracle/_build/rmc_oracle: `make -C oracle`):
+    python tests/golden/make_golden.py [--shipped]
+
+Every SMALL case is computed twice, by the literal Python oracle and by the
+C oracle, and written only if the two agree on generated/distinct/depth and
+every per-level count.  --shipped adds the shipped reference configs (C oracle
+only; minutes of CPU).  The reference itself records no counts anywhere
+(SURVEY.md §4, §8c): these vectors are pinned by the hand-derived first levels
+of SURVEY.md Appendix B plus the agreement of two independent restatements.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from oracle import run_c  # noqa: E402
+from oracle.pyoracle import make_spec  # noqa: E402
+from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
+from oracle.pyoracle.tlc import bfs  # noqa: E402
+from cfgs import MEDIUM, SMALL, cfg_text  # noqa: E402
+
+SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
+    ("Raft_cfg", "Raft", "configs/Raft.cfg"),
+    ("PullRaft_cfg", "PullRaft", "configs/PullRaft.cfg"),
+    ("RaftFsync_cfg", "RaftFsync", "configs/RaftFsync.cfg"),
+]
+
+
+def main():
+    out = {}
+    for name, module, kw in SMALL:
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=4)
+        spec = make_spec(module, cfg)
+        p = bfs(spec)
+        pr = (p.generated, p.distinct, p.depth, p.status, [list(x) for x in p.levels])
+        cr = (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"])
+        if pr != cr:
+            raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pr[:4], cr[:4]))
+        out[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"],
+                         depth=c["depth"], status=c["status"], levels=c["levels"],
+                         action_counts=c["action_counts"], max_msgs=c["max_msgs"],
+                         hidden_same_level=c["hidden_same_level"], pinned_by="pyoracle==coracle")
+        print(name, c["generated"], c["distinct"], c["depth"], flush=True)
+    with open(os.path.join(HERE, "small.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    med = {}
+    for name, module, kw in MEDIUM:
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=8, extra=["--trace"])
+        med[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"],
+                         depth=c["depth"], status=c["status"], levels=c["levels"], violated=c["violated"],
+                         action_counts=c["action_counts"], max_msgs=c["max_msgs"],
+                         hidden_same_level=c["hidden_same_level"], pinned_by="coracle",
+                         trace_len=len(c.get("trace", [])))
+        print(name, c["generated"], c["distinct"], c["depth"], c["status"], c["violated"], flush=True)
+    with open(os.path.join(HERE, "medium.json"), "w") as f:
+        json.dump(med, f, indent=1, sort_keys=True)
+    if "--shipped" in sys.argv:
+        ship = {}
+        for name, module, path in SHIPPED:
+            with open(os.path.join(ROOT, path)) as fh:
+                txt = fh.read()
+            cfg = parse_cfg(txt)
+            c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=8)
+            ship[name] = dict(module=module, cfg_path=path, generated=c["generated"], distinct=c["distinct"],
+                              depth=c["depth"], status=c["status"], levels=c["levels"],
+                              action_counts=c["action_counts"], max_msgs=c["max_msgs"],
+                              hidden_same_level=c["hidden_same_level"],
+                              hidden_cross_level=c["hidden_cross_level"], pinned_by="coracle",
+                              oracle_seconds=c["seconds"])
+            print(name, c["generated"], c["distinct"], c["depth"], flush=True)
+        with open(os.path.join(HERE, "shipped.json"), "w") as f:
+            json.dump(ship, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
