@@ -30,13 +30,14 @@ WORKLOADS = {
     "raft_cfg": ("Raft", "configs/Raft.cfg", 1,
                  "standard-raft Raft.cfg: 3 servers, Value={v1}, MaxElections=2, MaxRestarts=0"),
     "raft_n3v2e2": ("Raft", "configs/Raft_n3v2e2.cfg", 2,
-                    "standard-raft: 3 servers, Value={v1,v2}, MaxElections=2, MaxRestarts=0"),
+                    "standard-raft: 3 servers, Value={v1,v2} (log bound 2), MaxElections=2 (term bound 3), "
+                    "MaxRestarts=0"),
     "raft_n3v1e3": ("Raft", "configs/Raft_n3v1e3.cfg", 2,
                     "standard-raft: 3 servers, Value={v1}, MaxElections=3, MaxRestarts=0"),
     "raft_n3v2e3": ("Raft", "configs/Raft_n3v2e3.cfg", 2,
                     "standard-raft: 3 servers, Value={v1,v2}, MaxElections=3, MaxRestarts=0"),
 }
-DEFAULT_WORKLOAD = "raft_cfg"
+DEFAULT_WORKLOAD = "raft_n3v2e2"
 HBM_PEAK = 8.0e12  # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
 
 
@@ -69,7 +70,7 @@ def cpu_baseline(module, cfg_path, seconds=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default=os.environ.get("RMC_WORKLOAD", DEFAULT_WORKLOAD))
     ap.add_argument("--no-cpu-baseline", action="store_true")
