@@ -252,6 +252,8 @@ void build_actions(Model& M) {
   }
   M.nfixed = nf;
   M.ordinal_limit = off;
+  M.bind_words = (M.nfixed + M.kmax + 31) / 32;
+  M.ord_words = (off + 31) / 32;
   if (off >= 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");
 }
 
@@ -695,6 +697,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       }
       LevelArgs a;
       memset(&a, 0, sizeof a);
+      a.model = &M;
       a.frontier = cur + c0 * W;
       a.nparents = n;
       a.pbase = cur_base + c0;

@@ -17,6 +17,7 @@ struct DevStatus {
 };
 
 struct LevelArgs {
+  const Model* model;
   const uint32_t* frontier;
   unsigned long long nparents, pbase;
   unsigned level;  // level of the successors (parents are level-1)

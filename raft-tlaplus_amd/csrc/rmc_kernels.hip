@@ -105,6 +105,62 @@ __device__ __forceinline__ unsigned long long successor_fp(const PState<SPEC, N>
   return best;
 }
 
+// Parents per expand/materialize tile.  N=5 has 120 permutations, so its
+// per-parent H_pi vectors (960 B each) force a smaller tile.
+template <int N>
+struct Tile {
+  static constexpr int PB = N >= 5 ? 16 : 64;
+};
+
+// Dynamic LDS layout of k_expand (bytes, host mirrors it in expand_lds_bytes).
+struct ExpandLds {
+  int Wp, off_H, off_En, off_Ord, off_Base, bytes;
+};
+__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int nperm, int enw, int ordw) {
+  ExpandLds L;
+  L.Wp = words | 1;  // odd row stride: lane-per-parent LDS reads are bank-conflict free
+  int o = PB * L.Wp * 4;
+  o = (o + 7) & ~7;
+  L.off_H = o;
+  o += PB * nperm * 8;
+  L.off_En = o;
+  o += PB * enw * 4;
+  L.off_Ord = o;
+  o += PB * ordw * 4;
+  L.off_Base = o;
+  o += (PB + 1) * 4;
+  L.bytes = o;
+  return L;
+}
+
+__device__ __forceinline__ int select_bit(const uint32_t* w, int j) {  // j-th set bit (0-based)
+  for (int q = 0;; q++) {
+    uint32_t x = w[q];
+    int c = __popc(x);
+    if (j < c) {
+      for (int k = 0; k < j; k++) x &= x - 1u;
+      return 32 * q + (__ffs(x) - 1);
+    }
+    j -= c;
+  }
+}
+__device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set bits below `bit`
+  int r = 0;
+  for (int q = 0; q < (bit >> 5); q++) r += __popc(w[q]);
+  uint32_t m = (bit & 31) ? ((1u << (bit & 31)) - 1u) : 0u;
+  return r + __popc(w[bit >> 5] & m);
+}
+
+// One block = one tile of PB consecutive parents, 256 threads.
+//   A: parents -> LDS (coalesced), H_pi(parent) for every (parent, pi) pair.
+//   B: lane-per-parent binding evaluation.  Within a wave every lane runs the
+//      SAME binding of a different parent, so the fixed-binding actions are
+//      wave-uniform; enabled bindings and their TLC ordinals go to per-parent
+//      LDS bitmasks.
+//   C: lane-per-successor.  The tile's enabled (parent, binding) pairs are
+//      enumerated densely; each lane rebuilds its successor delta, computes
+//      the canonical fingerprint incrementally from H_pi and inserts it.
+//      Candidates are laid out per parent in TLC ordinal order.
 template <int SPEC, int N>
 __global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                 unsigned long long pbase, unsigned level,
@@ -114,99 +170,114 @@ __global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ fro
                                                 uint32_t* __restrict__ par_n,
                                                 unsigned long long* __restrict__ counters, unsigned long long cand_cap,
                                                 DevStatus* st) {
-  __shared__ uint32_t sS[WAVES_PER_BLOCK][MAXW];
-  __shared__ unsigned long long sH[WAVES_PER_BLOCK][MAXPERM];
-  const int w = threadIdx.x / WAVE, lane = lane_id();
-  const unsigned long long p = (unsigned long long)blockIdx.x * WAVES_PER_BLOCK + w;
-  if (p >= nparents) return;
-  const int words = cM.words, nperm = cM.nperm;
-  uint32_t* S = sS[w];
-  const uint32_t* src = frontier + p * (unsigned long long)words;
-  for (int q = lane; q < words; q += WAVE) S[q] = src[q];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  PState<SPEC, N> s{S};
-  const int nm = s.nmsg();
-  // ---- H_pi(parent) for all pi: items = N servers + nm messages (+ acked for Pull)
-  const int nitems = N + nm;
-  for (int pi = 0; pi < nperm; pi++) {
+  constexpr int PB = Tile<N>::PB;
+  extern __shared__ __align__(16) unsigned char lds[];
+  __shared__ unsigned long long sG;
+  const int tid = threadIdx.x;
+  const int words = cM.words, nperm = cM.nperm, enw = cM.bind_words, ordw = cM.ord_words;
+  const ExpandLds L = expand_lds(PB, words, nperm, enw, ordw);
+  uint32_t* sS = (uint32_t*)lds;
+  unsigned long long* sH = (unsigned long long*)(lds + L.off_H);
+  uint32_t* sEn = (uint32_t*)(lds + L.off_En);
+  uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
+  uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
+  const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
+  const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
+  // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
+  const uint32_t* src = frontier + p0 * (unsigned long long)words;
+  for (int q = tid; q < np * words; q += 256) {
+    int p = q / words;
+    sS[p * L.Wp + (q - p * words)] = src[q];
+  }
+  for (int q = tid; q < PB * (enw + ordw); q += 256) sEn[q] = 0;  // sEn and sOrd are adjacent
+  __syncthreads();
+  for (int idx = tid; idx < np * nperm; idx += 256) {
+    int p = idx % np, pi = idx / np;
+    PState<SPEC, N> s{sS + p * L.Wp};
     uint32_t P = cM.perm[pi];
     unsigned long long acc = 0;
-    for (int it = lane; it < nitems; it += WAVE) {
-      if (it < N) acc += h_server<SPEC, N>(P, it, s.A(it), s.B(it), s.Cw(it), s.Dw(it));
-      else acc += h_msg<SPEC>(P, s.msg(it - N));
-    }
-    acc = wave_sum_u64(acc);
+#pragma unroll
+    for (int i = 0; i < N; i++) acc += h_server<SPEC, N>(P, i, s.A(i), s.B(i), s.Cw(i), s.Dw(i));
+    const int nm = s.nmsg();
+    for (int k = 0; k < nm; k++) acc += h_msg<SPEC>(P, s.msg(k));
     if (SPEC == PULL) acc += h_acked_view(s.hdr());
-    if (lane == 0) sH[w][pi] = acc;
+    sH[p * nperm + pi] = acc;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // ---- enabled bindings
-  const int B = cM.nfixed + nm;
-  const int rounds = (B + WAVE - 1) / WAVE;
-  if (rounds > MAXROUNDS) {
-    if (lane == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
+  // ---- B: enabled bindings, lane per parent
+  {
+    const int p = tid % PB, bstride = 256 / PB;
+    if (p < np) {
+      PState<SPEC, N> s{sS + p * L.Wp};
+      const int nm = s.nmsg();
+      const int B = cM.nfixed + nm;
+      const unsigned long long pg = pbase + p0 + p;
+      for (int b = tid / PB; b < B; b += bstride) {
+        Delta d;
+        if (!eval_binding<SPEC, N>(s, cM, b, d)) continue;
+        if (d.err) {
+          if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pg, d.ordinal, b));
+          else atomicOr(&st->cap_flags, 1u << d.err);
+        } else {
+          int adds = 0;
+#pragma unroll
+          for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
+          if (nm + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
+        }
+        atomicOr(&sEn[p * enw + (b >> 5)], 1u << (b & 31));
+        atomicOr(&sOrd[p * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
+      }
+    }
+  }
+  __syncthreads();
+  // ---- per-parent successor counts -> tile prefix (wave 0), one global reservation per tile
+  if (tid < 64) {
+    int c = 0;
+    if (tid < np)
+      for (int q = 0; q < enw; q++) c += __popc(sEn[tid * enw + q]);
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int y = __shfl_up(incl, o, WAVE);
+      if (tid >= o) incl += y;
+    }
+    if (tid < PB) sBase[tid + 1] = (uint32_t)incl;
+    if (tid == 0) sBase[0] = 0;
+    int total = __shfl(incl, 63, WAVE);
+    if (tid == 0) sG = total ? atomicAdd(&counters[0], (unsigned long long)total) : 0ULL;
+  }
+  __syncthreads();
+  const int total = (int)sBase[np];
+  const unsigned long long gbase = sG;
+  if (tid < np) {
+    par_off[p0 + tid] = (uint32_t)(gbase + sBase[tid]);
+    par_n[p0 + tid] = sBase[tid + 1] - sBase[tid];
+  }
+  if (gbase + (unsigned long long)total > cand_cap) {
+    if (tid == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
     return;
   }
-  unsigned long long masks[MAXROUNDS] = {0, 0, 0, 0};
-  int total = 0;
-  const unsigned long long pg = pbase + p;
-#pragma unroll
-  for (int r = 0; r < MAXROUNDS; r++) {
-    if (r >= rounds) break;
-    int b = r * WAVE + lane;
+  // ---- C: fingerprints + inserts, lane per successor
+  for (int idx = tid; idx < total; idx += 256) {
+    int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
+    }
+    const int p = lo;
+    const int b = select_bit(sEn + p * enw, idx - (int)sBase[p]);
+    PState<SPEC, N> s{sS + p * L.Wp};
     Delta d;
-    bool en = false;
-    if (b < B) {
-      en = eval_binding<SPEC, N>(s, cM, b, d);
-      if (en && d.err) {
-        if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pg, d.ordinal, b));
-        else atomicOr(&st->cap_flags, 1u << d.err);
-      }
-      if (en && !d.err) {
-        // capacity: the successor must fit in kmax message slots
-        int adds = 0;
-#pragma unroll
-        for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
-        if (nm + adds > cM.kmax) { atomicOr(&st->cap_flags, 1u << E_CAP_MSG); }
-      }
+    eval_binding<SPEC, N>(s, cM, b, d);
+    const unsigned long long t = gbase + sBase[p] + rank_below(sOrd + p * ordw, d.ordinal);
+    const unsigned long long pg = pbase + p0 + p;
+    unsigned long long slot = 0;
+    if (!d.err) {
+      unsigned long long fp = successor_fp<SPEC, N>(s, d, sH + p * nperm, nperm);
+      unsigned long long val = ((unsigned long long)level << 48) | (pg << 10) | (unsigned long long)d.ordinal;
+      slot = table_insert(table, mask, fp, val, level, st);
     }
-    masks[r] = __ballot(en);
-    total += __popcll(masks[r]);
-  }
-  unsigned long long off = 0;
-  if (lane == 0 && total) off = atomicAdd(&counters[0], (unsigned long long)total);
-  off = __shfl(off, 0, WAVE);
-  if (lane == 0) {
-    par_off[p] = (uint32_t)off;
-    par_n[p] = (uint32_t)total;
-  }
-  if (off + total > cand_cap) {
-    if (lane == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
-    return;
-  }
-  // ---- fingerprints + inserts
-  int before = 0;
-  const unsigned long long* Hp = sH[w];
-#pragma unroll
-  for (int r = 0; r < MAXROUNDS; r++) {
-    if (r >= rounds) break;
-    if ((masks[r] >> lane) & 1ULL) {
-      int b = r * WAVE + lane;
-      Delta d;
-      eval_binding<SPEC, N>(s, cM, b, d);
-      unsigned long long t = off + before + __popcll(masks[r] & lanemask_lt());
-      unsigned long long slot = 0;
-      if (!d.err) {
-        unsigned long long fp = successor_fp<SPEC, N>(s, d, Hp, nperm);
-        unsigned long long val = ((unsigned long long)level << 48) | (pg << 10) | (unsigned long long)d.ordinal;
-        slot = table_insert(table, mask, fp, val, level, st);
-      }
-      cand_slot[t] = slot;
-      cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? 0x8000u : 0u);
-    }
-    before += __popcll(masks[r]);
+    cand_slot[t] = slot;
+    cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? 0x8000u : 0u);
   }
 }
 
@@ -288,8 +359,11 @@ __global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict_
 struct Launch {
   template <int SPEC, int N>
   static void expand(const LevelArgs& a, hipStream_t s) {
-    unsigned long long blocks = (a.nparents + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), 0, s, a.frontier, a.nparents, a.pbase,
+    constexpr int PB = Tile<N>::PB;
+    unsigned long long blocks = (a.nparents + PB - 1) / PB;
+    const Model& M = *a.model;
+    ExpandLds L = expand_lds(PB, M.words, M.nperm, M.bind_words, M.ord_words);
+    hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.level, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st);
   }
@@ -353,12 +427,12 @@ void launch_rehash(const unsigned long long* old, unsigned long long nold, unsig
 }
 size_t scan_temp_bytes(unsigned long long n) {
   size_t bytes = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
   return bytes;
 }
 void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
                  hipStream_t s) {
-  hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
+  (void)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
 }
 hipError_t upload_model(const Model& m) { return hipMemcpyToSymbol(HIP_SYMBOL(cM), &m, sizeof(Model)); }
 

@@ -74,6 +74,7 @@ struct Model {
   uint8_t fb_act[MAXFIXED], fb_x[MAXFIXED];  // fixed binding -> (action slot, binding index)
   int msg_act_slot[A_NUM];                   // action slot of each message action
   int ordinal_limit;
+  int bind_words, ord_words;  // u32 words of a per-parent bitmask over bindings / over ordinals
 };
 
 // ------------------------------------------------------------- bit helpers
