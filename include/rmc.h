@@ -80,6 +80,9 @@ int rmc_trace_action(const rmc_model* m, int k, char* text, size_t len);   /* "I
 /* Print the TLC-format report for a finished check into buf. */
 int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t len);
 void rmc_model_free(rmc_model* m);
+/* Free the device buffers librmc keeps per GPU between checks (fingerprint set,
+ * frontiers, trace records).  They are otherwise reused by the next check. */
+void rmc_release_device_memory(void);
 const char* rmc_last_error(void);
 const char* rmc_version(void);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */

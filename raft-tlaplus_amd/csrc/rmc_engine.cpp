@@ -10,6 +10,7 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <mutex>
 #include <unordered_map>
 #include <set>
 #include <sstream>
@@ -190,6 +191,8 @@ struct rmc_model {
   std::vector<std::vector<uint32_t>> trace_states;
   std::vector<std::string> trace_actions;
   uint32_t kmax_user = 0;
+  // sizes the last check ended with (pre-size the next check of this model)
+  unsigned long long hint_slots = 0, hint_fcap = 0, hint_trcap = 0;
 };
 
 namespace {
@@ -564,12 +567,38 @@ struct DevBuf {
     p = q;
     bytes = b;
   }
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+  void ensure(size_t b) {  // at least b bytes; contents not kept
+    if (p && bytes >= b) return;
+    alloc(b);
   }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  ~DevBuf() { release(); }
   template <class T>
   T* as() const { return (T*)p; }
 };
+
+struct Arena {
+  DevBuf table, table2, fa, fb, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp, trp, trb;
+  void release() {
+    for (DevBuf* b : {&table, &table2, &fa, &fb, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
+                      &scantmp, &trp, &trb})
+      b->release();
+  }
+};
+std::mutex g_arena_mu;
+std::map<int, Arena*> g_arenas;
+Arena& arena_for_current_device() {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  Arena*& a = g_arenas[dev];
+  if (!a) a = new Arena();
+  return *a;
+}
 
 struct EventTimer {
   hipEvent_t a, b;
@@ -596,33 +625,40 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   HIPCHK(hipMemGetInfo(&freeb, &totalb));
   unsigned long long slots = opt->hash_slots;
   if (!slots) {
-    slots = 1ULL << 26;  // 1 GiB table; grown on demand
+    // 1 GiB table grown on demand; a model checked before starts at the size
+    // its last check ended with (TLC's preallocated FPSet, -fpmem, in spirit)
+    slots = std::max(1ULL << 26, m->hint_slots);
   }
   if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
-  unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : (1ULL << 22);
+  unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
   const int maxsucc = M.nfixed + M.kmax;
   unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 20);
   const unsigned long long cand_cap = chunk * (unsigned long long)std::min(maxsucc, 256);
 
-  DevBuf table, fa, fb, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp, trp, trb;
-  table.alloc(slots * 16);
-  HIPCHK(hipMemsetAsync(table.p, 0xFF, table.bytes, stream));
-  fa.alloc(fcap * W * 4);
-  fb.alloc(fcap * W * 4);
-  cslot.alloc(cand_cap * 8);
-  cob.alloc(cand_cap * 4);
-  cwin.alloc(cand_cap);
-  poff.alloc(chunk * 4);
-  pn.alloc(chunk * 4);
-  pwin.alloc(chunk * 4);
-  ppos.alloc(chunk * 4);
-  counters.alloc(64);
-  stbuf.alloc(sizeof(DevStatus));
+  // Device buffers persist per device across checks (grow-only), so repeated
+  // checks do not pay hipMalloc/hipFree of tens of GB each time.
+  Arena& A = arena_for_current_device();
+  DevBuf &table = A.table, &fa = A.fa, &fb = A.fb, &cslot = A.cslot, &cob = A.cob, &cwin = A.cwin;
+  DevBuf &poff = A.poff, &pn = A.pn, &pwin = A.pwin, &ppos = A.ppos, &counters = A.counters, &stbuf = A.stbuf;
+  DevBuf &scantmp = A.scantmp, &trp = A.trp, &trb = A.trb;
+  table.ensure(slots * 16);
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * 16, stream));
+  fa.ensure(fcap * W * 4);
+  fb.ensure(fcap * W * 4);
+  cslot.ensure(cand_cap * 8);
+  cob.ensure(cand_cap * 4);
+  cwin.ensure(cand_cap * 2);
+  poff.ensure(chunk * 4);
+  pn.ensure(chunk * 4);
+  pwin.ensure(chunk * 4);
+  ppos.ensure(chunk * 4);
+  counters.ensure(64);
+  stbuf.ensure(sizeof(DevStatus));
   size_t stb = scan_temp_bytes(chunk);
-  scantmp.alloc(stb ? stb : 16);
-  unsigned long long trcap = fcap * 4;
-  trp.alloc(trcap * 8);
-  trb.alloc(trcap * 2);
+  scantmp.ensure(stb ? stb : 16);
+  unsigned long long trcap = std::max(fcap * 4, m->hint_trcap);
+  trp.ensure(trcap * 8);
+  trb.ensure(trcap * 2);
 
   DevStatus hst;
   auto reset_status = [&]() {
@@ -666,6 +702,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     else if (bad >= 0) { status = 1; snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str()); bad_state = 0; }
   }
   EventTimer te, tm, tz;
+  double rehash_s = 0, grow_s = 0;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
   double expand_ms = 0, mark_ms = 0, mat_ms = 0;
   unsigned long long expand_launches = 0;
   uint32_t* cur = fa.as<uint32_t>();
@@ -684,9 +725,10 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         unsigned long long nslots = slots;
         while ((entries_hint + n * (unsigned long long)maxsucc) * 2 > nslots) nslots <<= 1;
         if (opt->hash_slots) throw std::runtime_error("fingerprint set full (raise hash_slots)");
-        DevBuf nt;
-        nt.alloc(nslots * 16);
-        HIPCHK(hipMemsetAsync(nt.p, 0xFF, nt.bytes, stream));
+        auto tr0 = now();
+        DevBuf& nt = A.table2;
+        nt.ensure(nslots * 16);
+        HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
         launch_rehash(table.as<unsigned long long>(), slots, nt.as<unsigned long long>(), nslots - 1,
                       stbuf.as<DevStatus>(), stream);
         HIPCHK(hipGetLastError());
@@ -694,6 +736,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         std::swap(table.p, nt.p);
         std::swap(table.bytes, nt.bytes);
         slots = nslots;
+        rehash_s += secs(tr0, now());
+        if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots\n", __builtin_ctzll(slots));
       }
       LevelArgs a;
       memset(&a, 0, sizeof a);
@@ -706,7 +750,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       a.mask = slots - 1;
       a.cand_slot = cslot.as<unsigned long long>();
       a.cand_ob = cob.as<uint32_t>();
-      a.cand_win = cwin.as<uint8_t>();
+      a.cand_win = cwin.as<uint16_t>();
       a.par_off = poff.as<uint32_t>();
       a.par_n = pn.as<uint32_t>();
       a.par_win = pwin.as<uint32_t>();
@@ -758,6 +802,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       gen_lvl += ncand;
       if (next_n + W_chunk > fcap) {
         // grow both frontier buffers (keep what is already written)
+        auto tg0 = now();
         unsigned long long nf = fcap;
         while (next_n + W_chunk > nf) nf *= 2;
         size_t cur_off_words = (size_t)(cur - (cur == fa.as<uint32_t>() ? fa.as<uint32_t>() : fb.as<uint32_t>()));
@@ -771,13 +816,16 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         nxt = nb.as<uint32_t>();
         a.frontier = cur + c0 * W;
         fcap = nf;
+        grow_s += secs(tg0, now());
       }
       if (distinct + next_n + W_chunk > trcap) {
+        auto tg0 = now();
         unsigned long long nt = trcap;
         while (distinct + next_n + W_chunk > nt) nt *= 2;
         trp.grow_copy(nt * 8, (distinct + next_n) * 8);
         trb.grow_copy(nt * 2, (distinct + next_n) * 2);
         trcap = nt;
+        grow_s += secs(tg0, now());
       }
       a.out = nxt + next_n * W;
       a.out_base_global = distinct + next_n;
@@ -828,7 +876,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     cur_n = next_n;
     std::swap(cur, nxt);
     if (opt->verbose)
-      fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated\n", depth, next_n, distinct, generated);
+      fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated, t=%.3fs (rehash %.3fs, grow %.3fs)\n",
+              depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s);
   }
   HIPCHK(hipStreamSynchronize(stream));
   // ---- trace reconstruction: walk parent records, replay bindings on the host
@@ -880,6 +929,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     }
   }
   HIPCHK(hipStreamDestroy(stream));
+  if (!opt->hash_slots) m->hint_slots = slots;
+  if (!opt->frontier_cap) m->hint_fcap = fcap;
+  m->hint_trcap = trcap;
   res->generated = generated;
   res->distinct = distinct;
   res->left_on_queue = (status == 0) ? 0 : cur_n;
@@ -1039,6 +1091,16 @@ int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t
 }
 
 void rmc_model_free(rmc_model* m) { delete m; }
+
+void rmc_release_device_memory(void) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto& kv : g_arenas) {
+    if (hipSetDevice(kv.first) == hipSuccess) kv.second->release();
+  }
+  (void)hipSetDevice(cur);
+}
 
 // Test hook only (never called by rmc_check): sequential host BFS over the same
 // lowered actions and fingerprints the kernels use, in TLC order, so the CPU

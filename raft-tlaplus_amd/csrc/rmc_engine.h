@@ -25,7 +25,7 @@ struct LevelArgs {
   unsigned long long mask;
   unsigned long long* cand_slot;
   uint32_t* cand_ob;
-  uint8_t* cand_win;
+  uint16_t* cand_win;
   uint32_t *par_off, *par_n, *par_win, *par_pos;
   unsigned long long* counters;
   unsigned long long cand_cap;

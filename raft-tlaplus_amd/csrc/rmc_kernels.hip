@@ -1,20 +1,21 @@
 // rmc_kernels.hip — level-synchronous BFS kernels for gfx950 (MI355X).
 //
-// Per BFS level, per chunk of parents:
-//   k_expand       one wavefront per parent: stage the packed parent in LDS,
-//                  compute H_pi(parent) for every server permutation (lanes
-//                  split the items, wave reduction per pi), evaluate every
-//                  binding of Next in parallel (one lane per binding), ballot
-//                  the enabled ones, and for each successor compute its
-//                  canonical fingerprint incrementally from the parent's H_pi
-//                  and the successor delta, then insert it into the HBM
-//                  fingerprint set with first-in-TLC-order-wins semantics
-//                  (atomicMin on (level, parent, ordinal)).
-//   k_mark         one thread per parent: which of its candidates won.
+// Per BFS level, per chunk of parents.  Parents are
+// processed in tiles of PB consecutive states (Tile<N>), one 256-thread block
+// per tile:
+//   k_expand       stage the tile in LDS; H_pi(parent) for every server
+//                  permutation; evaluate every Next binding lane-per-parent
+//                  (one binding per wave step, so fixed actions are wave-
+//                  uniform); then lane-per-successor: rebuild the delta,
+//                  compute the canonical fingerprint incrementally from H_pi,
+//                  insert it into the HBM fingerprint set with first-in-TLC-
+//                  order-wins semantics (atomicMin on (level, parent, ordinal)).
+//   k_mark         one thread per parent: which of its candidates won, and
+//                  each winner's rank in TLC order.
 //   (scan)         exclusive scan of winners per parent -> output positions.
-//   k_materialize  one wavefront per parent: regenerate each winning successor
-//                  from parent + binding, write it to the next frontier in TLC
-//                  order, check the cfg's invariants, write the trace record.
+//   k_materialize  same tiling: compact the tile's winners in LDS, regenerate
+//                  each lane-per-winner, write it to its TLC-order slot of the
+//                  next frontier, write the trace record, check invariants.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include "rmc_spec.h"
@@ -25,21 +26,8 @@ namespace rmc {
 __constant__ Model cM;
 
 constexpr int WAVE = 64;
-constexpr int WAVES_PER_BLOCK = 4;
-constexpr int MAXW = 1 + 4 * MAXN + 128;  // words per state staged in LDS
-constexpr int MAXROUNDS = 4;              // up to 256 bindings per state
 constexpr unsigned long long EMPTY = ~0ULL;
 
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
-    lo = __shfl_xor(lo, o, WAVE);
-    hi = __shfl_xor(hi, o, WAVE);
-    v += ((unsigned long long)hi << 32) | lo;
-  }
-  return v;
-}
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
   int l = lane_id();
@@ -281,12 +269,15 @@ __global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ fro
   }
 }
 
+// One thread per parent: which of its candidates won their fingerprint, and
+// each winner's rank among the parent's winners (candidates are stored in TLC
+// ordinal order, so the rank is the output order).  cand_win = 1 + rank, 0 = lost.
 __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsigned long long pbase, unsigned level,
                                               const unsigned long long* __restrict__ table,
                                               const unsigned long long* __restrict__ cand_slot,
                                               const uint32_t* __restrict__ cand_ob,
                                               const uint32_t* __restrict__ par_off, const uint32_t* __restrict__ par_n,
-                                              uint8_t* __restrict__ cand_win, uint32_t* __restrict__ par_win) {
+                                              uint16_t* __restrict__ cand_win, uint32_t* __restrict__ par_win) {
   unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= nparents) return;
   uint32_t off = par_off[p], n = par_n[p];
@@ -294,64 +285,96 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
   unsigned long long base = ((unsigned long long)level << 48) | ((pbase + p) << 10);
   for (uint32_t t = off; t < off + n; t++) {
     uint32_t ob = cand_ob[t];
-    uint8_t win = 0;
+    bool win = false;
     if (!(ob & 0x8000u)) {
       unsigned long long mine = base | (ob >> 16);
       win = table[2 * cand_slot[t] + 1] == mine;
     }
-    cand_win[t] = win;
-    cnt += win;
+    cand_win[t] = win ? (uint16_t)(++cnt) : (uint16_t)0;
   }
   par_win[p] = cnt;
 }
 
+// Materialize the level's new states, tile by tile (same tiling as k_expand,
+// so a tile's candidates are one contiguous range).  Winners are compacted
+// into an LDS list and processed lane-per-winner: regenerate the successor
+// from the LDS-staged parent and its binding, write it to its TLC-order slot
+// of the next frontier, write the trace record, check the cfg's invariants.
+constexpr int MAT_LIST = 1024;
 template <int SPEC, int N>
 __global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                      unsigned long long pbase, const uint32_t* __restrict__ cand_ob,
-                                                     const uint8_t* __restrict__ cand_win,
+                                                     const uint16_t* __restrict__ cand_win,
                                                      const uint32_t* __restrict__ par_off,
                                                      const uint32_t* __restrict__ par_n,
                                                      const uint32_t* __restrict__ par_pos, uint32_t* __restrict__ out,
                                                      unsigned long long out_base_global,
                                                      unsigned long long* __restrict__ tr_parent,
                                                      uint16_t* __restrict__ tr_bind, DevStatus* st) {
-  __shared__ uint32_t sS[WAVES_PER_BLOCK][MAXW];
-  __shared__ uint32_t sOrd[WAVES_PER_BLOCK][MAXROUNDS * WAVE];
-  const int w = threadIdx.x / WAVE, lane = lane_id();
-  const unsigned long long p = (unsigned long long)blockIdx.x * WAVES_PER_BLOCK + w;
-  if (p >= nparents) return;
-  const uint32_t n = par_n[p], off = par_off[p];
-  const int words = cM.words;
-  uint32_t* S = sS[w];
-  const uint32_t* src = frontier + p * (unsigned long long)words;
-  for (int q = lane; q < words; q += WAVE) S[q] = src[q];
-  // winners' ordinals (0xFFFF for losers) so each winner can find its rank in TLC order
-  for (uint32_t t = lane; t < n; t += WAVE)
-    sOrd[w][t] = cand_win[off + t] ? (cand_ob[off + t] >> 16) : 0xFFFFu;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  PState<SPEC, N> s{S};
-  const unsigned long long pg = pbase + p;
-  const uint32_t pos0 = par_pos[p];
-  for (uint32_t t = lane; t < n; t += WAVE) {
-    uint32_t my = sOrd[w][t];
-    if (my == 0xFFFFu) continue;
-    uint32_t rank = 0;
-    for (uint32_t u = 0; u < n; u++) rank += sOrd[w][u] < my;
-    int b = (int)(cand_ob[off + t] & 0x3FFu);
-    Delta d;
-    eval_binding<SPEC, N>(s, cM, b, d);
-    unsigned long long dst = (unsigned long long)pos0 + rank;
-    uint32_t* o = out + dst * (unsigned long long)words;
-    int e = apply_delta<SPEC, N>(s, cM, d, o);
-    if (e) atomicOr(&st->cap_flags, 1u << e);
-    tr_parent[out_base_global + dst] = pg;
-    tr_bind[out_base_global + dst] = (uint16_t)b;
-    PState<SPEC, N> ns{o};
-    int err = 0;
-    int bad = check_invariants<SPEC, N>(ns, cM, err);
-    if (err) atomicMin(&st->inv_err_key, order_key(pg, (int)my, b));
-    else if (bad >= 0) atomicMin(&st->viol_key, order_key(pg, (int)my, b));
+  constexpr int PB = Tile<N>::PB;
+  extern __shared__ __align__(16) unsigned char lds[];
+  __shared__ uint32_t sOff[PB + 1], sPos[PB], sList[MAT_LIST];
+  __shared__ int sCount;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int words = cM.words, Wp = words | 1;
+  uint32_t* sS = (uint32_t*)lds;
+  const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
+  const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
+  const uint32_t start = par_off[p0];
+  const uint32_t* src = frontier + p0 * (unsigned long long)words;
+  for (int q = tid; q < np * words; q += 256) {
+    int p = q / words;
+    sS[p * Wp + (q - p * words)] = src[q];
+  }
+  if (tid < np) {
+    sOff[tid] = par_off[p0 + tid] - start;
+    sPos[tid] = par_pos[p0 + tid];
+    if (tid == np - 1) sOff[np] = par_off[p0 + tid] + par_n[p0 + tid] - start;
+  }
+  __syncthreads();
+  const int total = (int)sOff[np];
+  for (int r0 = 0; r0 < total; r0 += MAT_LIST) {
+    if (tid == 0) sCount = 0;
+    __syncthreads();
+    const int rn = total - r0 < MAT_LIST ? total - r0 : MAT_LIST;
+    for (int idx = tid; idx < ((rn + 255) & ~255); idx += 256) {
+      bool w = idx < rn && cand_win[start + r0 + idx] != 0;
+      unsigned long long m = __ballot(w);
+      int base = 0;
+      if (lane == 0 && m) base = atomicAdd(&sCount, __popcll(m));
+      base = __shfl(base, 0, WAVE);
+      if (w) sList[base + __popcll(m & lanemask_lt())] = (uint32_t)(r0 + idx);
+    }
+    __syncthreads();
+    const int nw = sCount;
+    for (int e = tid; e < nw; e += 256) {
+      const int idx = (int)sList[e];
+      int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
+      while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if ((int)sOff[mid] <= idx) lo = mid; else hi = mid - 1;
+      }
+      const int p = lo;
+      const uint32_t ob = cand_ob[start + idx];
+      const int b = (int)(ob & 0x3FFu);
+      const int rank = (int)cand_win[start + idx] - 1;
+      PState<SPEC, N> s{sS + p * Wp};
+      Delta d;
+      eval_binding<SPEC, N>(s, cM, b, d);
+      const unsigned long long dst = (unsigned long long)sPos[p] + rank;
+      uint32_t* o = out + dst * (unsigned long long)words;
+      int err = apply_delta<SPEC, N>(s, cM, d, o);
+      if (err) atomicOr(&st->cap_flags, 1u << err);
+      const unsigned long long pg = pbase + p0 + p;
+      tr_parent[out_base_global + dst] = pg;
+      tr_bind[out_base_global + dst] = (uint16_t)b;
+      PState<SPEC, N> ns{o};
+      int ierr = 0;
+      int bad = check_invariants<SPEC, N>(ns, cM, ierr);
+      if (ierr) atomicMin(&st->inv_err_key, order_key(pg, (int)(ob >> 16), b));
+      else if (bad >= 0) atomicMin(&st->viol_key, order_key(pg, (int)(ob >> 16), b));
+    }
+    __syncthreads();
   }
 }
 
@@ -369,8 +392,10 @@ struct Launch {
   }
   template <int SPEC, int N>
   static void materialize(const LevelArgs& a, hipStream_t s) {
-    unsigned long long blocks = (a.nparents + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(256), 0, s, a.frontier, a.nparents,
+    constexpr int PB = Tile<N>::PB;
+    unsigned long long blocks = (a.nparents + PB - 1) / PB;
+    size_t lds_bytes = (size_t)PB * (a.model->words | 1) * 4;
+    hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(256), lds_bytes, s, a.frontier, a.nparents,
                        a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
                        a.tr_parent, a.tr_bind, a.st);
   }

@@ -47,7 +47,8 @@ class Result(ctypes.Structure):
 # every entry point include/rmc.h declares (checked by tests/test_abi.py)
 EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_check",
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
-           "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels"]
+           "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
+           "rmc_release_device_memory"]
 
 _lib = None
 
