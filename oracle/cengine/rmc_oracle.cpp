@@ -18,6 +18,10 @@
 // attain it) hashed to 128 bits; the GPU path uses a different construction
 // (min over permutations of a 64-bit additive hash), so agreement between the
 // two is evidence for both.
+//
+// Parity unpinned against TLC: the reference ships no counts or traces and TLC
+// (Java) is absent here and on the GPU box; this restatement is
+// pinned by SURVEY.md Appendix B and by agreement with oracle/pyoracle.
 #include <algorithm>
 #include <chrono>
 #include <cstdint>

@@ -3,6 +3,11 @@
 TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py may import this package, and only as the
 checker.  The product path (raft-tlaplus_amd/) never imports it.
+
+Parity unpinned against TLC: the reference holds no counts, traces or
+fixtures and TLC (Java) is absent here and on the GPU box.
+The pins are the hand-derived first levels of SURVEY.md Appendix B and the
+agreement of this oracle with the independent C oracle (oracle/cengine).
 """
 from .cfg import load_cfg, parse_cfg
 from .tlc import bfs, EvalError
