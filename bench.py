@@ -49,6 +49,22 @@ def algorithmic_bytes(res):
     return D * S + G * 8 + G * 12
 
 
+def pmc_traffic(workload):
+    """Per-launch HBM bytes of k_expand from the committed rocprofv3 --pmc summary
+    of this workload (tools/gpu_profile.sh -> profiles/<round>/pmc_summary_<workload>.json),
+    priced (2*FETCH_SIZE + WRITE_SIZE) KiB as MI355X_MICROARCH.md prescribes for gfx950."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_%s.json" % workload)), reverse=True):
+        try:
+            d = json.load(open(path))
+            for k, v in d["kernels"].items():
+                if k.startswith("rmc::k_expand") and "traffic_bytes_per_dispatch" in v:
+                    return v["traffic_bytes_per_dispatch"], os.path.relpath(path, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
 def cpu_baseline(module, cfg_path, seconds=20.0):
     """The C oracle (oracle/_build/rmc_oracle, a port) timed on this host for a
     bounded wall budget on the same config; returns distinct states/s."""
@@ -70,7 +86,7 @@ def cpu_baseline(module, cfg_path, seconds=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default=os.environ.get("RMC_WORKLOAD", DEFAULT_WORKLOAD))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -97,8 +113,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    cold = []
     for _ in range(args.warmup):
+        t = time.perf_counter()
         model.check()
+        cold.append(time.perf_counter() - t)
     barrier()
     t0 = time.perf_counter()
     results = []
@@ -115,6 +134,7 @@ def main():
     value = world * res["distinct"] / per_step
     exp_bytes = algorithmic_bytes(res)
     achieved = exp_bytes / (res["expand_ms"] * 1e-3) if res["expand_ms"] > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(args.workload)
     if rank == 0:
         line = {
             "metric": "distinct states/sec + time-to-exhaust, standard-raft",
@@ -133,9 +153,10 @@ def main():
                        "spec": module, "cfg": cfg_rel,
                        "parallelism": "replicas" if world > 1 else "single"},
             "result": {"generated": res["generated"], "distinct": res["distinct"], "depth": res["depth"],
-                       "status": res["status"], "time_to_exhaust_s": per_step},
+                       "status": res["status"], "time_to_exhaust_s": per_step,
+                       "first_check_s": cold[0] if cold else None},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": None,
+                         "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                          "kernel": "k_expand", "launches": res["expand_launches"],
                          "avg_launch_ms": res["expand_ms"] / max(1, res["expand_launches"]),
                          "bytes_per_launch": exp_bytes / max(1, res["expand_launches"])},
