@@ -16,21 +16,12 @@
 #include <sstream>
 #include <string>
 #include <vector>
-#include "../../include/rmc.h"
-#include "rmc_engine.h"
+#include "rmc_internal.h"
 
 using namespace rmc;
+using namespace rmcx;
 
 static thread_local std::string g_last_error;
-
-#define HIPCHK(x)                                                                   \
-  do {                                                                              \
-    hipError_t e_ = (x);                                                            \
-    if (e_ != hipSuccess) {                                                         \
-      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + \
-                               " at " #x);                                          \
-    }                                                                               \
-  } while (0)
 
 // ------------------------------------------------------------------ cfg
 namespace {
@@ -179,23 +170,7 @@ Cfg parse_cfg(const std::string& text) {
 
 }  // namespace
 
-// ---------------------------------------------------------------- model
-struct rmc_model {
-  std::string module, tla_text;
-  Model M;
-  int fp_aux = 0;  // reserved: no VIEW -> aux vars would join the fingerprint
-  std::vector<std::string> server_names, value_names, inv_names;
-  std::vector<std::string> var_order;
-  // results of the last check
-  std::vector<std::pair<unsigned long long, unsigned long long>> levels;
-  std::vector<std::vector<uint32_t>> trace_states;
-  std::vector<std::string> trace_actions;
-  uint32_t kmax_user = 0;
-  // sizes the last check ended with (pre-size the next check of this model)
-  unsigned long long hint_slots = 0, hint_fcap = 0, hint_trcap = 0;
-};
-
-namespace {
+namespace rmcx {
 
 int spec_of_module(const std::string& m) {
   if (m == "Raft") return RAFT;
@@ -548,38 +523,7 @@ std::string def_location(const rmc_model* m, const std::string& op) {
 }  // namespace
 
 // ----------------------------------------------------------- BFS driver
-namespace {
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  void alloc(size_t b) {
-    if (p) HIPCHK(hipFree(p));
-    p = nullptr;
-    bytes = b;
-    if (b) HIPCHK(hipMalloc(&p, b));
-  }
-  void grow_copy(size_t b, size_t keep) {
-    void* q = nullptr;
-    HIPCHK(hipMalloc(&q, b));
-    if (p && keep) HIPCHK(hipMemcpy(q, p, keep, hipMemcpyDeviceToDevice));
-    if (p) HIPCHK(hipFree(p));
-    p = q;
-    bytes = b;
-  }
-  void ensure(size_t b) {  // at least b bytes; contents not kept
-    if (p && bytes >= b) return;
-    alloc(b);
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  ~DevBuf() { release(); }
-  template <class T>
-  T* as() const { return (T*)p; }
-};
+namespace rmcx {
 
 struct Arena {
   DevBuf table, table2, fa, fb, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp, trp, trb;
@@ -600,11 +544,38 @@ Arena& arena_for_current_device() {
   return *a;
 }
 
-struct EventTimer {
-  hipEvent_t a, b;
-  EventTimer() { HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b)); }
-  ~EventTimer() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
-};
+void set_last_error(const std::string& s) { g_last_error = s; }
+
+void replay_trace(rmc_model* m, const std::vector<int>& binds, int last_b, int status, std::string& message,
+                  rmc_result* res) {
+  const Model& M = m->M;
+  const size_t W = (size_t)M.words;
+  std::vector<uint32_t> s = init_state(M);
+  m->trace_states.push_back(s);
+  m->trace_actions.push_back("Initial predicate");
+  auto step = [&](int b) {
+    std::vector<uint32_t> t(W, 0);
+    int ordv = 0, act = -1, err = 0;
+    int en = host_eval_apply(M, s.data(), b, t.data(), &ordv, &act, &err);
+    if (en != 1) throw std::runtime_error("trace replay: binding not enabled");
+    std::string lbl = binding_label(m, b, act);
+    if (err) return lbl;  // the erroring step: no successor state
+    s = t;
+    m->trace_states.push_back(s);
+    m->trace_actions.push_back(lbl);
+    return std::string();
+  };
+  for (int b : binds) step(b);
+  if (last_b >= 0) {
+    std::string e = step(last_b);
+    if (!e.empty()) message += " in action " + e;
+  }
+  if (status == 1 && !m->trace_states.empty()) {
+    int err = 0;
+    int bad = host_check_invariants(M, m->trace_states.back().data(), &err);
+    if (bad >= 0) snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str());
+  }
+}
 
 int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   auto t0 = std::chrono::steady_clock::now();
@@ -902,31 +873,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       g = pp;
     }
     std::reverse(binds.begin(), binds.end());
-    std::vector<uint32_t> s = init;
-    m->trace_states.push_back(s);
-    m->trace_actions.push_back("Initial predicate");
-    auto step = [&](int b) {
-      std::vector<uint32_t> t(W, 0);
-      int ordv = 0, act = -1, err = 0;
-      int en = host_eval_apply(M, s.data(), b, t.data(), &ordv, &act, &err);
-      if (en != 1) throw std::runtime_error("trace replay: binding not enabled");
-      std::string lbl = binding_label(m, b, act);
-      if (err) return lbl;  // the erroring step: no successor state
-      s = t;
-      m->trace_states.push_back(s);
-      m->trace_actions.push_back(lbl);
-      return std::string();
-    };
-    for (int b : binds) step(b);
-    if (last_b >= 0) {
-      std::string e = step(last_b);
-      if (!e.empty()) message += " in action " + e;
-    }
-    if (status == 1 && !m->trace_states.empty()) {
-      int err = 0;
-      int bad = host_check_invariants(M, m->trace_states.back().data(), &err);
-      if (bad >= 0) snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str());
-    }
+    replay_trace(m, binds, last_b, status, message, res);
   }
   HIPCHK(hipStreamDestroy(stream));
   if (!opt->hash_slots) m->hint_slots = slots;
