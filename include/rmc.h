@@ -85,6 +85,17 @@ void rmc_model_free(rmc_model* m);
 void rmc_release_device_memory(void);
 const char* rmc_last_error(void);
 const char* rmc_version(void);
+/* Fingerprint-sharded search.  One process per GPU: rank 0
+ * calls rmc_comm_unique_id, the 128-byte id is broadcast out of band (e.g.
+ * torch.distributed), then every rank calls rmc_check_sharded with its rank,
+ * the world size and its GPU; shards exchange over RCCL (xGMI).  Every rank
+ * receives the same global result.  rmc_check_logical runs `shards` logical
+ * shards of the same protocol in this process on its current GPU (the
+ * transport is device copies) -- the multi-GPU path without a cluster. */
+int rmc_comm_unique_id(unsigned char* id128);
+int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, int device, const unsigned char* id128,
+                      rmc_result* out);
+int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result* out);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
 int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
 

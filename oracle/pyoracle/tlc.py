@@ -51,6 +51,13 @@ class Rec(tuple):
         d.update(kw)
         return Rec(**d)
 
+    def __reduce__(self):  # picklable (the sharded-protocol test ships states between ranks)
+        return (_rec_from_items, (tuple(tuple.__iter__(self)),))
+
+
+def _rec_from_items(items):
+    return Rec(**dict(items))
+
 
 def tlc_key(v):
     """Sort key reproducing TLC's compareTo for the value kinds the specs use."""

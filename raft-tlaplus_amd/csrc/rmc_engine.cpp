@@ -1040,6 +1040,7 @@ int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t
 void rmc_model_free(rmc_model* m) { delete m; }
 
 void rmc_release_device_memory(void) {
+  release_shard_buffers();
   std::lock_guard<std::mutex> lk(g_arena_mu);
   int cur = 0;
   (void)hipGetDevice(&cur);

@@ -23,7 +23,8 @@ struct LevelArgs {
   unsigned level;  // level of the successors (parents are level-1)
   unsigned long long* table;
   unsigned long long mask;
-  unsigned long long* cand_slot;
+  unsigned long long* cand_slot;  // single shard: table slot; sharded: the candidate's fp
+  unsigned long long* cand_val;   // sharded only (else nullptr): the candidate's (level, parent, ordinal) key
   uint32_t* cand_ob;
   uint16_t* cand_win;
   uint32_t *par_off, *par_n, *par_win, *par_pos;
@@ -45,6 +46,21 @@ size_t scan_temp_bytes(unsigned long long n);
 void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
                  hipStream_t s);
 hipError_t upload_model(const Model& m);
+
+// sharded search (rmc_sharded.cpp)
+void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_ob, unsigned long long n, int W,
+                        unsigned int* counts, hipStream_t s);
+void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
+                   unsigned long long n, int W, const unsigned int* seg_off, unsigned int* cursor,
+                   unsigned long long* send, uint32_t* perm, hipStream_t s);
+void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
+                        unsigned long long mask, unsigned level, unsigned long long* recv_slot, DevStatus* st,
+                        hipStream_t s);
+void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
+                      const unsigned long long* table, uint8_t* flag, unsigned long long* newcount, hipStream_t s);
+void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
+                     const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s);
+int host_fp_owner(unsigned long long fp, int W);
 
 // host-side (rmc_host.cpp): replay + formatting use the same action code
 int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,

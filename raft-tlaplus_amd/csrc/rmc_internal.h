@@ -80,6 +80,7 @@ uint32_t default_kmax(const rmc::Model& M);
 std::vector<uint32_t> init_state(const rmc::Model& M);
 std::string binding_label(const rmc_model* m, int b, int act);
 void set_last_error(const std::string& s);
+void release_shard_buffers();
 // Rebuild the behaviour Init -> ... from the binding chain (root first), plus
 // the failing binding (last_b >= 0) whose successor violated or erred.
 void replay_trace(rmc_model* m, const std::vector<int>& binds, int last_b, int status, std::string& message,

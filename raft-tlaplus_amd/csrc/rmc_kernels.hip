@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ fro
                                                 uint32_t* __restrict__ cand_ob, uint32_t* __restrict__ par_off,
                                                 uint32_t* __restrict__ par_n,
                                                 unsigned long long* __restrict__ counters, unsigned long long cand_cap,
-                                                DevStatus* st) {
+                                                DevStatus* st, unsigned long long* __restrict__ cand_val) {
   constexpr int PB = Tile<N>::PB;
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG;
@@ -262,7 +262,12 @@ __global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ fro
     if (!d.err) {
       unsigned long long fp = successor_fp<SPEC, N>(s, d, sH + p * nperm, nperm);
       unsigned long long val = ((unsigned long long)level << 48) | (pg << 10) | (unsigned long long)d.ordinal;
-      slot = table_insert(table, mask, fp, val, level, st);
+      if (cand_val) {  // sharded search: the fp's owner inserts it (k_insert_recv)
+        slot = fp == EMPTY ? EMPTY - 1 : fp;
+        cand_val[t] = val;
+      } else {
+        slot = table_insert(table, mask, fp, val, level, st);
+      }
     }
     cand_slot[t] = slot;
     cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? 0x8000u : 0u);
@@ -378,6 +383,143 @@ __global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict_
   }
 }
 
+// ------------------------------------------------- sharded search
+// Owner of a fingerprint among W shards: multiply-shift range reduction of the
+// high word (the table slot uses the low bits, so the two are independent).
+__host__ __device__ __forceinline__ int fp_owner(unsigned long long fp, int W) {
+  return (int)(((fp >> 32) * (unsigned long long)W) >> 32);
+}
+
+// Per-owner candidate counts, one atomic per (wave, owner).
+__global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* __restrict__ cand_fp,
+                                                     const uint32_t* __restrict__ cand_ob, unsigned long long n, int W,
+                                                     unsigned int* __restrict__ counts) {
+  unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int o = -1;
+  if (t < n && !(cand_ob[t] & 0x8000u)) o = fp_owner(cand_fp[t], W);
+  const int lane = lane_id();
+  unsigned long long pending = __ballot(o >= 0);
+  while (pending) {
+    int leader = __ffsll((long long)pending) - 1;
+    int lo = __shfl(o, leader, WAVE);
+    unsigned long long m = __ballot(o == lo);
+    if (lane == leader) atomicAdd(&counts[lo], (unsigned)__popcll(m));
+    pending &= ~m;
+  }
+}
+
+// Scatter (fp, val) records into per-owner segments of the send buffer;
+// perm[t] = the record's position (replies come back in send order).
+__global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __restrict__ cand_fp,
+                                                const unsigned long long* __restrict__ cand_val,
+                                                const uint32_t* __restrict__ cand_ob, unsigned long long n, int W,
+                                                const unsigned int* __restrict__ seg_off,
+                                                unsigned int* __restrict__ cursor,
+                                                unsigned long long* __restrict__ send, uint32_t* __restrict__ perm) {
+  unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int o = -1;
+  unsigned long long fp = 0;
+  if (t < n && !(cand_ob[t] & 0x8000u)) {
+    fp = cand_fp[t];
+    o = fp_owner(fp, W);
+  }
+  const int lane = lane_id();
+  unsigned long long pending = __ballot(o >= 0);
+  while (pending) {
+    int leader = __ffsll((long long)pending) - 1;
+    int lo = __shfl(o, leader, WAVE);
+    unsigned long long m = __ballot(o == lo);
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(&cursor[lo], (unsigned)__popcll(m));
+    base = __shfl(base, leader, WAVE);
+    if (o == lo) {
+      unsigned pos = seg_off[lo] + base + (unsigned)__popcll(m & lanemask_lt());
+      send[2ULL * pos] = fp;
+      send[2ULL * pos + 1] = cand_val[t];
+      perm[t] = pos;
+    }
+    pending &= ~m;
+  }
+  if (t < n && o < 0) perm[t] = 0xFFFFFFFFu;
+}
+
+// Owner side: insert every received (fp, val); first in TLC order wins.
+__global__ __launch_bounds__(256) void k_insert_recv(const unsigned long long* __restrict__ recv, unsigned long long n,
+                                                     unsigned long long* __restrict__ table, unsigned long long mask,
+                                                     unsigned level, unsigned long long* __restrict__ recv_slot,
+                                                     DevStatus* st) {
+  unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  recv_slot[j] = table_insert(table, mask, recv[2 * j], recv[2 * j + 1], level, st);
+}
+
+// Owner side, after all of the round's inserts: did the record win its fp?
+// newcount += number of winners (= entries added to the table this round).
+__global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __restrict__ recv,
+                                                   const unsigned long long* __restrict__ recv_slot,
+                                                   unsigned long long n, const unsigned long long* __restrict__ table,
+                                                   uint8_t* __restrict__ flag, unsigned long long* __restrict__ newcount) {
+  unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  bool w = false;
+  if (j < n) {
+    w = table[2 * recv_slot[j] + 1] == recv[2 * j + 1];
+    flag[j] = w ? 1 : 0;
+  }
+  unsigned long long m = __ballot(w);
+  if (lane_id() == 0 && m) atomicAdd(newcount, (unsigned long long)__popcll(m));
+}
+
+// Generator side: per parent, winners (flags returned in send order) ranked
+// in TLC ordinal order, as k_mark does for the single-shard search.
+__global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, const uint32_t* __restrict__ par_off,
+                                                  const uint32_t* __restrict__ par_n,
+                                                  const uint32_t* __restrict__ perm,
+                                                  const uint8_t* __restrict__ flag_back,
+                                                  uint16_t* __restrict__ cand_win, uint32_t* __restrict__ par_win) {
+  unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nparents) return;
+  uint32_t off = par_off[p], n = par_n[p], cnt = 0;
+  for (uint32_t t = off; t < off + n; t++) {
+    uint32_t q = perm[t];
+    bool win = q != 0xFFFFFFFFu && flag_back[q];
+    cand_win[t] = win ? (uint16_t)(++cnt) : (uint16_t)0;
+  }
+  par_win[p] = cnt;
+}
+
+void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_ob, unsigned long long n, int W,
+                        unsigned int* counts, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_owner_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cand_fp, cand_ob, n, W, counts);
+}
+void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
+                   unsigned long long n, int W, const unsigned int* seg_off, unsigned int* cursor,
+                   unsigned long long* send, uint32_t* perm, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_bucket, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cand_fp, cand_val, cand_ob, n, W,
+                     seg_off, cursor, send, perm);
+}
+void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
+                        unsigned long long mask, unsigned level, unsigned long long* recv_slot, DevStatus* st,
+                        hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_insert_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, n, table, mask, level,
+                     recv_slot, st);
+}
+void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
+                      const unsigned long long* table, uint8_t* flag, unsigned long long* newcount, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, recv_slot, n, table, flag,
+                     newcount);
+}
+void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
+                     const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s) {
+  if (!nparents) return;
+  hipLaunchKernelGGL(k_mark_gen, dim3((unsigned)((nparents + 255) / 256)), dim3(256), 0, s, nparents, par_off, par_n,
+                     perm, flag_back, cand_win, par_win);
+}
+int host_fp_owner(unsigned long long fp, int W) { return fp_owner(fp, W); }
+
 // ------------------------------------------------------------ host driver
 struct Launch {
   template <int SPEC, int N>
@@ -388,7 +530,7 @@ struct Launch {
     ExpandLds L = expand_lds(PB, M.words, M.nperm, M.bind_words, M.ord_words);
     hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.level, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
-                       a.st);
+                       a.st, a.cand_val);
   }
   template <int SPEC, int N>
   static void materialize(const LevelArgs& a, hipStream_t s) {

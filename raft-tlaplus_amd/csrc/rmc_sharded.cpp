@@ -1,0 +1,755 @@
+// rmc_sharded.cpp — the fingerprint-sharded BFS over W shards:
+// one shard per GPU, one process per GPU, RCCL over xGMI; or W logical shards
+// driven by one process on one GPU (the same protocol with device copies as
+// the transport — SURVEY §4 item 5, "multi-GPU without a cluster").
+//
+// Exactness.  TLC keeps, per fingerprint, the successor first in its BFS
+// exploration order (parent position in the level, then the action's ordinal
+// in Next).  A level's states are distributed BLOCK-CYCLICALLY by their global
+// TLC position g: shard (g / CH) mod W holds g at local index
+// (g / (W·CH))·CH + g mod CH.  Round c of a level has every shard expand its
+// c-th local block, which together are the contiguous global range
+// [c·W·CH, (c+1)·W·CH): rounds are increasing in TLC order, so a fingerprint
+// won in an earlier round can never be displaced by a later one, and within a
+// round the owner's atomicMin on (parent gid, ordinal) picks TLC's winner.
+// The winners of a round are, in TLC order, the generators' winners in shard
+// order; they are written to their global positions (next level's block-
+// cyclic layout) by an all-to-all of state rows.
+//
+// Per round: expand (fp + key per candidate, no insert) -> bucket by owner ->
+// all-to-all (fp, key) 16 B -> owner inserts, then marks -> reverse all-to-all
+// of 1-byte win flags -> per-parent winner ranks, scan -> materialize into a
+// staging array -> all-to-all of rows + trace records to their owners.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+#include <rccl/rccl.h>
+#include "rmc_internal.h"
+
+using namespace rmc;
+
+namespace rmcx {
+
+// -------------------------------------------------------------- transports
+struct Xfer {
+  int src, dst;        // global shard ids
+  const void* sbuf;    // valid on the sender
+  void* rbuf;          // valid on the receiver
+  size_t bytes;
+};
+
+struct Comm {
+  int world = 1;
+  std::vector<int> local;  // global ids of the shards this process drives
+  virtual ~Comm() {}
+  // in[i] = the k values of local shard local[i]; out = world*k values by shard id
+  virtual void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) = 0;
+  // every transfer this process takes part in, in one global order
+  virtual void alltoallv(const std::vector<Xfer>& x) = 0;
+  hipStream_t stream = nullptr;
+};
+
+// All W shards in this process, on one GPU: transfers are device copies on the
+// shared stream (stream order is the synchronisation).
+struct LocalComm : Comm {
+  LocalComm(int W, hipStream_t s) {
+    world = W;
+    for (int i = 0; i < W; i++) local.push_back(i);
+    stream = s;
+  }
+  void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) override {
+    out.assign((size_t)world * k, 0);
+    for (int i = 0; i < world; i++)
+      for (int j = 0; j < k; j++) out[(size_t)i * k + j] = in[i][j];
+  }
+  void alltoallv(const std::vector<Xfer>& x) override {
+    for (auto& t : x)
+      if (t.bytes) HIPCHK(hipMemcpyAsync(t.rbuf, t.sbuf, t.bytes, hipMemcpyDeviceToDevice, stream));
+  }
+};
+
+#define NCCLCHK(x)                                                                                   \
+  do {                                                                                               \
+    ncclResult_t r_ = (x);                                                                           \
+    if (r_ != ncclSuccess) throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r_) + " at " #x); \
+  } while (0)
+
+// One shard per process (one process per GPU); RCCL point-to-point over xGMI.
+struct RcclComm : Comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0;
+  DevBuf gbuf;
+  RcclComm(int r, int W, const ncclUniqueId& id, hipStream_t s) {
+    rank = r;
+    world = W;
+    local = {r};
+    stream = s;
+    NCCLCHK(ncclCommInitRank(&comm, W, id, r));
+  }
+  ~RcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) override {
+    gbuf.ensure((size_t)world * k * 8 + (size_t)k * 8);
+    uint64_t* d = gbuf.as<uint64_t>();
+    uint64_t* mine = d + (size_t)world * k;
+    HIPCHK(hipMemcpyAsync(mine, in[0].data(), (size_t)k * 8, hipMemcpyHostToDevice, stream));
+    NCCLCHK(ncclAllGather(mine, d, (size_t)k, ncclUint64, comm, stream));
+    out.assign((size_t)world * k, 0);
+    HIPCHK(hipMemcpyAsync(out.data(), d, (size_t)world * k * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  void alltoallv(const std::vector<Xfer>& x) override {
+    NCCLCHK(ncclGroupStart());
+    for (auto& t : x) {
+      if (!t.bytes) continue;
+      if (t.src == rank && t.dst == rank) {
+        HIPCHK(hipMemcpyAsync(t.rbuf, t.sbuf, t.bytes, hipMemcpyDeviceToDevice, stream));
+      } else if (t.src == rank) {
+        NCCLCHK(ncclSend(t.sbuf, t.bytes, ncclChar, t.dst, comm, stream));
+      } else if (t.dst == rank) {
+        NCCLCHK(ncclRecv(t.rbuf, t.bytes, ncclChar, t.src, comm, stream));
+      }
+    }
+    NCCLCHK(ncclGroupEnd());
+  }
+};
+
+// ---------------------------------------------------------- shard buffers
+struct ShardBufs {
+  DevBuf table, table2, fa, fb, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, trp, trb, small;
+  void release() {
+    for (DevBuf* b : {&table, &table2, &fa, &fb, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters,
+                      &stbuf, &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &trp, &trb,
+                      &small})
+      b->release();
+  }
+};
+static std::mutex g_shard_mu;
+static std::map<std::pair<int, int>, ShardBufs*> g_shard_bufs;
+static ShardBufs& shard_bufs(int slot) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_shard_mu);
+  ShardBufs*& b = g_shard_bufs[{dev, slot}];
+  if (!b) b = new ShardBufs();
+  return *b;
+}
+void release_shard_buffers() {
+  std::lock_guard<std::mutex> lk(g_shard_mu);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto& kv : g_shard_bufs)
+    if (hipSetDevice(kv.first.first) == hipSuccess) kv.second->release();
+  (void)hipSetDevice(cur);
+}
+
+struct Shard {
+  int id = 0;
+  ShardBufs* B = nullptr;
+  unsigned long long slots = 0, entries = 0;
+  uint32_t *cur = nullptr, *nxt = nullptr;
+  unsigned long long fcap = 0;       // states per frontier buffer
+  unsigned long long ncur = 0;       // local states of the current level
+  unsigned long long next_fill = 0;  // local states of the next level written so far
+  unsigned long long trcap = 0;      // trace records
+  std::vector<unsigned long long> tr_base;  // local trace index of each level's first local state (by depth)
+  unsigned long long ncand = 0, nrecv = 0, nwin = 0, n = 0;
+  std::vector<uint64_t> seg_off, rseg_off;  // send segments by owner / recv segments by source
+  DevStatus hst;
+};
+
+static unsigned long long local_count(unsigned long long P, int W, unsigned long long CH, int r) {
+  unsigned long long full = P / (W * CH), rem = P - full * W * CH;
+  long long part = (long long)rem - (long long)r * (long long)CH;
+  part = part < 0 ? 0 : (part > (long long)CH ? (long long)CH : part);
+  return full * CH + (unsigned long long)part;
+}
+
+static void table_grow(Shard& s, unsigned long long need_entries, hipStream_t stream, const rmc_options* opt) {
+  if (need_entries * 2 <= s.slots) return;
+  if (opt->hash_slots) throw std::runtime_error("fingerprint set full (raise hash_slots)");
+  unsigned long long nslots = s.slots;
+  while (need_entries * 2 > nslots) nslots <<= 1;
+  DevBuf& nt = s.B->table2;
+  nt.ensure(nslots * 16);
+  HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
+  launch_rehash(s.B->table.as<unsigned long long>(), s.slots, nt.as<unsigned long long>(), nslots - 1,
+                s.B->stbuf.as<DevStatus>(), stream);
+  HIPCHK(hipGetLastError());
+  std::swap(s.B->table.p, nt.p);
+  std::swap(s.B->table.bytes, nt.bytes);
+  s.slots = nslots;
+}
+
+// grow a frontier / trace buffer keeping its first `keep` bytes (stream-ordered)
+static void grow_keep(DevBuf& b, size_t need, size_t keep, hipStream_t stream) {
+  if (b.p && b.bytes >= need) return;
+  size_t nb = std::max(need, b.bytes * 2);
+  void* q = nullptr;
+  HIPCHK(hipStreamSynchronize(stream));
+  HIPCHK(hipMalloc(&q, nb));
+  if (b.p && keep) HIPCHK(hipMemcpy(q, b.p, keep, hipMemcpyDeviceToDevice));
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = q;
+  b.bytes = nb;
+}
+
+// Returns 1 when the check must be re-run with a larger message capacity.
+static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, rmc_result* res) {
+  auto t0 = std::chrono::steady_clock::now();
+  Model& M = m->M;
+  if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
+  if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("only 64-bit fingerprints are supported");
+  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : default_kmax(M));
+  if (kmax > 120) kmax = 120;
+  finalize_model(m, kmax);
+  HIPCHK(upload_model(M));
+  hipStream_t stream = comm.stream;
+  const int W = comm.world;
+  const size_t WD = (size_t)M.words;
+  res->state_bytes = (uint32_t)(WD * 4);
+  const int maxsucc = M.nfixed + M.kmax;
+  const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 20);
+  const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
+  const int NL = (int)comm.local.size();
+
+  std::vector<Shard> sh(NL);
+  for (int i = 0; i < NL; i++) {
+    Shard& s = sh[i];
+    s.id = comm.local[i];
+    s.B = &shard_bufs(i);
+    ShardBufs& B = *s.B;
+    s.slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 24, m->hint_slots);
+    if (s.slots & (s.slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
+    B.table.ensure(s.slots * 16);
+    HIPCHK(hipMemsetAsync(B.table.p, 0xFF, s.slots * 16, stream));
+    s.fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 20, m->hint_fcap);
+    B.fa.ensure(s.fcap * WD * 4);
+    B.fb.ensure(s.fcap * WD * 4);
+    s.cur = B.fa.as<uint32_t>();
+    s.nxt = B.fb.as<uint32_t>();
+    B.cfp.ensure(cand_cap * 8);
+    B.cval.ensure(cand_cap * 8);
+    B.cob.ensure(cand_cap * 4);
+    B.cwin.ensure(cand_cap * 2);
+    B.perm.ensure(cand_cap * 4);
+    B.poff.ensure(CH * 4);
+    B.pn.ensure(CH * 4);
+    B.pwin.ensure(CH * 4);
+    B.ppos.ensure(CH * 4);
+    B.counters.ensure(64);
+    B.stbuf.ensure(sizeof(DevStatus));
+    size_t stb = scan_temp_bytes(CH);
+    B.scantmp.ensure(stb ? stb : 16);
+    B.small.ensure(4096);
+    s.trcap = std::max(s.fcap * 4, m->hint_trcap);
+    B.trp.ensure(s.trcap * 8);
+    B.trb.ensure(s.trcap * 2);
+    s.hst.err_key = s.hst.inv_err_key = s.hst.viol_key = ~0ULL;
+    s.hst.cap_flags = 0;
+    s.hst.pad = 0;
+    HIPCHK(hipMemcpyAsync(B.stbuf.p, &s.hst, sizeof s.hst, hipMemcpyHostToDevice, stream));
+  }
+
+  // ---- level 1: Init on shard 0 (global position 0); its fp on its owner
+  std::vector<uint32_t> init = init_state(M);
+  unsigned long long fp0 = host_fingerprint(M, init.data());
+  if (fp0 == ~0ULL) fp0--;
+  const int owner0 = host_fp_owner(fp0, W);
+  for (Shard& s : sh) {
+    s.tr_base.assign(2, 0);  // index by depth (1-based)
+    s.ncur = s.id == 0 ? 1 : 0;
+    s.tr_base.push_back(s.ncur);  // tr_base[2] = first record of level 2
+    if (s.id == 0) {
+      HIPCHK(hipMemcpyAsync(s.cur, init.data(), WD * 4, hipMemcpyHostToDevice, stream));
+      unsigned long long root = ~0ULL;
+      uint16_t zero = 0;
+      HIPCHK(hipMemcpyAsync(s.B->trp.p, &root, 8, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(s.B->trb.p, &zero, 2, hipMemcpyHostToDevice, stream));
+    }
+    if (s.id == owner0) {
+      unsigned long long slot = (fp0 ^ (fp0 >> 29)) & (s.slots - 1);
+      unsigned long long ent[2] = {fp0, (1ULL << 48)};
+      HIPCHK(hipMemcpyAsync(s.B->table.as<unsigned long long>() + 2 * slot, ent, 16, hipMemcpyHostToDevice, stream));
+      s.entries = 1;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  m->levels.clear();
+  m->trace_states.clear();
+  m->trace_actions.clear();
+  std::vector<unsigned long long> level_base = {0, 0}, level_size = {0, 1};  // by depth
+  unsigned long long generated = 1, distinct = 1, P = 1;
+  unsigned depth = 1;
+  m->levels.push_back({1, 1});
+  int status = 0;
+  std::string message;
+  unsigned long long bad_key = ~0ULL, bad_state = ~0ULL;
+  {
+    int err = 0;
+    int bad = host_check_invariants(M, init.data(), &err);
+    if (err) { status = 2; message = "evaluation error in an invariant on the initial state"; bad_state = 0; }
+    else if (bad >= 0) { status = 1; snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str()); bad_state = 0; }
+  }
+  EventTimer te, tz;
+  double expand_ms = 0, mat_ms = 0;
+  unsigned long long expand_launches = 0;
+  std::vector<std::vector<uint64_t>> rows(NL);
+  std::vector<uint64_t> all;
+  auto read_status = [&](Shard& s) {
+    HIPCHK(hipMemcpyAsync(&s.hst, s.B->stbuf.p, sizeof s.hst, hipMemcpyDeviceToHost, stream));
+  };
+  bool stop = false;
+  while (status == 0 && P > 0 && !stop) {
+    if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
+    const unsigned level = depth + 1;
+    if (level >= 0xFFFF) throw std::runtime_error("too many levels");
+    const unsigned long long rounds = (P + W * CH - 1) / (W * CH);
+    const unsigned long long lbase = level_base[depth];
+    unsigned long long GW = 0, gen_lvl = 0;
+    for (Shard& s : sh) s.next_fill = 0;
+    for (unsigned long long c = 0; c < rounds && !stop; c++) {
+      // ---- expand: fp + key per candidate
+      for (Shard& s : sh) {
+        s.n = s.ncur > c * CH ? std::min(CH, s.ncur - c * CH) : 0;
+        HIPCHK(hipMemsetAsync(s.B->counters.p, 0, 64, stream));
+        if (s.n) {
+          LevelArgs a;
+          memset(&a, 0, sizeof a);
+          a.model = &M;
+          a.frontier = s.cur + c * CH * WD;
+          a.nparents = s.n;
+          a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
+          a.level = level;
+          a.cand_slot = s.B->cfp.as<unsigned long long>();
+          a.cand_val = s.B->cval.as<unsigned long long>();
+          a.cand_ob = s.B->cob.as<uint32_t>();
+          a.par_off = s.B->poff.as<uint32_t>();
+          a.par_n = s.B->pn.as<uint32_t>();
+          a.counters = s.B->counters.as<unsigned long long>();
+          a.cand_cap = cand_cap;
+          a.st = s.B->stbuf.as<DevStatus>();
+          HIPCHK(hipEventRecord(te.a, stream));
+          launch_expand(M.spec, M.N, a, stream);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipEventRecord(te.b, stream));
+          HIPCHK(hipEventSynchronize(te.b));
+          float ms = 0;
+          HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
+          expand_ms += ms;
+          expand_launches++;
+        }
+        HIPCHK(hipMemcpyAsync(&s.ncand, s.B->counters.p, 8, hipMemcpyDeviceToHost, stream));
+        read_status(s);
+      }
+      HIPCHK(hipStreamSynchronize(stream));
+      for (int i = 0; i < NL; i++) rows[i] = {sh[i].ncand, sh[i].hst.cap_flags};
+      comm.allgather(rows, all, 2);
+      unsigned capf = 0;
+      for (int r = 0; r < W; r++) { gen_lvl += all[2 * r]; capf |= (unsigned)all[2 * r + 1]; }
+      if (capf) {
+        int e = 0;
+        while (!((capf >> e) & 1)) e++;
+        if (e == E_CAP_MSG && !opt->msg_cap_K && kmax < 120) {
+          m->kmax_user = std::min(120u, kmax * 2);
+          return 1;
+        }
+        status = 3;
+        message = "capacity overflow (sharded search, code " + std::to_string(e) + ")";
+        break;
+      }
+      // ---- bucket by owner, exchange counts
+      for (Shard& s : sh) {
+        unsigned int* cnt = s.B->small.as<unsigned int>();  // [0,W) counts, [W,2W) offsets, [2W,3W) cursors
+        HIPCHK(hipMemsetAsync(cnt, 0, 3 * W * 4, stream));
+        launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, cnt, stream);
+        HIPCHK(hipGetLastError());
+      }
+      std::vector<std::vector<unsigned int>> cnts(NL, std::vector<unsigned int>(W));
+      for (int i = 0; i < NL; i++)
+        HIPCHK(hipMemcpyAsync(cnts[i].data(), sh[i].B->small.p, W * 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      for (int i = 0; i < NL; i++) rows[i].assign(cnts[i].begin(), cnts[i].end());
+      comm.allgather(rows, all, W);  // all[src*W + dst] = records src sends to dst
+      for (int i = 0; i < NL; i++) {
+        Shard& s = sh[i];
+        s.seg_off.assign(W + 1, 0);
+        for (int d = 0; d < W; d++) s.seg_off[d + 1] = s.seg_off[d] + all[(size_t)s.id * W + d];
+        s.rseg_off.assign(W + 1, 0);
+        for (int q = 0; q < W; q++) s.rseg_off[q + 1] = s.rseg_off[q] + all[(size_t)q * W + s.id];
+        s.nrecv = s.rseg_off[W];
+        std::vector<unsigned int> off(W);
+        for (int d = 0; d < W; d++) off[d] = (unsigned int)s.seg_off[d];
+        unsigned int* dev = s.B->small.as<unsigned int>();
+        HIPCHK(hipMemcpyAsync(dev + W, off.data(), W * 4, hipMemcpyHostToDevice, stream));
+        s.B->send.ensure(std::max<size_t>(16, s.seg_off[W] * 16));
+        s.B->sflag.ensure(std::max<size_t>(1, s.seg_off[W]));
+        s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
+        s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
+        s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
+        launch_bucket(s.B->cfp.as<unsigned long long>(), s.B->cval.as<unsigned long long>(), s.B->cob.as<uint32_t>(),
+                      s.ncand, W, dev + W, dev + 2 * W, s.B->send.as<unsigned long long>(), s.B->perm.as<uint32_t>(),
+                      stream);
+        HIPCHK(hipGetLastError());
+      }
+      // ---- (fp, key) records to their owners
+      {
+        std::vector<Xfer> x;
+        for (int q = 0; q < W; q++)
+          for (int d = 0; d < W; d++) {
+            size_t cntqd = all[(size_t)q * W + d];
+            if (!cntqd) continue;
+            Xfer t{q, d, nullptr, nullptr, cntqd * 16};
+            for (Shard& s : sh) {
+              if (s.id == q) t.sbuf = s.B->send.as<unsigned long long>() + 2 * s.seg_off[d];
+              if (s.id == d) t.rbuf = s.B->recv.as<unsigned long long>() + 2 * s.rseg_off[q];
+            }
+            x.push_back(t);
+          }
+        comm.alltoallv(x);
+      }
+      // ---- owners insert, then mark
+      for (Shard& s : sh) {
+        table_grow(s, s.entries + s.nrecv, stream, opt);
+        launch_insert_recv(s.B->recv.as<unsigned long long>(), s.nrecv, s.B->table.as<unsigned long long>(),
+                           s.slots - 1, level, s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
+        HIPCHK(hipGetLastError());
+      }
+      for (Shard& s : sh) {
+        unsigned long long* nc = s.B->counters.as<unsigned long long>() + 1;
+        launch_mark_recv(s.B->recv.as<unsigned long long>(), s.B->rslot.as<unsigned long long>(), s.nrecv,
+                         s.B->table.as<unsigned long long>(), s.B->rflag.as<uint8_t>(), nc, stream);
+        HIPCHK(hipGetLastError());
+      }
+      // ---- win flags back to the generators (reverse of the record exchange)
+      {
+        std::vector<Xfer> x;
+        for (int q = 0; q < W; q++)
+          for (int d = 0; d < W; d++) {
+            size_t cntqd = all[(size_t)q * W + d];
+            if (!cntqd) continue;
+            Xfer t{d, q, nullptr, nullptr, cntqd};
+            for (Shard& s : sh) {
+              if (s.id == d) t.sbuf = s.B->rflag.as<uint8_t>() + s.rseg_off[q];
+              if (s.id == q) t.rbuf = s.B->sflag.as<uint8_t>() + s.seg_off[d];
+            }
+            x.push_back(t);
+          }
+        comm.alltoallv(x);
+      }
+      // ---- generators: winner ranks per parent, positions
+      std::vector<unsigned long long> newc(NL, 0);
+      for (int i = 0; i < NL; i++) {
+        Shard& s = sh[i];
+        s.nwin = 0;
+        if (s.n) {
+          launch_mark_gen(s.n, s.B->poff.as<uint32_t>(), s.B->pn.as<uint32_t>(), s.B->perm.as<uint32_t>(),
+                          s.B->sflag.as<uint8_t>(), s.B->cwin.as<uint16_t>(), s.B->pwin.as<uint32_t>(), stream);
+          HIPCHK(hipGetLastError());
+          launch_scan(s.B->scantmp.p, s.B->scantmp.bytes, s.B->pwin.as<uint32_t>(), s.B->ppos.as<uint32_t>(), s.n,
+                      stream);
+          HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemcpyAsync(&newc[i], s.B->counters.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, stream));
+      }
+      std::vector<uint32_t> lastpos(NL, 0), lastwin(NL, 0);
+      for (int i = 0; i < NL; i++)
+        if (sh[i].n) {
+          HIPCHK(hipMemcpyAsync(&lastpos[i], sh[i].B->ppos.as<uint32_t>() + sh[i].n - 1, 4, hipMemcpyDeviceToHost, stream));
+          HIPCHK(hipMemcpyAsync(&lastwin[i], sh[i].B->pwin.as<uint32_t>() + sh[i].n - 1, 4, hipMemcpyDeviceToHost, stream));
+        }
+      HIPCHK(hipStreamSynchronize(stream));
+      for (int i = 0; i < NL; i++) {
+        sh[i].nwin = (unsigned long long)lastpos[i] + lastwin[i];
+        sh[i].entries += newc[i];
+        HIPCHK(hipMemsetAsync(sh[i].B->counters.as<unsigned long long>() + 1, 0, 8, stream));
+        rows[i] = {sh[i].nwin};
+      }
+      comm.allgather(rows, all, 1);  // all[r] = winners generated by shard r this round
+      std::vector<unsigned long long> go(W + 1, 0);
+      for (int r = 0; r < W; r++) go[r + 1] = go[r] + all[r];
+      // ---- materialize winners into staging (TLC order within the generator)
+      for (Shard& s : sh) {
+        if (!s.n || !s.nwin) continue;
+        s.B->stage.ensure(s.nwin * WD * 4);
+        s.B->stp.ensure(s.nwin * 8);
+        s.B->stb.ensure(s.nwin * 2);
+        LevelArgs a;
+        memset(&a, 0, sizeof a);
+        a.model = &M;
+        a.frontier = s.cur + c * CH * WD;
+        a.nparents = s.n;
+        a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
+        a.level = level;
+        a.cand_ob = s.B->cob.as<uint32_t>();
+        a.cand_win = s.B->cwin.as<uint16_t>();
+        a.par_off = s.B->poff.as<uint32_t>();
+        a.par_n = s.B->pn.as<uint32_t>();
+        a.par_pos = s.B->ppos.as<uint32_t>();
+        a.out = s.B->stage.as<uint32_t>();
+        a.out_base_global = 0;
+        a.tr_parent = s.B->stp.as<unsigned long long>();
+        a.tr_bind = s.B->stb.as<uint16_t>();
+        a.st = s.B->stbuf.as<DevStatus>();
+        HIPCHK(hipEventRecord(tz.a, stream));
+        launch_materialize(M.spec, M.N, a, stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(tz.b, stream));
+        HIPCHK(hipEventSynchronize(tz.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, tz.a, tz.b));
+        mat_ms += ms;
+      }
+      // ---- rows + trace records to their next-level owners (block-cyclic by global position)
+      {
+        struct Piece { int q, d; unsigned long long a, b, dl; };
+        std::vector<Piece> pcs;
+        for (int q = 0; q < W; q++) {
+          unsigned long long a = GW + go[q], end = GW + go[q + 1];
+          while (a < end) {
+            unsigned long long blk = a / CH, b = std::min(end, (blk + 1) * CH);
+            pcs.push_back({q, (int)(blk % W), a, b, (blk / W) * CH + a % CH});
+            a = b;
+          }
+        }
+        for (Shard& s : sh) {  // capacity of the receiving side
+          unsigned long long need = s.next_fill;
+          for (auto& pc : pcs)
+            if (pc.d == s.id) need = std::max(need, pc.dl + (pc.b - pc.a));
+          if (need > s.fcap) {
+            unsigned long long nf = s.fcap;
+            while (need > nf) nf *= 2;
+            bool cur_is_a = s.cur == s.B->fa.as<uint32_t>();
+            DevBuf& cb = cur_is_a ? s.B->fa : s.B->fb;
+            DevBuf& nb = cur_is_a ? s.B->fb : s.B->fa;
+            grow_keep(cb, nf * WD * 4, s.ncur * WD * 4, stream);
+            grow_keep(nb, nf * WD * 4, s.next_fill * WD * 4, stream);
+            s.cur = cb.as<uint32_t>();
+            s.nxt = nb.as<uint32_t>();
+            s.fcap = nf;
+          }
+          unsigned long long trneed = s.tr_base[depth + 1] + need;
+          if (trneed > s.trcap) {
+            unsigned long long nt = s.trcap;
+            while (trneed > nt) nt *= 2;
+            grow_keep(s.B->trp, nt * 8, s.tr_base[depth + 1] * 8 + s.next_fill * 8, stream);
+            grow_keep(s.B->trb, nt * 2, s.tr_base[depth + 1] * 2 + s.next_fill * 2, stream);
+            s.trcap = nt;
+          }
+          s.next_fill = need;
+        }
+        std::vector<Xfer> x;
+        for (auto& pc : pcs) {
+          unsigned long long cnt = pc.b - pc.a, so = pc.a - (GW + go[pc.q]);
+          Xfer rowsx{pc.q, pc.d, nullptr, nullptr, cnt * WD * 4};
+          Xfer parx{pc.q, pc.d, nullptr, nullptr, cnt * 8};
+          Xfer bndx{pc.q, pc.d, nullptr, nullptr, cnt * 2};
+          for (Shard& s : sh) {
+            if (s.id == pc.q) {
+              rowsx.sbuf = s.B->stage.as<uint32_t>() + so * WD;
+              parx.sbuf = s.B->stp.as<unsigned long long>() + so;
+              bndx.sbuf = s.B->stb.as<uint16_t>() + so;
+            }
+            if (s.id == pc.d) {
+              unsigned long long tr = s.tr_base[depth + 1] + pc.dl;
+              rowsx.rbuf = s.nxt + pc.dl * WD;
+              parx.rbuf = s.B->trp.as<unsigned long long>() + tr;
+              bndx.rbuf = s.B->trb.as<uint16_t>() + tr;
+            }
+          }
+          x.push_back(rowsx);
+          x.push_back(parx);
+          x.push_back(bndx);
+        }
+        comm.alltoallv(x);
+      }
+      GW += go[W];
+      // ---- first problem in TLC order stops the search (as TLC does)
+      for (Shard& s : sh) read_status(s);
+      HIPCHK(hipStreamSynchronize(stream));
+      for (int i = 0; i < NL; i++) rows[i] = {sh[i].hst.err_key, sh[i].hst.inv_err_key, sh[i].hst.viol_key, sh[i].hst.cap_flags};
+      comm.allgather(rows, all, 4);
+      unsigned long long ek = ~0ULL, iek = ~0ULL, vk = ~0ULL;
+      unsigned capm = 0;
+      for (int r = 0; r < W; r++) {
+        ek = std::min(ek, (unsigned long long)all[4 * r]);
+        iek = std::min(iek, (unsigned long long)all[4 * r + 1]);
+        vk = std::min(vk, (unsigned long long)all[4 * r + 2]);
+        capm |= (unsigned)all[4 * r + 3];
+      }
+      if (capm) {
+        status = 3;
+        message = "capacity overflow while materializing";
+        stop = true;
+      } else if (ek != ~0ULL || iek != ~0ULL || vk != ~0ULL) {
+        unsigned long long k_err = std::min(ek, iek);
+        if (k_err < vk) {
+          status = 2;
+          bad_key = k_err;
+          message = ek <= iek ? "evaluation error in the next-state relation (a sequence applied outside its domain)"
+                              : "evaluation error while checking an invariant";
+        } else {
+          status = 1;
+          bad_key = vk;
+        }
+        stop = true;
+      }
+    }
+    generated += gen_lvl;
+    distinct += GW;
+    if (GW || gen_lvl) m->levels.push_back({gen_lvl, GW});
+    level_base.push_back(lbase + P);
+    level_size.push_back(GW);
+    if (GW) depth++;
+    for (Shard& s : sh) {
+      s.tr_base.push_back(s.tr_base[depth] + local_count(GW, W, CH, s.id));
+      s.ncur = local_count(GW, W, CH, s.id);
+      std::swap(s.cur, s.nxt);
+    }
+    P = GW;
+    if (opt->verbose && comm.local[0] == 0)
+      fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated (%d shards)\n", depth,
+              (unsigned long long)GW, (unsigned long long)distinct, (unsigned long long)generated, W);
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  // ---- trace: walk the distributed parent records from the failing state to Init
+  if (status == 1 || status == 2) {
+    unsigned long long g = ~0ULL;
+    int last_b = -1;
+    if (bad_key != ~0ULL) {
+      g = bad_key >> 20;
+      last_b = (int)(bad_key & 0x3FF);
+    } else if (bad_state != ~0ULL) {
+      g = bad_state;
+    }
+    std::vector<int> binds;
+    while (g != ~0ULL && g != 0) {
+      int L = 1;
+      while (L + 1 < (int)level_base.size() && level_base[L + 1] <= g) L++;
+      unsigned long long pos = g - level_base[L];
+      int owner = (int)((pos / CH) % W);
+      unsigned long long li = (pos / (W * CH)) * CH + pos % CH;
+      for (int i = 0; i < NL; i++) {
+        Shard& s = sh[i];
+        unsigned long long pp = 0;
+        uint16_t bb = 0;
+        if (s.id == owner) {
+          HIPCHK(hipMemcpy(&pp, s.B->trp.as<unsigned long long>() + s.tr_base[L] + li, 8, hipMemcpyDeviceToHost));
+          HIPCHK(hipMemcpy(&bb, s.B->trb.as<uint16_t>() + s.tr_base[L] + li, 2, hipMemcpyDeviceToHost));
+        }
+        rows[i] = {pp, bb};
+      }
+      comm.allgather(rows, all, 2);
+      binds.push_back((int)all[2 * owner + 1]);
+      g = all[2 * owner];
+    }
+    std::reverse(binds.begin(), binds.end());
+    replay_trace(m, binds, last_b, status, message, res);
+  }
+  if (!opt->hash_slots) m->hint_slots = sh[0].slots;
+  if (!opt->frontier_cap) m->hint_fcap = sh[0].fcap;
+  m->hint_trcap = sh[0].trcap;
+  res->generated = generated;
+  res->distinct = distinct;
+  res->left_on_queue = status == 0 ? 0 : P;
+  res->depth = depth;
+  res->status = status;
+  snprintf(res->message, sizeof res->message, "%s", message.c_str());
+  res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  res->expand_ms = expand_ms;
+  res->materialize_ms = mat_ms;
+  res->expand_launches = expand_launches;
+  res->hash_capacity = sh[0].slots;
+  return 0;
+}
+
+static int run_with_regrow(rmc_model* m, const rmc_options* o, Comm& comm, rmc_result* out) {
+  m->kmax_user = 0;
+  int rc;
+  while ((rc = check_sharded_impl(m, o, comm, out)) == 1) memset(out, 0, sizeof *out);
+  return rc;
+}
+
+}  // namespace rmcx
+
+using namespace rmcx;
+
+extern "C" {
+
+int rmc_comm_unique_id(unsigned char* id) {
+  if (!id) return -1;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) {
+    set_last_error("ncclGetUniqueId failed");
+    return -6;
+  }
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, int device, const unsigned char* id,
+                      rmc_result* out) {
+  if (!m || !out || !id || world < 1 || rank < 0 || rank >= world) { set_last_error("bad argument"); return -1; }
+  rmc_options def;
+  rmc_options_default(&def);
+  if (!o) o = &def;
+  memset(out, 0, sizeof *out);
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+      set_last_error("no HIP device available: the raftmc GPU path requires an MI355X (gfx950)");
+      return -4;
+    }
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    int rc;
+    {
+      RcclComm comm(rank, world, u, s);
+      rc = run_with_regrow(m, o, comm, out);
+    }
+    HIPCHK(hipStreamDestroy(s));
+    return rc;
+  } catch (std::exception& e) {
+    set_last_error(e.what());
+    return -5;
+  }
+}
+
+int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result* out) {
+  if (!m || !out || shards < 1 || shards > 64) { set_last_error("bad argument"); return -1; }
+  rmc_options def;
+  rmc_options_default(&def);
+  if (!o) o = &def;
+  memset(out, 0, sizeof *out);
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+      set_last_error("no HIP device available: the raftmc GPU path requires an MI355X (gfx950)");
+      return -4;
+    }
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int rc;
+    {
+      LocalComm comm(shards, s);
+      rc = run_with_regrow(m, o, comm, out);
+    }
+    HIPCHK(hipStreamDestroy(s));
+    return rc;
+  } catch (std::exception& e) {
+    set_last_error(e.what());
+    return -5;
+  }
+}
+
+}  // extern "C"

@@ -48,7 +48,7 @@ class Result(ctypes.Structure):
 EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_check",
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
-           "rmc_release_device_memory"]
+           "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical"]
 
 _lib = None
 
@@ -74,6 +74,10 @@ def lib():
     L.rmc_last_error.restype = ctypes.c_char_p
     L.rmc_version.restype = ctypes.c_char_p
     L.rmc_levels.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), c_int]
+    L.rmc_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
+                                    ctypes.POINTER(Result)]
+    L.rmc_check_logical.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(Result)]
     L.rmc_selftest_host_bfs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64,
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), c_int]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
@@ -102,17 +106,18 @@ class Model:
             _lib.rmc_model_free(self._h)
             self._h = None
 
-    def check(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
-              chunk_parents=0, verbose=False, max_depth=0, workers=0):
-        """Run the model check on the GPU; returns a dict of TLC's results."""
+    def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
+                 chunk_parents=0, verbose=False, max_depth=0, workers=0):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
         o.deadlock_check = 1 if deadlock else 0
         o.hash_slots, o.msg_cap_K, o.frontier_cap = hash_slots, msg_cap_K, frontier_cap
         o.chunk_parents, o.verbose, o.max_depth, o.cpu_workers = chunk_parents, int(verbose), max_depth, workers
-        r = Result()
-        rc = L.rmc_check(self._h, ctypes.byref(o), ctypes.byref(r))
+        return o
+
+    def _result(self, rc, r):
+        L = lib()
         if rc != 0:
             raise RaftmcError(L.rmc_last_error().decode())
         levels = (ctypes.c_uint64 * 2048)()
@@ -128,6 +133,24 @@ class Model:
         if r.status in (1, 2):
             out["trace"] = self.trace()
         return out
+
+    def check(self, **kw):
+        """Run the model check on this process's GPU; returns a dict of TLC's results."""
+        o, r = self._options(**kw), Result()
+        return self._result(lib().rmc_check(self._h, ctypes.byref(o), ctypes.byref(r)), r)
+
+    def check_logical(self, shards, **kw):
+        """The fingerprint-sharded protocol with `shards` logical shards on this GPU."""
+        o, r = self._options(**kw), Result()
+        return self._result(lib().rmc_check_logical(self._h, ctypes.byref(o), int(shards), ctypes.byref(r)), r)
+
+    def check_sharded(self, rank, world, device, unique_id, **kw):
+        """One shard of a multi-GPU check (one process per GPU, RCCL).  unique_id =
+        comm_unique_id() from rank 0, shared with every rank out of band."""
+        o, r = self._options(**kw), Result()
+        rc = lib().rmc_check_sharded(self._h, ctypes.byref(o), int(rank), int(world), int(device),
+                                     bytes(unique_id), ctypes.byref(r))
+        return self._result(rc, r)
 
     def trace(self):
         L = lib()
@@ -164,6 +187,14 @@ class Model:
 def check(tla_path, cfg_path=None, **kw):
     """TLC-equivalent run: check(M.tla, M.cfg) -> dict (generated, distinct, depth, ...)."""
     return Model(tla_path, cfg_path).check(**kw)
+
+
+def comm_unique_id():
+    """128-byte RCCL communicator id (call on rank 0, broadcast to every rank)."""
+    buf = ctypes.create_string_buffer(128)
+    if lib().rmc_comm_unique_id(buf) != 0:
+        raise RaftmcError(lib().rmc_last_error().decode())
+    return buf.raw
 
 
 def check_text(module, cfg_text, **kw):
