@@ -8,9 +8,12 @@ are the input; the frontier, fingerprint set and trace records never leave
 the GPU while timed).  `value` = distinct states / seconds-per-check, summed
 over ranks.
 
-Multi-GPU: one process per GPU (torch.distributed.run).  The fingerprint-
-sharded multi-GPU search is not built yet, so N>1 runs N independent replica
-checks ("parallelism": "replicas").
+Multi-GPU: one process per GPU (torch.distributed.run).  N>1 runs ONE check
+of the same workload, fingerprint-sharded across the N GPUs (rmc_check_sharded:
+RCCL over xGMI); every rank gets the global counts.  Total work
+is fixed as N grows ("scaling": "strong"); `value` = distinct states of the
+check / seconds per check.  --logical-shards W runs the same sharded protocol
+with W shards on one GPU (a measurement of the protocol's overhead).
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 """
@@ -91,6 +94,7 @@ def main():
     ap.add_argument("--workload", default=os.environ.get("RMC_WORKLOAD", DEFAULT_WORKLOAD))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--logical-shards", type=int, default=0)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -107,6 +111,14 @@ def main():
 
     module, cfg_rel, bcfg, desc = WORKLOADS[args.workload]
     model = raftmc.Model(os.path.join(ROOT, "configs", module + ".tla"), os.path.join(ROOT, cfg_rel))
+    if world > 1:
+        uid = [raftmc.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        run_check = lambda: model.check_sharded(rank, world, local, uid[0])  # noqa: E731
+    elif args.logical_shards:
+        run_check = lambda: model.check_logical(args.logical_shards)  # noqa: E731
+    else:
+        run_check = model.check
 
     def barrier():
         if dist is not None:
@@ -116,13 +128,13 @@ def main():
     cold = []
     for _ in range(args.warmup):
         t = time.perf_counter()
-        model.check()
+        run_check()
         cold.append(time.perf_counter() - t)
     barrier()
     t0 = time.perf_counter()
     results = []
     for _ in range(args.steps):
-        results.append(model.check())
+        results.append(run_check())
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -131,7 +143,7 @@ def main():
         elapsed = float(t.item())
     res = results[-1]
     per_step = elapsed / args.steps
-    value = world * res["distinct"] / per_step
+    value = res["distinct"] / per_step
     exp_bytes = algorithmic_bytes(res)
     achieved = exp_bytes / (res["expand_ms"] * 1e-3) if res["expand_ms"] > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args.workload)
@@ -145,13 +157,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": per_step * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic: the model constants are the input (no dataset)",
             "config": {"workload": args.workload, "baseline_config": bcfg, "description": desc,
                        "spec": module, "cfg": cfg_rel,
-                       "parallelism": "replicas" if world > 1 else "single"},
+                       "parallelism": ("fp-sharded x%d (RCCL)" % world) if world > 1 else
+                       ("fp-sharded x%d logical shards on 1 GPU" % args.logical_shards if args.logical_shards
+                        else "single")},
             "result": {"generated": res["generated"], "distinct": res["distinct"], "depth": res["depth"],
                        "status": res["status"], "time_to_exhaust_s": per_step,
                        "first_check_s": cold[0] if cold else None},

@@ -48,11 +48,13 @@ void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* ou
 hipError_t upload_model(const Model& m);
 
 // sharded search (rmc_sharded.cpp)
+unsigned long long bucket_blocks(unsigned long long n);
+// blk_counts / blk_off: owner-major [W][bucket_blocks(n)]
 void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_ob, unsigned long long n, int W,
-                        unsigned int* counts, hipStream_t s);
+                        unsigned int* blk_counts, hipStream_t s);
 void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
-                   unsigned long long n, int W, const unsigned int* seg_off, unsigned int* cursor,
-                   unsigned long long* send, uint32_t* perm, hipStream_t s);
+                   unsigned long long n, int W, const unsigned int* blk_off, unsigned long long* send, uint32_t* perm,
+                   hipStream_t s);
 void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
                         unsigned long long mask, unsigned level, unsigned long long* recv_slot, DevStatus* st,
                         hipStream_t s);

@@ -390,22 +390,21 @@ __host__ __device__ __forceinline__ int fp_owner(unsigned long long fp, int W) {
   return (int)(((fp >> 32) * (unsigned long long)W) >> 32);
 }
 
-// Per-owner candidate counts, one atomic per (wave, owner).
+// Bucketing by owner without global atomics: per-block LDS histograms land in
+// an owner-major [W][nblocks] array; its exclusive scan gives every (owner,
+// block) pair its offset in the send buffer (= owner segment + earlier blocks).
+constexpr int BUCKET_MAXW = 64;
 __global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* __restrict__ cand_fp,
                                                      const uint32_t* __restrict__ cand_ob, unsigned long long n, int W,
-                                                     unsigned int* __restrict__ counts) {
+                                                     unsigned int* __restrict__ blk_counts) {
+  __shared__ unsigned int h[BUCKET_MAXW];
+  const unsigned nb = gridDim.x;
+  if (threadIdx.x < W) h[threadIdx.x] = 0;
+  __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int o = -1;
-  if (t < n && !(cand_ob[t] & 0x8000u)) o = fp_owner(cand_fp[t], W);
-  const int lane = lane_id();
-  unsigned long long pending = __ballot(o >= 0);
-  while (pending) {
-    int leader = __ffsll((long long)pending) - 1;
-    int lo = __shfl(o, leader, WAVE);
-    unsigned long long m = __ballot(o == lo);
-    if (lane == leader) atomicAdd(&counts[lo], (unsigned)__popcll(m));
-    pending &= ~m;
-  }
+  if (t < n && !(cand_ob[t] & 0x8000u)) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
+  __syncthreads();
+  if (threadIdx.x < W) blk_counts[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
 // Scatter (fp, val) records into per-owner segments of the send buffer;
@@ -413,34 +412,23 @@ __global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* _
 __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __restrict__ cand_fp,
                                                 const unsigned long long* __restrict__ cand_val,
                                                 const uint32_t* __restrict__ cand_ob, unsigned long long n, int W,
-                                                const unsigned int* __restrict__ seg_off,
-                                                unsigned int* __restrict__ cursor,
+                                                const unsigned int* __restrict__ blk_off,
                                                 unsigned long long* __restrict__ send, uint32_t* __restrict__ perm) {
+  __shared__ unsigned int h[BUCKET_MAXW];
+  const unsigned nb = gridDim.x;
+  if (threadIdx.x < W) h[threadIdx.x] = blk_off[(size_t)threadIdx.x * nb + blockIdx.x];
+  __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int o = -1;
-  unsigned long long fp = 0;
-  if (t < n && !(cand_ob[t] & 0x8000u)) {
-    fp = cand_fp[t];
-    o = fp_owner(fp, W);
+  if (t >= n) return;
+  if (cand_ob[t] & 0x8000u) {
+    perm[t] = 0xFFFFFFFFu;
+    return;
   }
-  const int lane = lane_id();
-  unsigned long long pending = __ballot(o >= 0);
-  while (pending) {
-    int leader = __ffsll((long long)pending) - 1;
-    int lo = __shfl(o, leader, WAVE);
-    unsigned long long m = __ballot(o == lo);
-    unsigned base = 0;
-    if (lane == leader) base = atomicAdd(&cursor[lo], (unsigned)__popcll(m));
-    base = __shfl(base, leader, WAVE);
-    if (o == lo) {
-      unsigned pos = seg_off[lo] + base + (unsigned)__popcll(m & lanemask_lt());
-      send[2ULL * pos] = fp;
-      send[2ULL * pos + 1] = cand_val[t];
-      perm[t] = pos;
-    }
-    pending &= ~m;
-  }
-  if (t < n && o < 0) perm[t] = 0xFFFFFFFFu;
+  unsigned long long fp = cand_fp[t];
+  unsigned pos = atomicAdd(&h[fp_owner(fp, W)], 1u);
+  send[2ULL * pos] = fp;
+  send[2ULL * pos + 1] = cand_val[t];
+  perm[t] = pos;
 }
 
 // Owner side: insert every received (fp, val); first in TLC order wins.
@@ -465,8 +453,13 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
     w = table[2 * recv_slot[j] + 1] == recv[2 * j + 1];
     flag[j] = w ? 1 : 0;
   }
+  __shared__ unsigned int c;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
   unsigned long long m = __ballot(w);
-  if (lane_id() == 0 && m) atomicAdd(newcount, (unsigned long long)__popcll(m));
+  if (lane_id() == 0 && m) atomicAdd(&c, (unsigned)__popcll(m));
+  __syncthreads();
+  if (threadIdx.x == 0 && c) atomicAdd(newcount, (unsigned long long)c);
 }
 
 // Generator side: per parent, winners (flags returned in send order) ranked
@@ -487,17 +480,18 @@ __global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, c
   par_win[p] = cnt;
 }
 
+unsigned long long bucket_blocks(unsigned long long n) { return n ? (n + 255) / 256 : 1; }
 void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_ob, unsigned long long n, int W,
-                        unsigned int* counts, hipStream_t s) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_owner_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cand_fp, cand_ob, n, W, counts);
+                        unsigned int* blk_counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_owner_count, dim3((unsigned)bucket_blocks(n)), dim3(256), 0, s, cand_fp, cand_ob, n, W,
+                     blk_counts);
 }
 void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
-                   unsigned long long n, int W, const unsigned int* seg_off, unsigned int* cursor,
-                   unsigned long long* send, uint32_t* perm, hipStream_t s) {
+                   unsigned long long n, int W, const unsigned int* blk_off, unsigned long long* send, uint32_t* perm,
+                   hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_bucket, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cand_fp, cand_val, cand_ob, n, W,
-                     seg_off, cursor, send, perm);
+  hipLaunchKernelGGL(k_bucket, dim3((unsigned)bucket_blocks(n)), dim3(256), 0, s, cand_fp, cand_val, cand_ob, n, W,
+                     blk_off, send, perm);
 }
 void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
                         unsigned long long mask, unsigned level, unsigned long long* recv_slot, DevStatus* st,

@@ -123,11 +123,11 @@ struct RcclComm : Comm {
 // ---------------------------------------------------------- shard buffers
 struct ShardBufs {
   DevBuf table, table2, fa, fb, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
-  DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, trp, trb, small;
+  DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, trp, trb, small, bcnt, boff, btmp;
   void release() {
     for (DevBuf* b : {&table, &table2, &fa, &fb, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters,
                       &stbuf, &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &trp, &trb,
-                      &small})
+                      &small, &bcnt, &boff, &btmp})
       b->release();
   }
 };
@@ -219,6 +219,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 20);
   const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
   const int NL = (int)comm.local.size();
+  if (W > 64) throw std::runtime_error("at most 64 shards");
 
   std::vector<Shard> sh(NL);
   for (int i = 0; i < NL; i++) {
@@ -365,18 +366,31 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         message = "capacity overflow (sharded search, code " + std::to_string(e) + ")";
         break;
       }
-      // ---- bucket by owner, exchange counts
-      for (Shard& s : sh) {
-        unsigned int* cnt = s.B->small.as<unsigned int>();  // [0,W) counts, [W,2W) offsets, [2W,3W) cursors
-        HIPCHK(hipMemsetAsync(cnt, 0, 3 * W * 4, stream));
-        launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, cnt, stream);
+      // ---- bucket by owner (per-block histograms, owner-major scan), exchange counts
+      std::vector<std::vector<unsigned int>> cnts(NL, std::vector<unsigned int>(W + 1));
+      for (int i = 0; i < NL; i++) {
+        Shard& s = sh[i];
+        const unsigned long long nb = bucket_blocks(s.ncand), nbw = nb * (unsigned long long)W;
+        s.B->bcnt.ensure((nbw + 1) * 4);
+        s.B->boff.ensure((nbw + 1) * 4);
+        size_t tb = scan_temp_bytes(nbw + 1);
+        s.B->btmp.ensure(tb ? tb : 16);
+        unsigned int* bc = s.B->bcnt.as<unsigned int>();
+        HIPCHK(hipMemsetAsync(bc + nbw, 0, 4, stream));
+        launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, bc, stream);
         HIPCHK(hipGetLastError());
+        launch_scan(s.B->btmp.p, s.B->btmp.bytes, bc, s.B->boff.as<unsigned int>(), nbw + 1, stream);
+        HIPCHK(hipGetLastError());
+        // owner segment starts (boff[o*nb]) and the total (boff[nbw])
+        HIPCHK(hipMemcpy2DAsync(cnts[i].data(), 4, s.B->boff.as<unsigned int>(), nb * 4, 4, W, hipMemcpyDeviceToHost,
+                                stream));
+        HIPCHK(hipMemcpyAsync(&cnts[i][W], s.B->boff.as<unsigned int>() + nbw, 4, hipMemcpyDeviceToHost, stream));
       }
-      std::vector<std::vector<unsigned int>> cnts(NL, std::vector<unsigned int>(W));
-      for (int i = 0; i < NL; i++)
-        HIPCHK(hipMemcpyAsync(cnts[i].data(), sh[i].B->small.p, W * 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      for (int i = 0; i < NL; i++) rows[i].assign(cnts[i].begin(), cnts[i].end());
+      for (int i = 0; i < NL; i++) {
+        rows[i].assign(W, 0);
+        for (int d = 0; d < W; d++) rows[i][d] = cnts[i][d + 1] - cnts[i][d];
+      }
       comm.allgather(rows, all, W);  // all[src*W + dst] = records src sends to dst
       for (int i = 0; i < NL; i++) {
         Shard& s = sh[i];
@@ -385,18 +399,14 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         s.rseg_off.assign(W + 1, 0);
         for (int q = 0; q < W; q++) s.rseg_off[q + 1] = s.rseg_off[q] + all[(size_t)q * W + s.id];
         s.nrecv = s.rseg_off[W];
-        std::vector<unsigned int> off(W);
-        for (int d = 0; d < W; d++) off[d] = (unsigned int)s.seg_off[d];
-        unsigned int* dev = s.B->small.as<unsigned int>();
-        HIPCHK(hipMemcpyAsync(dev + W, off.data(), W * 4, hipMemcpyHostToDevice, stream));
         s.B->send.ensure(std::max<size_t>(16, s.seg_off[W] * 16));
         s.B->sflag.ensure(std::max<size_t>(1, s.seg_off[W]));
         s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
         s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
         s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
         launch_bucket(s.B->cfp.as<unsigned long long>(), s.B->cval.as<unsigned long long>(), s.B->cob.as<uint32_t>(),
-                      s.ncand, W, dev + W, dev + 2 * W, s.B->send.as<unsigned long long>(), s.B->perm.as<uint32_t>(),
-                      stream);
+                      s.ncand, W, s.B->boff.as<unsigned int>(), s.B->send.as<unsigned long long>(),
+                      s.B->perm.as<uint32_t>(), stream);
         HIPCHK(hipGetLastError());
       }
       // ---- (fp, key) records to their owners
