@@ -718,17 +718,26 @@ int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, i
       return -4;
     }
     HIPCHK(hipSetDevice(device));
-    hipStream_t s;
-    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    ncclUniqueId u;
-    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
-    int rc;
+    // The communicator (and its stream) is kept for later checks with the same
+    // id, rank and world: repeated checks do not pay ncclCommInitRank again.
+    static std::mutex mu;
+    static std::map<std::string, RcclComm*> cache;
+    std::string key(reinterpret_cast<const char*>(id), NCCL_UNIQUE_ID_BYTES);
+    key += ":" + std::to_string(rank) + ":" + std::to_string(world) + ":" + std::to_string(device);
+    RcclComm* comm = nullptr;
     {
-      RcclComm comm(rank, world, u, s);
-      rc = run_with_regrow(m, o, comm, out);
+      std::lock_guard<std::mutex> lk(mu);
+      RcclComm*& c = cache[key];
+      if (!c) {
+        hipStream_t s;
+        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        ncclUniqueId u;
+        memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+        c = new RcclComm(rank, world, u, s);
+      }
+      comm = c;
     }
-    HIPCHK(hipStreamDestroy(s));
-    return rc;
+    return run_with_regrow(m, o, *comm, out);
   } catch (std::exception& e) {
     set_last_error(e.what());
     return -5;

@@ -33,6 +33,8 @@ SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
 
 
 def main():
+    if "--shipped-one" in sys.argv:
+        return shipped()
     out = {}
     for name, module, kw in SMALL:
         txt = cfg_text(module, **kw)
@@ -65,21 +67,30 @@ def main():
     with open(os.path.join(HERE, "medium.json"), "w") as f:
         json.dump(med, f, indent=1, sort_keys=True)
     if "--shipped" in sys.argv:
-        ship = {}
-        for name, module, path in SHIPPED:
-            with open(os.path.join(ROOT, path)) as fh:
-                txt = fh.read()
-            cfg = parse_cfg(txt)
-            c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=8)
-            ship[name] = dict(module=module, cfg_path=path, generated=c["generated"], distinct=c["distinct"],
-                              depth=c["depth"], status=c["status"], levels=c["levels"],
-                              action_counts=c["action_counts"], max_msgs=c["max_msgs"],
-                              hidden_same_level=c["hidden_same_level"],
-                              hidden_cross_level=c["hidden_cross_level"], pinned_by="coracle",
-                              oracle_seconds=c["seconds"])
-            print(name, c["generated"], c["distinct"], c["depth"], flush=True)
-        with open(os.path.join(HERE, "shipped.json"), "w") as f:
-            json.dump(ship, f, indent=1, sort_keys=True)
+        shipped()
+
+
+def shipped():
+    """--shipped: every shipped cfg; --shipped-one NAME: one, merged into shipped.json."""
+    only = sys.argv[sys.argv.index("--shipped-one") + 1] if "--shipped-one" in sys.argv else None
+    sp = os.path.join(HERE, "shipped.json")
+    ship = json.load(open(sp)) if (only and os.path.exists(sp)) else {}
+    for name, module, path in SHIPPED:
+        if only and name != only:
+            continue
+        with open(os.path.join(ROOT, path)) as fh:
+            txt = fh.read()
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=8)
+        ship[name] = dict(module=module, cfg_path=path, generated=c["generated"], distinct=c["distinct"],
+                          depth=c["depth"], status=c["status"], levels=c["levels"],
+                          action_counts=c["action_counts"], max_msgs=c["max_msgs"],
+                          hidden_same_level=c["hidden_same_level"],
+                          hidden_cross_level=c["hidden_cross_level"], pinned_by="coracle",
+                          oracle_seconds=c["seconds"])
+        print(name, c["generated"], c["distinct"], c["depth"], flush=True)
+    with open(os.path.join(HERE, "shipped.json"), "w") as f:
+        json.dump(ship, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
