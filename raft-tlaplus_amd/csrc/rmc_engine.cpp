@@ -875,6 +875,14 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     std::reverse(binds.begin(), binds.end());
     replay_trace(m, binds, last_b, status, message, res);
   }
+  if (opt->verbose) {
+    unsigned long long stp[8];
+    read_stamps(stp);
+    double tot = (double)(stp[0] + stp[1] + stp[2] + stp[3]);
+    if (tot > 0)
+      fprintf(stderr, "[rmc] k_expand phase shares: stage %.1f%%, H_pi %.1f%%, bindings %.1f%%, fp+insert %.1f%%\n",
+              100 * stp[0] / tot, 100 * stp[1] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot);
+  }
   HIPCHK(hipStreamDestroy(stream));
   if (!opt->hash_slots) m->hint_slots = slots;
   if (!opt->frontier_cap) m->hint_fcap = fcap;

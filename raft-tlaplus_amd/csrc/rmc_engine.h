@@ -63,6 +63,7 @@ void launch_mark_recv(const unsigned long long* recv, const unsigned long long* 
 void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
                      const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s);
 int host_fp_owner(unsigned long long fp, int W);
+void read_stamps(unsigned long long* out);  // -DRMC_STAMPS diagnostic builds
 
 // host-side (rmc_host.cpp): replay + formatting use the same action code
 int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,

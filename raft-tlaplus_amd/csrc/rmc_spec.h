@@ -613,6 +613,9 @@ RMC_HD bool act_sendpull(const PState<SPEC, N>& s, const Model& M, int i, int j,
 template <int SPEC, int N>
 RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
   uint32_t w = s.msg(k);
+  // Fast reject before the full decode: a delivered message (count 0) enables
+  // nothing unless its term is newer than its receiver's (UpdateTerm).
+  if (msg_count(w) == 0 && msg_term<SPEC>(w) <= a_term(s.A(msg_dst<SPEC>(w)))) return false;
   MsgF m = msg_decode<SPEC>(w);
   int i = m.dst, j = m.src;
   uint32_t a = s.A(i), b = s.B(i);
