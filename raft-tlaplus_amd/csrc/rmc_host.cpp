@@ -24,17 +24,7 @@ static int eval_apply_t(const Model& M, const uint32_t* parent, int b, uint32_t*
 template <int SPEC, int N>
 static unsigned long long fp_t(const Model& M, const uint32_t* S) {
   PState<SPEC, N> s{S};
-  unsigned long long best = ~0ULL;
-  for (int p = 0; p < M.nperm; p++) {
-    uint32_t P = M.perm[p];
-    unsigned long long h = 0;
-    for (int i = 0; i < N; i++) h += h_server<SPEC, N>(P, i, s.A(i), s.B(i), s.Cw(i), s.Dw(i));
-    for (int k = 0; k < s.nmsg(); k++) h += h_msg<SPEC>(P, s.msg(k));
-    if (SPEC == PULL) h += h_acked_view(s.hdr());
-    unsigned long long f = mix64(h);
-    if (f < best) best = f;
-  }
-  return best;
+  return state_fp<SPEC, N>(s, M);
 }
 
 template <int SPEC, int N>

@@ -67,43 +67,6 @@ __device__ __forceinline__ unsigned long long table_insert(unsigned long long* T
   return 0;
 }
 
-// Canonical fp of a successor from its parent's per-permutation sums Hp[pi]
-// and the parent's per-permutation server hashes HS[pi*N + i] (k_expand's
-// LDS caches): only the changed server and the changed messages are hashed.
-template <int SPEC, int N>
-__device__ __forceinline__ unsigned long long successor_fp(const PState<SPEC, N>& s, const Delta& d,
-                                                           const unsigned long long* Hp,
-                                                           const unsigned long long* HS, int nperm) {
-  unsigned long long best = EMPTY;
-  unsigned long long aux = 0;
-  if (SPEC == PULL && ((d.hdr ^ s.hdr()) & 0x00FF0000u)) aux = h_acked_view(d.hdr) - h_acked_view(s.hdr());
-  for (int p = 0; p < nperm; p++) {
-    uint32_t P = cM.perm[p];
-    unsigned long long h = Hp[p] + aux;
-    if (d.srv >= 0) {
-      int i = d.srv;
-      h += h_server<SPEC, N>(P, i, d.w[0], d.w[1], d.w[2], d.w[3]);
-      h -= HS ? HS[p * N + i] : h_server<SPEC, N>(P, i, s.A(i), s.B(i), s.Cw(i), s.Dw(i));
-    }
-#pragma unroll
-    for (int q = 0; q < MAXOPS; q++) {
-      if (q >= d.nops) break;
-      h += h_msg<SPEC>(P, d.opc[q]);
-      if (d.opk[q] >= 0) h -= h_msg<SPEC>(P, s.msg(d.opk[q]));
-    }
-    unsigned long long f = mix64(h);
-    best = f < best ? f : best;
-  }
-  return best;
-}
-
-// Cache each parent's per-permutation server hashes in LDS for phase C (costs
-// PB*N!*N*8 B of LDS per block, i.e. occupancy).  Measured slower on MI355X
-// for N=3 (1.42 s vs 1.33 s of k_expand on the bench workload), so off.
-#ifndef RMC_HS_CACHE
-#define RMC_HS_CACHE 0
-#endif
-
 // Diagnostic build only (-DRMC_STAMPS): per-phase block time of k_expand,
 // summed over blocks (thread 0's shader-clock deltas, with an extra barrier
 // between phases A and B).  Read the shares, not the absolute time.
@@ -131,26 +94,20 @@ void read_stamps(unsigned long long* out) {
 #endif
 }
 
-// Parents per expand/materialize tile.  N=5 has 120 permutations, so its
-// per-parent H_pi vectors (960 B each) force a smaller tile.
+// Parents per expand/materialize tile: one per lane of a wave in phase B.
 template <int N>
 struct Tile {
-  static constexpr int PB = N >= 5 ? 16 : 64;
+  static constexpr int PB = 64;
 };
 
 // Dynamic LDS layout of k_expand (bytes, host mirrors it in expand_lds_bytes).
 struct ExpandLds {
-  int Wp, off_H, off_HS, off_En, off_Ord, off_Base, bytes;
+  int Wp, off_En, off_Ord, off_Base, bytes;
 };
-__host__ __device__ inline ExpandLds expand_lds(int PB, int N, int words, int nperm, int enw, int ordw) {
+__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int enw, int ordw) {
   ExpandLds L;
   L.Wp = words | 1;  // odd row stride: lane-per-parent LDS reads are bank-conflict free
   int o = PB * L.Wp * 4;
-  o = (o + 7) & ~7;
-  L.off_H = o;
-  o += PB * nperm * 8;
-  L.off_HS = o;
-  if (RMC_HS_CACHE && N <= 4) o += PB * nperm * N * 8;
   L.off_En = o;
   o += PB * enw * 4;
   L.off_Ord = o;
@@ -180,15 +137,16 @@ __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set 
 }
 
 // One block = one tile of PB consecutive parents, 256 threads.
-//   A: parents -> LDS (coalesced), H_pi(parent) for every (parent, pi) pair.
+//   A: parents -> LDS (coalesced, odd row stride).
 //   B: lane-per-parent binding evaluation.  Within a wave every lane runs the
 //      SAME binding of a different parent, so the fixed-binding actions are
 //      wave-uniform; enabled bindings and their TLC ordinals go to per-parent
 //      LDS bitmasks.
 //   C: lane-per-successor.  The tile's enabled (parent, binding) pairs are
 //      enumerated densely; each lane rebuilds its successor delta, computes
-//      the canonical fingerprint incrementally from H_pi and inserts it.
-//      Candidates are laid out per parent in TLC ordinal order.
+//      the canonical fingerprint of parent+delta (delta_fp: signature-pruned
+//      permutations, rmc_spec.h) and inserts it.  Candidates are laid out per
+//      parent in TLC ordinal order.
 // Occupancy target (waves per SIMD) for k_expand: 8 caps it at 64 VGPRs with
 // no extra scratch for N <= 4, 4% faster than the compiler's 78-VGPR choice
 // on the bench workload (1.289 s vs 1.340 s).
@@ -208,11 +166,9 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG;
   const int tid = threadIdx.x;
-  const int words = cM.words, nperm = cM.nperm, enw = cM.bind_words, ordw = cM.ord_words;
-  const ExpandLds L = expand_lds(PB, N, words, nperm, enw, ordw);
+  const int words = cM.words, enw = cM.bind_words, ordw = cM.ord_words;
+  const ExpandLds L = expand_lds(PB, words, enw, ordw);
   uint32_t* sS = (uint32_t*)lds;
-  unsigned long long* sH = (unsigned long long*)(lds + L.off_H);
-  unsigned long long* sHS = (unsigned long long*)(lds + L.off_HS);
   uint32_t* sEn = (uint32_t*)(lds + L.off_En);
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
   uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
@@ -230,23 +186,6 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
   for (int q = tid; q < PB * (enw + ordw); q += 256) sEn[q] = 0;  // sEn and sOrd are adjacent
   __syncthreads();
   STAMP(0);
-  for (int idx = tid; idx < np * nperm; idx += 256) {
-    int p = idx % np, pi = idx / np;
-    PState<SPEC, N> s{sS + p * L.Wp};
-    uint32_t P = cM.perm[pi];
-    unsigned long long acc = 0;
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      unsigned long long hs = h_server<SPEC, N>(P, i, s.A(i), s.B(i), s.Cw(i), s.Dw(i));
-      if (RMC_HS_CACHE && N <= 4) sHS[(p * nperm + pi) * N + i] = hs;
-      acc += hs;
-    }
-    const int nm = s.nmsg();
-    for (int k = 0; k < nm; k++) acc += h_msg<SPEC>(P, s.msg(k));
-    if (SPEC == PULL) acc += h_acked_view(s.hdr());
-    sH[p * nperm + pi] = acc;
-  }
-  STAMP(1);
   // ---- B: enabled bindings, lane per parent
   {
     const int p = tid % PB, bstride = 256 / PB;
@@ -317,8 +256,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = 0;
     if (!d.err) {
-      unsigned long long fp = successor_fp<SPEC, N>(s, d, sH + p * nperm, (RMC_HS_CACHE && N <= 4) ? sHS + p * nperm * N : nullptr,
-                                                 nperm);
+      unsigned long long fp = delta_fp<SPEC, N>(s, cM, d);
       unsigned long long val = ((unsigned long long)level << 48) | (pg << 10) | (unsigned long long)d.ordinal;
       if (cand_val) {  // sharded search: the fp's owner inserts it (k_insert_recv)
         slot = fp == EMPTY ? EMPTY - 1 : fp;
@@ -580,7 +518,7 @@ struct Launch {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
-    ExpandLds L = expand_lds(PB, N, M.words, M.nperm, M.bind_words, M.ord_words);
+    ExpandLds L = expand_lds(PB, M.words, M.bind_words, M.ord_words);
     hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.level, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);

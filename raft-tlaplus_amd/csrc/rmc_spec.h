@@ -963,4 +963,167 @@ RMC_HD uint64_t h_acked_view(uint32_t hdr) {  // PullRaft's view includes acked 
   return mix64(((uint64_t)(hdr >> 16) & 0xFFu) + 0xE7037ED1A0B428DBULL);
 }
 
+// ------------------------------------------------- canonical fingerprint
+// VIEW + SYMMETRY (Raft.tla:115-116): fp(s) must be a function of the orbit
+// of view(s) under server permutations.  Each server gets a signature that is
+// permutation-EQUIVARIANT (sig of server i in s == sig of server pi(i) in
+// pi(s)): its own scalar fields, its relational fields reduced to invariants
+// (votedFor is Nil / self / other; |votesGranted|, self in votesGranted; the
+// multisets of its nextIndex/matchIndex row entries for j != i, plus its own
+// entry), and the multisets of the messages it sent and received with the
+// server fields masked out.  Let Pi(s) = the permutations that put the
+// servers in signature order (ties: every order within a tie).  Then
+//     fp(s) = min over pi in Pi(s) of mix(H_pi(s))
+// is orbit-invariant (Pi(sigma(s)) = Pi(s) o sigma^-1, so both minimise over
+// the same set of relabelled states), and usually |Pi(s)| = 1 instead of N!.
+// Signatures only prune; a tie just costs more permutations.
+RMC_HD uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+RMC_HD uint32_t row_multiset(uint32_t row, int N, int i) {  // count of each value (0..7) in 4-bit fields, j != i
+  uint32_t m = 0;
+  for (int j = 0; j < N; j++)
+    if (j != i) m += 1u << (4 * ((row >> (3 * j)) & 7u));
+  return m;
+}
+template <int SPEC>
+RMC_HD uint32_t msg_rest(uint32_t w) {  // the message with msource/mdest masked out
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  return w & ~((7u << sp) | (7u << dp));
+}
+template <int SPEC, int N>
+RMC_HD uint32_t server_sig_own(int i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  int v = a_voted(a);
+  uint32_t vcls = v == NILS ? 0u : (v == i ? 1u : 2u);
+  uint32_t votes = (uint32_t)a_votes(a), pend = (uint32_t)a_pending(a);
+  uint32_t x = (a & 0x0003FE3Fu);  // term | state | Len | commitIndex | fsyncIndex
+  x ^= vcls << 6;
+  x ^= ((uint32_t)popc7(votes) << 18) | (((votes >> i) & 1u) << 21) | ((uint32_t)popc7(pend) << 22) |
+       (((pend >> i) & 1u) << 25);
+  uint32_t h = mix32(x + 0x9E3779B9u);
+  h = mix32(h ^ b);
+  h = mix32(h ^ (row_multiset(c, N, i) + 0x85EBCA6Bu * (((c >> (3 * i)) & 7u) + 1u)));
+  h = mix32(h ^ (row_multiset(d, N, i) + 0xC2B2AE35u * (((d >> (3 * i)) & 7u) + 1u)));
+  return h;
+}
+// per-message contributions to the sender's / receiver's signature
+template <int SPEC>
+RMC_HD void msg_sig(uint32_t w, int& src, int& dst, uint32_t& hs, uint32_t& hd) {
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  src = (int)((w >> sp) & 7u);
+  dst = (int)((w >> dp) & 7u);
+  uint32_t r = w & ~((7u << sp) | (7u << dp));
+  hs = mix32(r ^ 0x27d4eb2fU);
+  hd = mix32(r ^ 0x165667b1U);
+}
+
+// The successor parent + delta as seen by the fingerprint, without
+// materializing it (a full state is the view with an empty delta).
+template <int SPEC, int N>
+struct DeltaView {
+  const PState<SPEC, N>& s;
+  const Delta& d;
+  RMC_HD uint32_t sw(int i, int t) const { return i == d.srv ? d.w[t] : s.S[1 + 4 * i + t]; }
+  RMC_HD uint32_t pmsg(int k) const {  // parent message k after in-place ops
+    uint32_t w = s.msg(k);
+#pragma unroll
+    for (int q = 0; q < MAXOPS; q++)
+      if (q < d.nops && d.opk[q] == k) w = d.opc[q];
+    return w;
+  }
+};
+
+template <int SPEC, int N>
+RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V) {
+  const Delta& d = V.d;
+  const int nm = V.s.nmsg();
+  uint32_t sig[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) sig[i] = server_sig_own<SPEC, N>(i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
+  auto add_sig = [&](uint32_t w) {
+    int src, dst;
+    uint32_t hs, hd;
+    msg_sig<SPEC>(w, src, dst, hs, hd);
+#pragma unroll
+    for (int i = 0; i < N; i++) sig[i] += (i == src ? hs : 0u) + (i == dst ? hd : 0u);
+  };
+#pragma unroll 1
+  for (int k = 0; k < nm; k++) add_sig(V.pmsg(k));
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++)  // compile-time q: the Delta arrays stay in registers
+    if (q < d.nops && d.opk[q] < 0) add_sig(d.opc[q]);
+  // rank of each server in signature order; ties -> enumerate
+  uint32_t P0 = 0;
+  bool ties = false;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      r += sig[k] < sig[j];
+      ties |= (k != j && sig[k] == sig[j]);
+    }
+    P0 |= (uint32_t)r << (3 * j);
+  }
+  const uint64_t aux = SPEC == PULL ? h_acked_view(d.hdr) : 0ULL;
+  uint64_t best = ~0ULL;
+  const int np = ties ? M.nperm : 1;
+#if defined(RMC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+  extern __device__ unsigned long long g_stamps[8];
+  atomicAdd(&g_stamps[4], 1ULL);
+  if (ties) atomicAdd(&g_stamps[5], 1ULL);
+#endif
+#pragma unroll 1
+  for (int p = 0; p < np; p++) {
+    uint32_t P = P0;
+    if (ties) {
+      P = M.perm[p];
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int k = 0; k < N; k++)
+          if (sig[j] < sig[k] && perm_of(P, j) > perm_of(P, k)) ok = false;
+      if (!ok) continue;
+#if defined(RMC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+      atomicAdd(&g_stamps[6], 1ULL);
+#endif
+    }
+    uint64_t h = aux;
+#pragma unroll 1
+    for (int i = 0; i < N; i++) h += h_server<SPEC, N>(P, i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
+#pragma unroll 1
+    for (int k = 0; k < nm; k++) h += h_msg<SPEC>(P, V.pmsg(k));
+#pragma unroll
+    for (int q = 0; q < MAXOPS; q++)
+      if (q < d.nops && d.opk[q] < 0) h += h_msg<SPEC>(P, d.opc[q]);
+    uint64_t f = mix64(h);
+    best = f < best ? f : best;
+  }
+  return best == ~0ULL ? best - 1 : best;  // ~0 marks an empty fingerprint-set slot
+}
+
+// Canonical fp of the successor parent + delta.
+template <int SPEC, int N>
+RMC_HD uint64_t delta_fp(const PState<SPEC, N>& s, const Model& M, const Delta& d) {
+  return canon_fp<SPEC, N>(M, DeltaView<SPEC, N>{s, d});
+}
+
+// Canonical fp of a full packed state (the view with an empty delta).
+template <int SPEC, int N>
+RMC_HD uint64_t state_fp(const PState<SPEC, N>& s, const Model& M) {
+  Delta d;
+  d.srv = -1;
+  d.nops = 0;
+  d.hdr = s.hdr();
+  return canon_fp<SPEC, N>(M, DeltaView<SPEC, N>{s, d});
+}
+
 }  // namespace rmc
