@@ -1040,28 +1040,49 @@ struct DeltaView {
   }
 };
 
+// One pass over the view's messages: each message's server-free part
+// (msource/mdest masked, count kept) is hashed once, u = mix64(rest); its low
+// half joins the sender's signature, its high half the receiver's, and u
+// joins the multiset sum S[src][dst] of its (source, destination) pair.  A
+// permutation P then hashes the messages as
+//     sum over ordered pairs (s, d) of mix64(S[s][d] + key(P(s), P(d)))
+// -- a hash of the function "relabelled pair -> multiset of message bodies",
+// i.e. of the relabelled message bag -- costing N(N-1) mixes, not |messages|.
 template <int SPEC, int N>
-RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V) {
+RMC_HD void view_scan(const DeltaView<SPEC, N>& V, uint32_t (&sig)[N], uint64_t (&S)[N][N]) {
   const Delta& d = V.d;
   const int nm = V.s.nmsg();
-  uint32_t sig[N];
 #pragma unroll
-  for (int i = 0; i < N; i++) sig[i] = server_sig_own<SPEC, N>(i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
-  auto add_sig = [&](uint32_t w) {
-    int src, dst;
-    uint32_t hs, hd;
-    msg_sig<SPEC>(w, src, dst, hs, hd);
+  for (int i = 0; i < N; i++) {
+    sig[i] = server_sig_own<SPEC, N>(i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
 #pragma unroll
-    for (int i = 0; i < N; i++) sig[i] += (i == src ? hs : 0u) + (i == dst ? hd : 0u);
+    for (int j = 0; j < N; j++) S[i][j] = 0;
+  }
+  auto add = [&](uint32_t w) {
+    int sp, dp;
+    msg_srcdst_pos<SPEC>(w, sp, dp);
+    const int src = (int)((w >> sp) & 7u), dst = (int)((w >> dp) & 7u);
+    const uint64_t u = mix64((uint64_t)(w & ~((7u << sp) | (7u << dp))) * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      sig[i] += (i == src ? (uint32_t)u : 0u) + (i == dst ? (uint32_t)(u >> 32) : 0u);
+#pragma unroll
+      for (int j = 0; j < N; j++)
+        if (i != j) S[i][j] += (i == src && j == dst) ? u : 0ULL;
+    }
   };
 #pragma unroll 1
-  for (int k = 0; k < nm; k++) add_sig(V.pmsg(k));
+  for (int k = 0; k < nm; k++) add(V.pmsg(k));
 #pragma unroll
   for (int q = 0; q < MAXOPS; q++)  // compile-time q: the Delta arrays stay in registers
-    if (q < d.nops && d.opk[q] < 0) add_sig(d.opc[q]);
-  // rank of each server in signature order; ties -> enumerate
+    if (q < d.nops && d.opk[q] < 0) add(d.opc[q]);
+}
+// The permutation putting servers in signature order (server j -> its rank);
+// ties = some signatures are equal.
+template <int N>
+RMC_HD uint32_t sig_perm(const uint32_t (&sig)[N], bool& ties) {
   uint32_t P0 = 0;
-  bool ties = false;
+  ties = false;
 #pragma unroll
   for (int j = 0; j < N; j++) {
     int r = 0;
@@ -1072,7 +1093,18 @@ RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V) {
     }
     P0 |= (uint32_t)r << (3 * j);
   }
-  const uint64_t aux = SPEC == PULL ? h_acked_view(d.hdr) : 0ULL;
+  return P0;
+}
+
+template <int SPEC, int N>
+RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V, uint32_t* P0_out = nullptr) {
+  uint32_t sig[N];
+  uint64_t S[N][N];
+  view_scan<SPEC, N>(V, sig, S);
+  bool ties;
+  const uint32_t P0 = sig_perm<N>(sig, ties);
+  if (P0_out) *P0_out = ties ? 0xFFFFFFFFu : P0;
+  const uint64_t aux = SPEC == PULL ? h_acked_view(V.d.hdr) : 0ULL;
   uint64_t best = ~0ULL;
   const int np = ties ? M.nperm : 1;
 #if defined(RMC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
@@ -1099,11 +1131,12 @@ RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V) {
     uint64_t h = aux;
 #pragma unroll 1
     for (int i = 0; i < N; i++) h += h_server<SPEC, N>(P, i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
-#pragma unroll 1
-    for (int k = 0; k < nm; k++) h += h_msg<SPEC>(P, V.pmsg(k));
 #pragma unroll
-    for (int q = 0; q < MAXOPS; q++)
-      if (q < d.nops && d.opk[q] < 0) h += h_msg<SPEC>(P, d.opc[q]);
+    for (int i = 0; i < N; i++)
+#pragma unroll
+      for (int j = 0; j < N; j++)
+        if (i != j)
+          h += mix64(S[i][j] + 0x9E3779B97F4A7C15ULL * (uint64_t)(8 * perm_of(P, i) + perm_of(P, j) + 1));
     uint64_t f = mix64(h);
     best = f < best ? f : best;
   }
