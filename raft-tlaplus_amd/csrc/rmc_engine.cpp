@@ -344,8 +344,12 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
 
 void finalize_model(rmc_model* m, uint32_t kmax) {
   Model& M = m->M;
-  M.kmax = (int)kmax;
-  M.words = 1 + 4 * M.N + M.kmax;
+  // rows are a multiple of 4 words (16 B aligned for the kernels' vector
+  // stores); the padding becomes message capacity
+  int words = (1 + 4 * M.N + (int)kmax + 3) & ~3;
+  if (words - 1 - 4 * M.N > 120) words -= 4;
+  M.words = words;
+  M.kmax = words - 1 - 4 * M.N;
   build_actions(M);
 }
 

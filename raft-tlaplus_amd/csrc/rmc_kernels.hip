@@ -303,8 +303,11 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
 // from the LDS-staged parent and its binding, write it to its TLC-order slot
 // of the next frontier, write the trace record, check the cfg's invariants.
 constexpr int MAT_LIST = 1024;
+#ifndef RMC_MAT_WAVES
+#define RMC_MAT_WAVES 1
+#endif
 template <int SPEC, int N>
-__global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+__global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                      unsigned long long pbase, const uint32_t* __restrict__ cand_ob,
                                                      const uint16_t* __restrict__ cand_win,
                                                      const uint32_t* __restrict__ par_off,
@@ -320,6 +323,7 @@ __global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict_
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int words = cM.words, Wp = words | 1;
   uint32_t* sS = (uint32_t*)lds;
+  uint32_t* sInv = sS + PB * Wp;  // per thread: header + server words of its successor (odd stride)
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
   const uint32_t start = par_off[p0];
@@ -370,7 +374,15 @@ __global__ __launch_bounds__(256) void k_materialize(const uint32_t* __restrict_
       const unsigned long long pg = pbase + p0 + p;
       tr_parent[out_base_global + dst] = pg;
       tr_bind[out_base_global + dst] = (uint16_t)b;
-      PState<SPEC, N> ns{o};
+      // invariants read only the header and the server words: check them on
+      // an LDS copy instead of reading the row back from HBM
+      uint32_t* iv = sInv + tid * (1 + 4 * N);
+      iv[0] = d.hdr;
+#pragma unroll
+      for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int t = 0; t < 4; t++) iv[1 + 4 * i + t] = i == d.srv ? d.w[t] : s.S[1 + 4 * i + t];
+      PState<SPEC, N> ns{iv};
       int ierr = 0;
       int bad = check_invariants<SPEC, N>(ns, cM, ierr);
       if (ierr) atomicMin(&st->inv_err_key, order_key(pg, (int)(ob >> 16), b));
@@ -527,7 +539,7 @@ struct Launch {
   static void materialize(const LevelArgs& a, hipStream_t s) {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
-    size_t lds_bytes = (size_t)PB * (a.model->words | 1) * 4;
+    size_t lds_bytes = ((size_t)PB * (a.model->words | 1) + 256 * (1 + 4 * N)) * 4;
     hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(256), lds_bytes, s, a.frontier, a.nparents,
                        a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
                        a.tr_parent, a.tr_bind, a.st);

@@ -810,31 +810,75 @@ RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta&
   return en;
 }
 
-// Apply a delta: out = successor words (M.words), messages re-sorted.
+// Write parent + delta as a packed row of M.words words (a multiple of 4),
+// in order and without reading the output back: the inserted messages (at
+// most MAXOPS) are sorted in registers and merged into the parent's message
+// list (with its in-place count changes); the row leaves through a 4-word
+// register window, 16 B per store on the device.  Rows are 16 B aligned.
 template <int SPEC, int N>
 RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d, uint32_t* out) {
-  const int W0 = 1 + 4 * N;
-  for (int q = 0; q < W0; q++) out[q] = s.S[q];
-  if (d.srv >= 0) for (int t = 0; t < 4; t++) out[1 + 4 * d.srv + t] = d.w[t];
-  int n = s.nmsg();
-  uint32_t* mo = out + W0;
-  for (int k = 0; k < n; k++) mo[k] = s.msg(k);
-  int nn = n;
+  constexpr uint32_t NONE = 0xFFFFFFFFu;  // never a message word (mdest would be 7)
+  uint32_t ins[MAXOPS];
 #pragma unroll
-  for (int q = 0; q < MAXOPS; q++)
-    if (q < d.nops && d.opk[q] >= 0) mo[d.opk[q]] = d.opc[q];
+  for (int q = 0; q < MAXOPS; q++) ins[q] = NONE;
+  int ni = 0;
 #pragma unroll
   for (int q = 0; q < MAXOPS; q++) {
-    if (q >= d.nops || d.opk[q] >= 0) continue;
-    if (nn >= M.kmax) return E_CAP_MSG;
-    uint32_t w = d.opc[q];
-    int p = nn;
-    while (p > 0 && mo[p - 1] > w) { mo[p] = mo[p - 1]; p--; }
-    mo[p] = w;
-    nn++;
+    if (q < d.nops && d.opk[q] < 0) {
+      uint32_t w = d.opc[q];
+#pragma unroll
+      for (int r = 0; r < MAXOPS; r++) {  // insert into the sorted ins[] (NONE-padded)
+        uint32_t lo = ins[r] < w ? ins[r] : w, hi = ins[r] < w ? w : ins[r];
+        ins[r] = lo;
+        w = hi;
+      }
+      ni++;
+    }
   }
-  for (int k = nn; k < M.kmax; k++) mo[k] = 0;
-  out[0] = (d.hdr & ~0xFFu) | (uint32_t)nn;
+  const int n = s.nmsg(), nn = n + ni;
+  if (nn > M.kmax) return E_CAP_MSG;
+  uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+  int cnt = 0;
+  uint32_t* o = out;
+  auto emit = [&](uint32_t w) {
+    b0 = b1;
+    b1 = b2;
+    b2 = b3;
+    b3 = w;
+    if (++cnt == 4) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      *reinterpret_cast<uint4*>(o) = make_uint4(b0, b1, b2, b3);
+#else
+      o[0] = b0; o[1] = b1; o[2] = b2; o[3] = b3;
+#endif
+      o += 4;
+      cnt = 0;
+    }
+  };
+  auto pop_ins = [&]() {
+    uint32_t w = ins[0];
+#pragma unroll
+    for (int r = 0; r + 1 < MAXOPS; r++) ins[r] = ins[r + 1];
+    ins[MAXOPS - 1] = NONE;
+    return w;
+  };
+  emit((d.hdr & ~0xFFu) | (uint32_t)nn);
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int t = 0; t < 4; t++) emit(i == d.srv ? d.w[t] : s.S[1 + 4 * i + t]);
+#pragma unroll 1
+  for (int k = 0; k < n; k++) {
+    uint32_t w = s.msg(k);
+#pragma unroll
+    for (int q = 0; q < MAXOPS; q++)
+      if (q < d.nops && d.opk[q] == k) w = d.opc[q];
+    while (ins[0] < w) emit(pop_ins());
+    emit(w);
+  }
+  while (ins[0] != NONE) emit(pop_ins());
+#pragma unroll 1
+  for (int k = nn; k < M.kmax; k++) emit(0);
   return E_NONE;
 }
 
