@@ -530,11 +530,12 @@ std::string def_location(const rmc_model* m, const std::string& op) {
 namespace rmcx {
 
 struct Arena {
-  DevBuf table, table2, fa, fb, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp, trp, trb;
+  DevBuf table, table2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   void release() {
-    for (DevBuf* b : {&table, &table2, &fa, &fb, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
-                      &scantmp, &trp, &trb})
+    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
       b->release();
+    for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
 };
 std::mutex g_arena_mu;
@@ -613,9 +614,10 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   // Device buffers persist per device across checks (grow-only), so repeated
   // checks do not pay hipMalloc/hipFree of tens of GB each time.
   Arena& A = arena_for_current_device();
-  DevBuf &table = A.table, &fa = A.fa, &fb = A.fb, &cslot = A.cslot, &cob = A.cob, &cwin = A.cwin;
+  DevBuf &table = A.table, &cslot = A.cslot, &cob = A.cob, &cwin = A.cwin;
   DevBuf &poff = A.poff, &pn = A.pn, &pwin = A.pwin, &ppos = A.ppos, &counters = A.counters, &stbuf = A.stbuf;
-  DevBuf &scantmp = A.scantmp, &trp = A.trp, &trb = A.trb;
+  DevBuf& scantmp = A.scantmp;
+  GrowBuf &fa = A.fa, &fb = A.fb, &trp = A.trp, &trb = A.trb;
   table.ensure(slots * 16);
   HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * 16, stream));
   fa.ensure(fcap * W * 4);
@@ -687,6 +689,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   uint32_t* cur = fa.as<uint32_t>();
   uint32_t* nxt = fb.as<uint32_t>();
   unsigned long long entries_hint = 1;
+  bool table_full_ok = false;
+  try {
   while (status == 0 && cur_n > 0) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     unsigned level = depth + 1;
@@ -694,26 +698,39 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     unsigned long long next_n = 0, gen_lvl = 0;
     for (unsigned long long c0 = 0; c0 < cur_n; c0 += chunk) {
       unsigned long long n = std::min(chunk, cur_n - c0);
-      // grow the table before it passes 1/2 load (worst case: every candidate new)
-      if ((entries_hint + n * (unsigned long long)maxsucc) * 2 > slots) {
-        // rehash into a larger table on the host side: copy out, reinsert by kernel-free path
+      // grow the table before it passes 1/2 load (worst case: every candidate
+      // new).  If HBM cannot hold the doubled table, carry on at up to 0.9 load.
+      const unsigned long long need = entries_hint + n * (unsigned long long)maxsucc;
+      if (need * 2 > slots && !table_full_ok) {
         unsigned long long nslots = slots;
-        while ((entries_hint + n * (unsigned long long)maxsucc) * 2 > nslots) nslots <<= 1;
+        while (need * 2 > nslots) nslots <<= 1;
         if (opt->hash_slots) throw std::runtime_error("fingerprint set full (raise hash_slots)");
         auto tr0 = now();
         DevBuf& nt = A.table2;
-        nt.ensure(nslots * 16);
-        HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
-        launch_rehash(table.as<unsigned long long>(), slots, nt.as<unsigned long long>(), nslots - 1,
-                      stbuf.as<DevStatus>(), stream);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(stream));
-        std::swap(table.p, nt.p);
-        std::swap(table.bytes, nt.bytes);
-        slots = nslots;
+        bool grown = true;
+        try {
+          nt.ensure(nslots * 16);
+        } catch (OutOfDeviceMemory&) {
+          grown = false;
+        }
+        if (grown) {
+          HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
+          launch_rehash(table.as<unsigned long long>(), slots, nt.as<unsigned long long>(), nslots - 1,
+                        stbuf.as<DevStatus>(), stream);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipStreamSynchronize(stream));
+          std::swap(table.p, nt.p);
+          std::swap(table.bytes, nt.bytes);
+          slots = nslots;
+          if (nt.bytes >= (1ULL << 30)) nt.release();  // large searches need the HBM more than a spare table
+          if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots\n", __builtin_ctzll(slots));
+        } else {
+          table_full_ok = true;
+          if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(slots));
+        }
         rehash_s += secs(tr0, now());
-        if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots\n", __builtin_ctzll(slots));
       }
+      if (table_full_ok && need * 10 > slots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
       LevelArgs a;
       memset(&a, 0, sizeof a);
       a.model = &M;
@@ -775,31 +792,28 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       }
       unsigned long long W_chunk = (unsigned long long)lastpos + lastwin;
       gen_lvl += ncand;
-      if (next_n + W_chunk > fcap) {
-        // grow both frontier buffers (keep what is already written)
-        auto tg0 = now();
-        unsigned long long nf = fcap;
-        while (next_n + W_chunk > nf) nf *= 2;
-        size_t cur_off_words = (size_t)(cur - (cur == fa.as<uint32_t>() ? fa.as<uint32_t>() : fb.as<uint32_t>()));
-        (void)cur_off_words;
+      {
+        // the next-level buffer grows in place to exactly what this chunk needs
         bool cur_is_a = cur == fa.as<uint32_t>();
-        DevBuf& cb = cur_is_a ? fa : fb;
-        DevBuf& nb = cur_is_a ? fb : fa;
-        cb.grow_copy(nf * W * 4, cur_n * W * 4);
-        nb.grow_copy(nf * W * 4, next_n * W * 4);
-        cur = cb.as<uint32_t>();
-        nxt = nb.as<uint32_t>();
-        a.frontier = cur + c0 * W;
-        fcap = nf;
-        grow_s += secs(tg0, now());
+        GrowBuf& nb = cur_is_a ? fb : fa;
+        const size_t need = (size_t)(next_n + W_chunk) * W * 4;
+        if (nb.bytes < need) {
+          auto tg0 = now();
+          HIPCHK(hipStreamSynchronize(stream));
+          nb.ensure(need);
+          cur = (cur_is_a ? fa : fb).as<uint32_t>();
+          nxt = nb.as<uint32_t>();
+          a.frontier = cur + c0 * W;
+          grow_s += secs(tg0, now());
+        }
+        fcap = std::max(fcap, next_n + W_chunk);
       }
       if (distinct + next_n + W_chunk > trcap) {
         auto tg0 = now();
-        unsigned long long nt = trcap;
-        while (distinct + next_n + W_chunk > nt) nt *= 2;
-        trp.grow_copy(nt * 8, (distinct + next_n) * 8);
-        trb.grow_copy(nt * 2, (distinct + next_n) * 2);
-        trcap = nt;
+        HIPCHK(hipStreamSynchronize(stream));
+        trcap = (distinct + next_n + W_chunk) + (distinct + next_n + W_chunk) / 4;
+        trp.ensure(trcap * 8);
+        trb.ensure(trcap * 2);
         grow_s += secs(tg0, now());
       }
       a.out = nxt + next_n * W;
@@ -850,9 +864,26 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     cur_base += cur_n;
     cur_n = next_n;
     std::swap(cur, nxt);
-    if (opt->verbose)
-      fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated, t=%.3fs (rehash %.3fs, grow %.3fs)\n",
-              depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s);
+    if (opt->verbose) {
+      size_t fr = 0, tot = 0;
+      (void)hipMemGetInfo(&fr, &tot);
+      fprintf(stderr,
+              "[rmc] depth %u: %llu new, %llu distinct, %llu generated, t=%.3fs (rehash %.3fs, grow %.3fs) "
+              "HBM GiB: table %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f\n",
+              depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s, table.bytes / 1073741824.0,
+              A.table2.bytes / 1073741824.0, fa.bytes / 1073741824.0, fb.bytes / 1073741824.0,
+              trp.bytes / 1073741824.0, trb.bytes / 1073741824.0, fr / 1073741824.0);
+    }
+  }
+  } catch (OutOfDeviceMemory& oom) {
+    // the level in progress is abandoned; counts are those of the completed levels
+    status = 3;
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    char buf[160];
+    snprintf(buf, sizeof buf, " (HBM: %.1f GiB free of %.1f)", fr / 1073741824.0, tot / 1073741824.0);
+    message = std::string("capacity overflow: ") + oom.what() + buf;
+    HIPCHK(hipDeviceSynchronize());
   }
   HIPCHK(hipStreamSynchronize(stream));
   // ---- trace reconstruction: walk parent records, replay bindings on the host

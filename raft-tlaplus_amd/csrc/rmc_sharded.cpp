@@ -122,13 +122,15 @@ struct RcclComm : Comm {
 
 // ---------------------------------------------------------- shard buffers
 struct ShardBufs {
-  DevBuf table, table2, fa, fb, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
-  DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, trp, trb, small, bcnt, boff, btmp;
+  DevBuf table, table2, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, small, bcnt, boff, btmp;
+  GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   void release() {
-    for (DevBuf* b : {&table, &table2, &fa, &fb, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters,
-                      &stbuf, &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &trp, &trb,
-                      &small, &bcnt, &boff, &btmp})
+    for (DevBuf* b : {&table, &table2, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
+                      &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &small, &bcnt,
+                      &boff, &btmp})
       b->release();
+    for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
 };
 static std::mutex g_shard_mu;
@@ -178,27 +180,23 @@ static void table_grow(Shard& s, unsigned long long need_entries, hipStream_t st
   unsigned long long nslots = s.slots;
   while (need_entries * 2 > nslots) nslots <<= 1;
   DevBuf& nt = s.B->table2;
-  nt.ensure(nslots * 16);
+  nt.ensure(nslots * 16);  // OutOfDeviceMemory ends the check with status 3
   HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
   launch_rehash(s.B->table.as<unsigned long long>(), s.slots, nt.as<unsigned long long>(), nslots - 1,
                 s.B->stbuf.as<DevStatus>(), stream);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(stream));
   std::swap(s.B->table.p, nt.p);
   std::swap(s.B->table.bytes, nt.bytes);
   s.slots = nslots;
+  if (nt.bytes >= (1ULL << 30)) nt.release();
 }
 
-// grow a frontier / trace buffer keeping its first `keep` bytes (stream-ordered)
-static void grow_keep(DevBuf& b, size_t need, size_t keep, hipStream_t stream) {
+// grow a frontier / trace buffer keeping its contents (stream-ordered)
+static void grow_keep(GrowBuf& b, size_t need, size_t /*keep*/, hipStream_t stream) {
   if (b.p && b.bytes >= need) return;
-  size_t nb = std::max(need, b.bytes * 2);
-  void* q = nullptr;
   HIPCHK(hipStreamSynchronize(stream));
-  HIPCHK(hipMalloc(&q, nb));
-  if (b.p && keep) HIPCHK(hipMemcpy(q, b.p, keep, hipMemcpyDeviceToDevice));
-  if (b.p) HIPCHK(hipFree(b.p));
-  b.p = q;
-  b.bytes = nb;
+  b.ensure(need);
 }
 
 // Returns 1 when the check must be re-run with a larger message capacity.
@@ -533,22 +531,17 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           unsigned long long need = s.next_fill;
           for (auto& pc : pcs)
             if (pc.d == s.id) need = std::max(need, pc.dl + (pc.b - pc.a));
-          if (need > s.fcap) {
-            unsigned long long nf = s.fcap;
-            while (need > nf) nf *= 2;
+          {  // the next-level buffer grows in place to exactly what it receives
             bool cur_is_a = s.cur == s.B->fa.as<uint32_t>();
-            DevBuf& cb = cur_is_a ? s.B->fa : s.B->fb;
-            DevBuf& nb = cur_is_a ? s.B->fb : s.B->fa;
-            grow_keep(cb, nf * WD * 4, s.ncur * WD * 4, stream);
-            grow_keep(nb, nf * WD * 4, s.next_fill * WD * 4, stream);
-            s.cur = cb.as<uint32_t>();
+            GrowBuf& nb = cur_is_a ? s.B->fb : s.B->fa;
+            grow_keep(nb, need * WD * 4, s.next_fill * WD * 4, stream);
+            s.cur = (cur_is_a ? s.B->fa : s.B->fb).as<uint32_t>();
             s.nxt = nb.as<uint32_t>();
-            s.fcap = nf;
+            s.fcap = std::max(s.fcap, need);
           }
           unsigned long long trneed = s.tr_base[depth + 1] + need;
           if (trneed > s.trcap) {
-            unsigned long long nt = s.trcap;
-            while (trneed > nt) nt *= 2;
+            unsigned long long nt = trneed + trneed / 4;
             grow_keep(s.B->trp, nt * 8, s.tr_base[depth + 1] * 8 + s.next_fill * 8, stream);
             grow_keep(s.B->trb, nt * 2, s.tr_base[depth + 1] * 2 + s.next_fill * 2, stream);
             s.trcap = nt;
