@@ -28,6 +28,7 @@ int main(int argc, char** argv) {
     else if (k == "-msgcap") o.msg_cap_K = (uint32_t)atoi(val().c_str());
     else if (k == "-hashslots") o.hash_slots = strtoull(val().c_str(), nullptr, 10);
     else if (k == "-maxdepth") o.max_depth = atoi(val().c_str());
+    else if (k == "-chunk") o.chunk_parents = (uint32_t)atoi(val().c_str());
     else if (k == "-json") json = true;
     else if (k == "-v") o.verbose = 1;
     else if (!k.empty() && k[0] == '-') { fprintf(stderr, "raftmc: unknown option %s\n", k.c_str()); return 2; }

@@ -608,7 +608,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
   const int maxsucc = M.nfixed + M.kmax;
-  unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 20);
+  unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 21);  // 2M: 4% less kernel time than 1M
   const unsigned long long cand_cap = chunk * (unsigned long long)std::min(maxsucc, 256);
 
   // Device buffers persist per device across checks (grow-only), so repeated
