@@ -1071,7 +1071,17 @@ int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t
       o += "\n";
     }
   }
-  if (r->status == 0) o += "Model checking completed. No error has been found.\n";
+  if (r->status == 0) {
+    o += "Model checking completed. No error has been found.\n";
+    // TLC's estimate for 64-bit fingerprints: distinct x (generated - distinct) / 2^64
+    double d = (double)r->distinct, g = (double)r->generated;
+    snprintf(line, sizeof line,
+             "  Estimates of the probability that TLC did not check all reachable states\n"
+             "  because two distinct states had the same fingerprint:\n"
+             "  calculated (optimistic):  val = %.1E\n",
+             d * (g > d ? g - d : 0.0) / 18446744073709551616.0);
+    o += line;
+  }
   snprintf(line, sizeof line, "%llu states generated, %llu distinct states found, %llu states left on queue.\n",
            (unsigned long long)r->generated, (unsigned long long)r->distinct, (unsigned long long)r->left_on_queue);
   o += line;
