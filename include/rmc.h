@@ -96,6 +96,16 @@ int rmc_comm_unique_id(unsigned char* id128);
 int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, int device, const unsigned char* id128,
                       rmc_result* out);
 int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result* out);
+/* TLC's random simulation mode (-simulate): rounds of `walkers` random
+ * behaviours in parallel on the GPU, each from Init for at most `depth` steps
+ * (a uniformly random enabled successor per step), invariants checked on every
+ * state, until `behaviors` behaviours are done, `seconds` pass (0 = no limit)
+ * or a violation / evaluation error is found (its behaviour is then available
+ * through rmc_trace_*).  Results: generated = states generated, distinct =
+ * behaviours generated, depth = longest behaviour in states, status as for
+ * rmc_check.  The same seed gives the same run. */
+int rmc_simulate(rmc_model* m, const rmc_options* o, uint64_t walkers, uint32_t depth, uint64_t seed,
+                 uint64_t behaviors, double seconds, rmc_result* out);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
 int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
 

@@ -14,7 +14,10 @@ int main(int argc, char** argv) {
   rmc_options_default(&o);
   o.deadlock_check = 1;  // TLC default; the reference always passes -deadlock
   std::string tla, cfg;
-  bool json = false;
+  bool json = false, simulate = false;
+  unsigned long long sim_walkers = 1ULL << 20, sim_num = 0, sim_seed = 0;
+  unsigned sim_depth = 100;
+  double sim_seconds = 0;
   for (int a = 1; a < argc; a++) {
     std::string k = argv[a];
     auto val = [&]() -> std::string {
@@ -29,13 +32,20 @@ int main(int argc, char** argv) {
     else if (k == "-hashslots") o.hash_slots = strtoull(val().c_str(), nullptr, 10);
     else if (k == "-maxdepth") o.max_depth = atoi(val().c_str());
     else if (k == "-chunk") o.chunk_parents = (uint32_t)atoi(val().c_str());
+    else if (k == "-simulate") simulate = true;
+    else if (k == "-depth") sim_depth = (unsigned)atoi(val().c_str());
+    else if (k == "-num") sim_num = strtoull(val().c_str(), nullptr, 10);
+    else if (k == "-seed") sim_seed = strtoull(val().c_str(), nullptr, 10);
+    else if (k == "-walkers") sim_walkers = strtoull(val().c_str(), nullptr, 10);
+    else if (k == "-seconds") sim_seconds = atof(val().c_str());
     else if (k == "-json") json = true;
     else if (k == "-v") o.verbose = 1;
     else if (!k.empty() && k[0] == '-') { fprintf(stderr, "raftmc: unknown option %s\n", k.c_str()); return 2; }
     else tla = k;
   }
   if (tla.empty()) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-config M.cfg] [-json] [-v] M.tla\n");
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-config M.cfg] [-json] [-v] M.tla\n"
+                    "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }
   char err[512];
@@ -44,8 +54,34 @@ int main(int argc, char** argv) {
     fprintf(stderr, "raftmc: %s\n", err);
     return 1;
   }
-  printf("raftmc %s: model checking %s\n", rmc_version(), tla.c_str());
   rmc_result r;
+  if (simulate) {
+    printf("raftmc %s: random simulation of %s, seed %llu, %llu walkers, depth %u\n", rmc_version(), tla.c_str(),
+           sim_seed, sim_walkers, sim_depth);
+    int rc = rmc_simulate(m, &o, sim_walkers, sim_depth, sim_seed, sim_num ? sim_num : sim_walkers, sim_seconds, &r);
+    if (rc != 0) {
+      fprintf(stderr, "raftmc: %s\n", rmc_last_error());
+      rmc_model_free(m);
+      return 1;
+    }
+    if (r.status == 1 || r.status == 2) {
+      std::vector<char> buf(1 << 22);
+      rmc_result rr = r;
+      rr.generated = 0;
+      rmc_format_report(m, &rr, buf.data(), buf.size());
+      std::string s(buf.data());
+      size_t cut = s.find(" states generated");
+      if (cut != std::string::npos) s = s.substr(0, s.rfind('\n', cut) + 1);
+      fputs(s.c_str(), stdout);
+    }
+    printf("The number of states generated: %llu\n", (unsigned long long)r.generated);
+    printf("Simulation using seed %llu generated %llu behaviours (longest %u states)\n", sim_seed,
+           (unsigned long long)r.distinct, r.depth);
+    printf("Finished in %.3fs\n", r.seconds);
+    rmc_model_free(m);
+    return r.status == 0 ? 0 : (r.status == 1 ? 12 : 13);
+  }
+  printf("raftmc %s: model checking %s\n", rmc_version(), tla.c_str());
   int rc = rmc_check(m, &o, &r);
   if (rc != 0) {
     fprintf(stderr, "raftmc: %s\n", rmc_last_error());

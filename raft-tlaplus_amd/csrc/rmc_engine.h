@@ -16,6 +16,13 @@ struct DevStatus {
   unsigned pad;
 };
 
+// simulation mode: the first behaviour to stop the run (violation / error)
+struct SimStatus {
+  unsigned stop;  // 0 running, 1 invariant violated, 2 evaluation error in Next, 3 evaluation error in an invariant
+  unsigned steps;  // steps of the stopping behaviour (its last binding is the failing one)
+  unsigned long long walker;
+};
+
 struct LevelArgs {
   const Model* model;
   const uint32_t* frontier;
@@ -64,6 +71,9 @@ void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const
                      const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s);
 int host_fp_owner(unsigned long long fp, int W);
 void read_stamps(unsigned long long* out);  // -DRMC_STAMPS diagnostic builds
+void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long walkers, unsigned depth,
+                     unsigned long long seed, uint16_t* binds, unsigned long long* counters, SimStatus* ss,
+                     DevStatus* st, int words, hipStream_t s);
 
 // host-side (rmc_host.cpp): replay + formatting use the same action code
 int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,

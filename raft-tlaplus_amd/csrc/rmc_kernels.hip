@@ -604,6 +604,92 @@ void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* ou
                  hipStream_t s) {
   (void)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
 }
+
+// ------------------------------------------------ simulation (TLC -simulate)
+// One lane per walker: a random behaviour from Init, up to `depth` steps.  Each
+// step evaluates every Next binding of the current state (all lanes of a wave
+// on the same binding, as in k_expand phase B), picks one enabled successor
+// uniformly at random, writes it, and checks the cfg's invariants on it.  A
+// state with no successor ends the behaviour (-deadlock).  The chosen bindings
+// are recorded so the host can replay a violating behaviour into a trace.
+__device__ __forceinline__ unsigned long long splitmix(unsigned long long& x) {
+  unsigned long long z = (x += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+constexpr int SIM_BLOCK = 64;
+template <int SPEC, int N>
+__global__ __launch_bounds__(SIM_BLOCK) void k_simulate(const uint32_t* __restrict__ init, unsigned long long walkers,
+                                                        unsigned depth, unsigned long long seed, uint16_t* __restrict__ binds,
+                                                        unsigned long long* __restrict__ counters, SimStatus* ss,
+                                                        DevStatus* st) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int words = cM.words, Wp = words | 1;
+  const int tid = threadIdx.x;
+  uint32_t* cur = (uint32_t*)lds + tid * Wp;                             // odd stride: conflict-free
+  uint32_t* nxt = (uint32_t*)lds + SIM_BLOCK * Wp + tid * words;         // 16 B aligned rows for apply_delta
+  const unsigned long long w = (unsigned long long)blockIdx.x * SIM_BLOCK + tid;
+  if (w >= walkers) return;
+  for (int q = 0; q < words; q++) cur[q] = init[q];
+  unsigned long long rng = seed ^ (w * 0xD1B54A32D192ED03ULL);
+  unsigned steps = 0;
+  for (; steps < depth; steps++) {
+    if (ss->stop) break;
+    PState<SPEC, N> s{cur};
+    const int B = cM.nfixed + s.nmsg();
+    int cnt = 0;
+    for (int b = 0; b < B; b++) {
+      Delta d;
+      if (eval_binding<SPEC, N>(s, cM, b, d)) cnt++;
+    }
+    if (!cnt) break;  // no successor: the behaviour ends (-deadlock)
+    int r = (int)(splitmix(rng) % (unsigned long long)cnt);
+    Delta d;
+    int b = 0;
+    for (; b < B; b++)
+      if (eval_binding<SPEC, N>(s, cM, b, d) && r-- == 0) break;
+    binds[w * depth + steps] = (uint16_t)b;
+    if (d.err) {  // an evaluation error in Next (TLC stops with an error)
+      if (atomicCAS(&ss->stop, 0u, 2u) == 0u) { ss->walker = w; ss->steps = steps + 1; }
+      steps++;
+      break;
+    }
+    int e = apply_delta<SPEC, N>(s, cM, d, nxt);
+    if (e) { atomicOr(&st->cap_flags, 1u << e); break; }
+    for (int q = 0; q < words; q++) cur[q] = nxt[q];
+    int ierr = 0;
+    PState<SPEC, N> ns{cur};
+    int bad = check_invariants<SPEC, N>(ns, cM, ierr);
+    if (ierr || bad >= 0) {
+      if (atomicCAS(&ss->stop, 0u, ierr ? 3u : 1u) == 0u) { ss->walker = w; ss->steps = steps + 1; }
+      steps++;
+      break;
+    }
+  }
+  atomicAdd(&counters[0], (unsigned long long)steps);  // states generated by this behaviour (after Init)
+  atomicMax(&counters[1], (unsigned long long)steps);
+}
+template <int SPEC, int N>
+static void launch_sim_t(const uint32_t* init, unsigned long long walkers, unsigned depth, unsigned long long seed,
+                         uint16_t* binds, unsigned long long* counters, SimStatus* ss, DevStatus* st, int words,
+                         hipStream_t s) {
+  size_t lds = (size_t)SIM_BLOCK * ((words | 1) + words) * 4;
+  hipLaunchKernelGGL((k_simulate<SPEC, N>), dim3((unsigned)((walkers + SIM_BLOCK - 1) / SIM_BLOCK)), dim3(SIM_BLOCK),
+                     lds, s, init, walkers, depth, seed, binds, counters, ss, st);
+}
+void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long walkers, unsigned depth,
+                     unsigned long long seed, uint16_t* binds, unsigned long long* counters, SimStatus* ss,
+                     DevStatus* st, int words, hipStream_t s) {
+#define RMC_SIM(SP, NN) \
+  if (spec == SP && N == NN) return launch_sim_t<SP, NN>(init, walkers, depth, seed, binds, counters, ss, st, words, s);
+  RMC_SIM(RAFT, 2) RMC_SIM(RAFT, 3) RMC_SIM(RAFT, 4) RMC_SIM(RAFT, 5)
+  RMC_SIM(FLEX, 2) RMC_SIM(FLEX, 3) RMC_SIM(FLEX, 4) RMC_SIM(FLEX, 5)
+  RMC_SIM(FSYNC, 2) RMC_SIM(FSYNC, 3) RMC_SIM(FSYNC, 4) RMC_SIM(FSYNC, 5)
+  RMC_SIM(PULL, 2) RMC_SIM(PULL, 3) RMC_SIM(PULL, 4) RMC_SIM(PULL, 5)
+#undef RMC_SIM
+}
+
 hipError_t upload_model(const Model& m) { return hipMemcpyToSymbol(HIP_SYMBOL(cM), &m, sizeof(Model)); }
 
 }  // namespace rmc

@@ -48,7 +48,8 @@ class Result(ctypes.Structure):
 EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_check",
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
-           "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical"]
+           "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
+           "rmc_simulate"]
 
 _lib = None
 
@@ -78,6 +79,8 @@ def lib():
     L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                     ctypes.POINTER(Result)]
     L.rmc_check_logical.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(Result)]
+    L.rmc_simulate.argtypes = [P, ctypes.POINTER(Options), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                               ctypes.c_uint64, ctypes.c_double, ctypes.POINTER(Result)]
     L.rmc_selftest_host_bfs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64,
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), c_int]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
@@ -151,6 +154,17 @@ class Model:
         rc = lib().rmc_check_sharded(self._h, ctypes.byref(o), int(rank), int(world), int(device),
                                      bytes(unique_id), ctypes.byref(r))
         return self._result(rc, r)
+
+    def simulate(self, walkers=1 << 16, depth=100, seed=0, behaviors=None, seconds=0.0, **kw):
+        """TLC -simulate on the GPU.  Returns generated (states), behaviors,
+        depth (longest behaviour), status and, on a violation, the trace."""
+        o, r = self._options(**kw), Result()
+        rc = lib().rmc_simulate(self._h, ctypes.byref(o), int(walkers), int(depth), int(seed) & (2**64 - 1),
+                                int(behaviors if behaviors else walkers), float(seconds), ctypes.byref(r))
+        out = self._result(rc, r)
+        out["behaviors"] = out.pop("distinct")
+        out.pop("levels", None)
+        return out
 
     def trace(self):
         L = lib()

@@ -51,3 +51,10 @@ MEDIUM = [
     ("fsync_n3v1e2_unsafe", "RaftFsync", dict(n=3, v=1, E=2, R=1, FollowerFsyncBeforeReply=False)),
     ("raft_n4v1e1", "Raft", dict(n=4, v=1, E=1)),
 ]
+
+# known-unsafe configs (violations reachable): Flexible
+# with quorums of 1 (FlexibleRaft.tla:16-24 lists the valid pairs; these are not)
+UNSAFE = [
+    ("flex_n3v1e2_q1", "FlexibleRaft", dict(n=3, v=1, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=1)),
+    ("flex_n3v2e2_eq1", "FlexibleRaft", dict(n=3, v=2, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=2)),
+]

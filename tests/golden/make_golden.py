@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import MEDIUM, SMALL, cfg_text  # noqa: E402
+from cfgs import MEDIUM, SMALL, UNSAFE, cfg_text  # noqa: E402
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
     ("Raft_cfg", "Raft", "configs/Raft.cfg"),
@@ -32,9 +32,26 @@ SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
 ]
 
 
+def unsafe():
+    """--unsafe: known-unsafe configs, C oracle with the violating trace's length."""
+    out = {}
+    for name, module, kw in UNSAFE:
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=1, extra=["--trace"])
+        out[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], violated=c["violated"], trace_len=len(c.get("trace", [])),
+                         pinned_by="coracle")
+        print(name, c["generated"], c["distinct"], c["depth"], c["status"], c["violated"], flush=True)
+    with open(os.path.join(HERE, "unsafe.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     if "--shipped-one" in sys.argv:
         return shipped()
+    if "--unsafe" in sys.argv:
+        return unsafe()
     out = {}
     for name, module, kw in SMALL:
         txt = cfg_text(module, **kw)

@@ -89,3 +89,18 @@ def test_violation_found_with_trace(name):
     tr = r["trace"]
     assert tr[0][0] == "Initial predicate"
     assert len(tr) == g["trace_len"]
+
+
+UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
+
+
+@pytest.mark.parametrize("name", sorted(UNSAFE))
+def test_unsafe_flexible_violation(name):
+    """Non-intersecting Flexible quorums: same invariant, same depth and a
+    trace of the oracle's length (counts at a violation depend on how much of
+    the level was expanded, so they are not compared)."""
+    g = UNSAFE[name]
+    r = raftmc.check_text(g["module"], g["cfg"])
+    assert r["status"] == "violation" and r["violated"] == g["violated"]
+    assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]
+    assert r["trace"][0][0] == "Initial predicate"

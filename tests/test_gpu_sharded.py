@@ -72,3 +72,16 @@ def test_logical_growth_paths():
     g = SMALL["raft_n3v1e1r1"]
     m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
     same(m.check_logical(3, chunk_parents=33, frontier_cap=16), g)
+
+
+UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
+
+
+@pytest.mark.parametrize("name", sorted(UNSAFE))
+@pytest.mark.parametrize("shards", [2, 3])
+def test_logical_shards_unsafe(name, shards):
+    g = UNSAFE[name]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    r = m.check_logical(shards, chunk_parents=50)
+    assert r["status"] == "violation" and r["violated"] == g["violated"]
+    assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]

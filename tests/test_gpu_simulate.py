@@ -1,0 +1,58 @@
+"""GPU: random simulation (TLC -simulate) through the C ABI.
+
+Simulation is random, so there are no oracle counts to match; what is pinned:
+known-unsafe configs yield the oracle's violated invariant with a behaviour
+that replays from Init through Next (the host replay refuses a disabled
+binding), a safe config yields none, a seed reproduces its run exactly, and
+the counters are consistent (every behaviour contributes 1..depth+1 states).
+"""
+import json
+import os
+
+import pytest
+
+import raftmc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SMALL = json.load(open(os.path.join(HERE, "golden", "small.json")))
+MEDIUM = json.load(open(os.path.join(HERE, "golden", "medium.json")))
+
+pytestmark = pytest.mark.gpu
+
+
+UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
+
+
+@pytest.mark.parametrize("name", sorted(UNSAFE))
+def test_simulation_finds_unsafe_flexible_violation(name):
+    """Non-intersecting Flexible quorums: random behaviours find the oracle's
+    violated invariant; the behaviour replays from Init (at least as long as
+    the BFS-shortest counterexample)."""
+    g = UNSAFE[name]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    r = m.simulate(walkers=1 << 14, depth=60, seed=7, behaviors=1 << 22, seconds=60)
+    assert r["status"] == "violation" and r["violated"] == g["violated"]
+    tr = r["trace"]
+    assert tr[0][0] == "Initial predicate" and len(tr) >= g["trace_len"]
+
+
+@pytest.mark.parametrize("name", ["raft_n3v1e1", "pull_n3v2e1", "flex_n3v1e1", "fsync_n3v1e1"])
+def test_simulation_safe_configs(name):
+    g = SMALL[name]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    depth, behaviors = 50, 1 << 16
+    r = m.simulate(walkers=1 << 14, depth=depth, seed=3, behaviors=behaviors)
+    assert r["status"] == "ok"
+    assert r["behaviors"] == behaviors
+    assert behaviors < r["generated"] <= behaviors * (depth + 1)
+    assert 2 <= r["depth"] <= depth + 1
+
+
+def test_simulation_is_reproducible_per_seed():
+    g = SMALL["raft_n3v1e1r1"]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    a = m.simulate(walkers=4096, depth=40, seed=11, behaviors=20000)
+    b = m.simulate(walkers=4096, depth=40, seed=11, behaviors=20000)
+    c = m.simulate(walkers=4096, depth=40, seed=12, behaviors=20000)
+    assert (a["generated"], a["depth"]) == (b["generated"], b["depth"])
+    assert a["generated"] != c["generated"]

@@ -112,3 +112,17 @@ def test_cfg_quirks():
     assert cfg["constants"]["n1"] == MV("n1")  # n1 = n1 self-assignment
     assert cfg["invariants"] == ["LeaderHasAllAckedValues", "NoLogDivergence"]
     assert cfg["view"] == "view" and cfg["symmetry"] == "symmServers"
+
+
+UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
+
+
+@pytest.mark.parametrize("name", sorted(UNSAFE))
+def test_unsafe_fixtures_pinned_by_both_oracles(name):
+    """Known-unsafe Flexible configs (quorums that do not intersect): the Python
+    oracle reproduces the C oracle's violation exactly -- invariant, depth,
+    trace length and the counts at the first violating state."""
+    g = UNSAFE[name]
+    p = bfs(make_spec(g["module"], parse_cfg(g["cfg"])))
+    assert (p.status, p.violated, p.depth, len(p.trace)) == (g["status"], g["violated"], g["depth"], g["trace_len"])
+    assert (p.generated, p.distinct) == (g["generated"], g["distinct"])
