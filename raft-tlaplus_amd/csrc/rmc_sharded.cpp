@@ -214,7 +214,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   const size_t WD = (size_t)M.words;
   res->state_bytes = (uint32_t)(WD * 4);
   const int maxsucc = M.nfixed + M.kmax;
-  const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 20);
+  const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 21);
   const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
   const int NL = (int)comm.local.size();
   if (W > 64) throw std::runtime_error("at most 64 shards");
