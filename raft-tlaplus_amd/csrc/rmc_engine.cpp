@@ -1138,6 +1138,10 @@ int rmc_selftest_host_bfs(rmc_model* m, uint32_t kmax, uint64_t max_distinct, ui
           int ord = 0, act = 0, err = 0;
           if (host_eval_apply(M, S, b, t.data(), &ord, &act, &err) != 1) continue;
           if (err) { out3[0] = gen; out3[1] = distinct; out3[2] = depth; return -10 - err; }
+          if (host_fp_check(M, S, b, t.data())) {
+            g_last_error = "selftest: incremental fingerprint differs from the materialized state's";
+            return -2;
+          }
           succ.push_back({ord, t});
         }
         std::stable_sort(succ.begin(), succ.end(), [](auto& x, auto& y) { return x.first < y.first; });

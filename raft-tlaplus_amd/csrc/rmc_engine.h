@@ -80,5 +80,6 @@ int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_
                     int* err);
 unsigned long long host_fingerprint(const Model& M, const uint32_t* S);
 int host_check_invariants(const Model& M, const uint32_t* S, int* err);
+int host_fp_check(const Model& M, const uint32_t* parent, int binding, const uint32_t* row);
 
 }  // namespace rmc

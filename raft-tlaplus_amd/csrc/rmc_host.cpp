@@ -27,6 +27,28 @@ static unsigned long long fp_t(const Model& M, const uint32_t* S) {
   return state_fp<SPEC, N>(s, M);
 }
 
+// Test hook: the three ways the fingerprint of a successor is computed agree
+// (delta_fp from parent + delta, delta_fp_sums from the parent's message sums
+// as k_expand does, state_fp of the materialized row).  0 = agree.
+template <int SPEC, int N>
+static int fp_check_t(const Model& M, const uint32_t* parent, int b, const uint32_t* row) {
+  PState<SPEC, N> s{parent};
+  Delta d;
+  if (!eval_binding<SPEC, N>(s, M, b, d) || d.err) return 0;
+  MsgSums<N> ms{};
+  for (int k = 0; k < s.nmsg(); k++) {
+    int src, dst;
+    const uint64_t u = msg_u<SPEC>(s.msg(k), src, dst);
+    ms.sig[src] += (uint32_t)u;
+    ms.sig[dst] += (uint32_t)(u >> 32);
+    if (src != dst) ms.S[MsgSums<N>::pair(src, dst)] += u;
+  }
+  const unsigned long long a = delta_fp<SPEC, N>(s, M, d), c = delta_fp_sums<SPEC, N>(s, M, d, ms);
+  PState<SPEC, N> t{row};
+  const unsigned long long f = state_fp<SPEC, N>(t, M);
+  return (a == f && c == f) ? 0 : 1;
+}
+
 template <int SPEC, int N>
 static int inv_t(const Model& M, const uint32_t* S, int* err) {
   PState<SPEC, N> s{S};
@@ -64,6 +86,10 @@ int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_
 unsigned long long host_fingerprint(const Model& M, const uint32_t* S) {
   RMC_DISPATCH(fp_t, M, S);
   return 0;
+}
+int host_fp_check(const Model& M, const uint32_t* parent, int binding, const uint32_t* row) {
+  RMC_DISPATCH(fp_check_t, M, parent, binding, row);
+  return -1;
 }
 int host_check_invariants(const Model& M, const uint32_t* S, int* err) {
   RMC_DISPATCH(inv_t, M, S, err);

@@ -97,21 +97,26 @@ void read_stamps(unsigned long long* out) {
 // Parents per expand/materialize tile: one per lane of a wave in phase B.
 template <int N>
 struct Tile {
-  static constexpr int PB = 64;
+  static constexpr int PB = 64;  // = one 64-bit parent mask per binding in k_expand
 };
 
 // Dynamic LDS layout of k_expand (bytes, host mirrors it in expand_lds_bytes).
 struct ExpandLds {
-  int Wp, off_En, off_Ord, off_Base, bytes;
+  int Wp, off_Ms, off_Ord, off_EnT, off_BP, off_Base, bytes;
 };
-__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int enw, int ordw) {
+// nbind = max bindings per state (nfixed + kmax).
+__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int nbind, int ordw, int msbytes) {
   ExpandLds L;
   L.Wp = words | 1;  // odd row stride: lane-per-parent LDS reads are bank-conflict free
-  int o = PB * L.Wp * 4;
-  L.off_En = o;
-  o += PB * enw * 4;
-  L.off_Ord = o;
+  int o = (PB * L.Wp * 4 + 7) & ~7;
+  L.off_Ms = o;  // per-parent message sums (MsgSums<N>, 8 B aligned)
+  o += PB * msbytes;
+  L.off_Ord = o;  // per parent: bitmask over TLC ordinals of its enabled bindings
   o += PB * ordw * 4;
+  L.off_EnT = o;  // per binding: 64-bit mask over the tile's parents where it is enabled
+  o += nbind * 8;
+  L.off_BP = o;  // exclusive prefix over bindings of the masks' popcounts
+  o += (nbind + 1) * 4;
   L.off_Base = o;
   o += (PB + 1) * 4;
   L.bytes = o;
@@ -151,7 +156,7 @@ __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set 
 // no extra scratch for N <= 4, 4% faster than the compiler's 78-VGPR choice
 // on the bench workload (1.289 s vs 1.340 s).
 #ifndef RMC_EXPAND_WAVES
-#define RMC_EXPAND_WAVES 8
+#define RMC_EXPAND_WAVES 7
 #endif
 template <int SPEC, int N>
 __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
@@ -166,11 +171,13 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG;
   const int tid = threadIdx.x;
-  const int words = cM.words, enw = cM.bind_words, ordw = cM.ord_words;
-  const ExpandLds L = expand_lds(PB, words, enw, ordw);
+  const int words = cM.words, ordw = cM.ord_words, nbind = cM.nfixed + cM.kmax;
+  const ExpandLds L = expand_lds(PB, words, nbind, ordw, (int)sizeof(MsgSums<N>));
   uint32_t* sS = (uint32_t*)lds;
-  uint32_t* sEn = (uint32_t*)(lds + L.off_En);
+  MsgSums<N>* sMS = (MsgSums<N>*)(lds + L.off_Ms);
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
+  uint32_t* sEnT = (uint32_t*)(lds + L.off_EnT);
+  uint32_t* sBP = (uint32_t*)(lds + L.off_BP);
   uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
@@ -183,7 +190,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     int p = q / words;
     sS[p * L.Wp + (q - p * words)] = src[q];
   }
-  for (int q = tid; q < PB * (enw + ordw); q += 256) sEn[q] = 0;  // sEn and sOrd are adjacent
+  for (int q = tid; q < PB * ordw + 2 * nbind; q += 256) sOrd[q] = 0;  // sOrd and sEnT are adjacent
+  for (int q = tid; q < PB * (int)(sizeof(MsgSums<N>) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
   __syncthreads();
   STAMP(0);
   // ---- B: enabled bindings, lane per parent
@@ -194,6 +202,15 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
       const int nm = s.nmsg();
       const int B = cM.nfixed + nm;
       const unsigned long long pg = pbase + p0 + p;
+      // the parent's message sums (MsgSums): each of its messages hashed once
+      // here instead of once per successor in phase C
+      for (int k = tid / PB; k < nm; k += bstride) {
+        int src, dst;
+        const uint64_t u = msg_u<SPEC>(s.msg(k), src, dst);
+        atomicAdd(&sMS[p].sig[src], (uint32_t)u);
+        atomicAdd(&sMS[p].sig[dst], (uint32_t)(u >> 32));
+        if (src != dst) atomicAdd((unsigned long long*)&sMS[p].S[MsgSums<N>::pair(src, dst)], (unsigned long long)u);
+      }
       for (int b = tid / PB; b < B; b += bstride) {
         Delta d;
         if (!eval_binding<SPEC, N>(s, cM, b, d)) continue;
@@ -206,18 +223,35 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
           for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
           if (nm + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
         }
-        atomicOr(&sEn[p * enw + (b >> 5)], 1u << (b & 31));
+        atomicOr(&sEnT[2 * b + (p >> 5)], 1u << (p & 31));
         atomicOr(&sOrd[p * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
       }
     }
   }
   __syncthreads();
   STAMP(2);
-  // ---- per-parent successor counts -> tile prefix (wave 0), one global reservation per tile
+  // ---- per-parent successor counts -> tile prefix (wave 0), one global reservation per tile;
+  //      per-binding counts -> binding prefix (wave 1)
+  if (tid >= 64 && tid < 128) {
+    const int lane = tid - 64;
+    uint32_t carry = 0;
+    if (lane == 0) sBP[0] = 0;
+    for (int b0 = 0; b0 < nbind; b0 += 64) {
+      const int b = b0 + lane;
+      uint32_t incl = b < nbind ? (uint32_t)(__popc(sEnT[2 * b]) + __popc(sEnT[2 * b + 1])) : 0u;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(incl, o, WAVE);
+        if (lane >= o) incl += y;
+      }
+      if (b < nbind) sBP[b + 1] = carry + incl;
+      carry += __shfl(incl, 63, WAVE);
+    }
+  }
   if (tid < 64) {
     int c = 0;
     if (tid < np)
-      for (int q = 0; q < enw; q++) c += __popc(sEn[tid * enw + q]);
+      for (int q = 0; q < ordw; q++) c += __popc(sOrd[tid * ordw + q]);  // one ordinal per enabled binding
     int incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -240,15 +274,18 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     if (tid == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
     return;
   }
-  // ---- C: fingerprints + inserts, lane per successor
+  // ---- C: fingerprints + inserts, lane per successor.  The tile's enabled
+  //      (parent, binding) pairs are enumerated binding-major, so neighbouring
+  //      lanes run the same binding (the same action, for the fixed ones) of
+  //      different parents instead of diverging over the parent's actions.
   for (int idx = tid; idx < total; idx += 256) {
-    int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
+    int lo = 0, hi = nbind - 1;  // binding b: sBP[b] <= idx < sBP[b+1]
     while (lo < hi) {
       int mid = (lo + hi + 1) >> 1;
-      if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
+      if ((int)sBP[mid] <= idx) lo = mid; else hi = mid - 1;
     }
-    const int p = lo;
-    const int b = select_bit(sEn + p * enw, idx - (int)sBase[p]);
+    const int b = lo;
+    const int p = select_bit(sEnT + 2 * b, idx - (int)sBP[b]);
     PState<SPEC, N> s{sS + p * L.Wp};
     Delta d;
     eval_binding<SPEC, N>(s, cM, b, d);
@@ -256,7 +293,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = 0;
     if (!d.err) {
-      unsigned long long fp = delta_fp<SPEC, N>(s, cM, d);
+      unsigned long long fp = delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
       unsigned long long val = ((unsigned long long)level << 48) | (pg << 10) | (unsigned long long)d.ordinal;
       if (cand_val) {  // sharded search: the fp's owner inserts it (k_insert_recv)
         slot = fp == EMPTY ? EMPTY - 1 : fp;
@@ -530,7 +567,7 @@ struct Launch {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
-    ExpandLds L = expand_lds(PB, M.words, M.bind_words, M.ord_words);
+    ExpandLds L = expand_lds(PB, M.words, M.nfixed + M.kmax, M.ord_words, (int)sizeof(MsgSums<N>));
     hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.level, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);

@@ -1092,6 +1092,36 @@ struct DeltaView {
 //     sum over ordered pairs (s, d) of mix64(S[s][d] + key(P(s), P(d)))
 // -- a hash of the function "relabelled pair -> multiset of message bodies",
 // i.e. of the relabelled message bag -- costing N(N-1) mixes, not |messages|.
+// One message's contribution to the signatures and pair sums (subtracted when
+// `neg`: the sums are additive mod 2^64 / 2^32, so a successor's sums are the
+// parent's with its changed messages swapped out -- see delta_fp_sums).
+template <int SPEC>
+RMC_HD uint64_t msg_u(uint32_t w, int& src, int& dst) {
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  src = (int)((w >> sp) & 7u);
+  dst = (int)((w >> dp) & 7u);
+  return mix64((uint64_t)(w & ~((7u << sp) | (7u << dp))) * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
+}
+template <int SPEC, int N>
+RMC_HD void msg_contrib(uint32_t w, bool neg, uint32_t (&sig)[N], uint64_t (&S)[N][N]) {
+  int src, dst;
+  uint64_t u = msg_u<SPEC>(w, src, dst);
+  uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+  if (neg) {
+    u = 0ULL - u;
+    lo = 0u - lo;
+    hi = 0u - hi;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    sig[i] += (i == src ? lo : 0u) + (i == dst ? hi : 0u);
+#pragma unroll
+    for (int j = 0; j < N; j++)
+      if (i != j) S[i][j] += (i == src && j == dst) ? u : 0ULL;
+  }
+}
+
 template <int SPEC, int N>
 RMC_HD void view_scan(const DeltaView<SPEC, N>& V, uint32_t (&sig)[N], uint64_t (&S)[N][N]) {
   const Delta& d = V.d;
@@ -1102,19 +1132,7 @@ RMC_HD void view_scan(const DeltaView<SPEC, N>& V, uint32_t (&sig)[N], uint64_t 
 #pragma unroll
     for (int j = 0; j < N; j++) S[i][j] = 0;
   }
-  auto add = [&](uint32_t w) {
-    int sp, dp;
-    msg_srcdst_pos<SPEC>(w, sp, dp);
-    const int src = (int)((w >> sp) & 7u), dst = (int)((w >> dp) & 7u);
-    const uint64_t u = mix64((uint64_t)(w & ~((7u << sp) | (7u << dp))) * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      sig[i] += (i == src ? (uint32_t)u : 0u) + (i == dst ? (uint32_t)(u >> 32) : 0u);
-#pragma unroll
-      for (int j = 0; j < N; j++)
-        if (i != j) S[i][j] += (i == src && j == dst) ? u : 0ULL;
-    }
-  };
+  auto add = [&](uint32_t w) { msg_contrib<SPEC, N>(w, false, sig, S); };
 #pragma unroll 1
   for (int k = 0; k < nm; k++) add(V.pmsg(k));
 #pragma unroll
@@ -1141,10 +1159,8 @@ RMC_HD uint32_t sig_perm(const uint32_t (&sig)[N], bool& ties) {
 }
 
 template <int SPEC, int N>
-RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V, uint32_t* P0_out = nullptr) {
-  uint32_t sig[N];
-  uint64_t S[N][N];
-  view_scan<SPEC, N>(V, sig, S);
+RMC_HD uint64_t canon_from_sums(const Model& M, const DeltaView<SPEC, N>& V, const uint32_t (&sig)[N],
+                                const uint64_t (&S)[N][N], uint32_t* P0_out = nullptr) {
   bool ties;
   const uint32_t P0 = sig_perm<N>(sig, ties);
   if (P0_out) *P0_out = ties ? 0xFFFFFFFFu : P0;
@@ -1185,6 +1201,55 @@ RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V, uint32_t* 
     best = f < best ? f : best;
   }
   return best == ~0ULL ? best - 1 : best;  // ~0 marks an empty fingerprint-set slot
+}
+template <int SPEC, int N>
+RMC_HD uint64_t canon_fp(const Model& M, const DeltaView<SPEC, N>& V, uint32_t* P0_out = nullptr) {
+  uint32_t sig[N];
+  uint64_t S[N][N];
+  view_scan<SPEC, N>(V, sig, S);
+  return canon_from_sums<SPEC, N>(M, V, sig, S, P0_out);
+}
+
+// The parent's message sums (what view_scan accumulates over the parent's
+// messages alone): sig_m[i] = message part of server i's signature, S[i][j].
+// k_expand computes them once per parent (LDS); each successor then costs
+// O(|delta ops|) message hashes instead of O(|DOMAIN messages|).
+template <int N>
+struct MsgSums {
+  uint64_t S[N * (N - 1)];  // ordered pairs i != j, row-major without the diagonal
+  uint32_t sig[N];
+  RMC_HD static int pair(int i, int j) { return i * (N - 1) + (j < i ? j : j - 1); }
+};
+// Canonical fp of parent + delta from the parent's message sums.  Equal to
+// delta_fp bit for bit: the in-place ops swap a parent message's contribution
+// for the new word's (the last op on a slot wins, as in DeltaView::pmsg), the
+// inserts add theirs.
+template <int SPEC, int N>
+RMC_HD uint64_t delta_fp_sums(const PState<SPEC, N>& s, const Model& M, const Delta& d, const MsgSums<N>& ms) {
+  const DeltaView<SPEC, N> V{s, d};
+  uint32_t sig[N];
+  uint64_t S[N][N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    sig[i] = server_sig_own<SPEC, N>(i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3)) + ms.sig[i];
+#pragma unroll
+    for (int j = 0; j < N; j++) S[i][j] = i == j ? 0ULL : ms.S[MsgSums<N>::pair(i, j)];
+  }
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++) {
+    if (q >= d.nops) continue;
+    const int k = d.opk[q];
+    if (k >= 0) {
+      bool last = true;
+#pragma unroll
+      for (int r = q + 1; r < MAXOPS; r++)
+        if (r < d.nops && d.opk[r] == k) last = false;
+      if (!last) continue;
+      msg_contrib<SPEC, N>(s.msg(k), true, sig, S);
+    }
+    msg_contrib<SPEC, N>(d.opc[q], false, sig, S);
+  }
+  return canon_from_sums<SPEC, N>(M, V, sig, S);
 }
 
 // Canonical fp of the successor parent + delta.
