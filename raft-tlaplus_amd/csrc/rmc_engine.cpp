@@ -915,9 +915,10 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     read_stamps(stp);
     double tot = (double)(stp[0] + stp[2] + stp[3]);
     if (tot > 0)
-      fprintf(stderr, "[rmc] k_expand phase shares: stage %.1f%%, bindings %.1f%%, fp+insert %.1f%%; "
+      fprintf(stderr, "[rmc] k_expand phase shares: stage %.1f%%, bindings %.1f%%, fp+insert %.1f%% "
+              "(the same without inserts: %.1f%%); "
               "fingerprints %llu, with signature ties %llu, permutations hashed under ties %llu\n",
-              100 * stp[0] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot, stp[4], stp[5], stp[6]);
+              100 * stp[0] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot, 100 * stp[7] / tot, stp[4], stp[5], stp[6]);
   }
   HIPCHK(hipStreamDestroy(stream));
   if (!opt->hash_slots) m->hint_slots = slots;
