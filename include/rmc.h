@@ -77,6 +77,16 @@ int rmc_check(rmc_model* m, const rmc_options* o, rmc_result* out); /* blocking 
 int rmc_trace_len(const rmc_model* m);                               /* after status 1/2 */
 int rmc_trace_state(const rmc_model* m, int k, char* tla_text, size_t len); /* TLC value syntax */
 int rmc_trace_action(const rmc_model* m, int k, char* text, size_t len);   /* "Initial predicate" / action label */
+/* TLC's -dumpTrace, after status 1/2.  rmc_trace_module writes a TLA+ module
+ * `name` that EXTENDS the checked spec, holds the error behaviour as
+ * TraceStates == << [var |-> value, ...], ... >> and replays it with the spec's
+ * own Init/Next (TraceInit/TraceNext), plus its companion cfg (the model's
+ * constants, INVARIANT TraceAccepted): TLC on the pair must report
+ * "Invariant TraceAccepted is violated" (the whole trace is a behaviour).
+ * rmc_trace_json writes the same behaviour as JSON.  Return the text length
+ * (the buffers get a truncated, NUL-terminated copy), or -1. */
+int rmc_trace_module(const rmc_model* m, const char* name, char* tla, size_t tla_len, char* cfg, size_t cfg_len);
+int rmc_trace_json(const rmc_model* m, char* buf, size_t len);
 /* Print the TLC-format report for a finished check into buf. */
 int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t len);
 void rmc_model_free(rmc_model* m);

@@ -9,12 +9,43 @@
 #include <vector>
 #include "../../include/rmc.h"
 
+// -dumpTrace tla FILE: FILE (module named after its basename) + the companion
+// cfg beside it; -dumpTrace json FILE: the behaviour as JSON.
+static int dump_trace(rmc_model* m, const std::string& fmt, const std::string& file) {
+  if (rmc_trace_len(m) <= 0) return 0;
+  std::vector<char> a(1 << 24), c(1 << 16);
+  std::string path = file, cfgpath;
+  if (fmt == "tla") {
+    if (path.size() < 4 || path.compare(path.size() - 4, 4, ".tla") != 0) path += ".tla";
+    std::string base = path.substr(0, path.size() - 4);
+    size_t sl = base.find_last_of('/');
+    std::string name = sl == std::string::npos ? base : base.substr(sl + 1);
+    if (rmc_trace_module(m, name.c_str(), a.data(), a.size(), c.data(), c.size()) < 0) return 1;
+    cfgpath = base + ".cfg";
+  } else if (rmc_trace_json(m, a.data(), a.size()) < 0) {
+    return 1;
+  }
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) { fprintf(stderr, "raftmc: cannot write %s\n", path.c_str()); return 1; }
+  fputs(a.data(), f);
+  fclose(f);
+  if (!cfgpath.empty()) {
+    FILE* g = fopen(cfgpath.c_str(), "w");
+    if (!g) { fprintf(stderr, "raftmc: cannot write %s\n", cfgpath.c_str()); return 1; }
+    fputs(c.data(), g);
+    fclose(g);
+  }
+  printf("The error trace was written to %s%s%s\n", path.c_str(), cfgpath.empty() ? "" : " and ", cfgpath.c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   rmc_options o;
   rmc_options_default(&o);
   o.deadlock_check = 1;  // TLC default; the reference always passes -deadlock
   std::string tla, cfg;
   bool json = false, simulate = false;
+  std::string dump_fmt, dump_file;
   unsigned long long sim_walkers = 1ULL << 20, sim_num = 0, sim_seed = 0;
   unsigned sim_depth = 100;
   double sim_seconds = 0;
@@ -39,12 +70,17 @@ int main(int argc, char** argv) {
     else if (k == "-walkers") sim_walkers = strtoull(val().c_str(), nullptr, 10);
     else if (k == "-seconds") sim_seconds = atof(val().c_str());
     else if (k == "-json") json = true;
+    else if (k == "-dumpTrace") {
+      dump_fmt = val();
+      dump_file = val();
+      if (dump_fmt != "tla" && dump_fmt != "json") { fprintf(stderr, "raftmc: -dumpTrace tla|json FILE\n"); return 2; }
+    }
     else if (k == "-v") o.verbose = 1;
     else if (!k.empty() && k[0] == '-') { fprintf(stderr, "raftmc: unknown option %s\n", k.c_str()); return 2; }
     else tla = k;
   }
   if (tla.empty()) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-config M.cfg] [-json] [-v] M.tla\n"
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }
@@ -73,6 +109,7 @@ int main(int argc, char** argv) {
       size_t cut = s.find(" states generated");
       if (cut != std::string::npos) s = s.substr(0, s.rfind('\n', cut) + 1);
       fputs(s.c_str(), stdout);
+      if (!dump_fmt.empty()) dump_trace(m, dump_fmt, dump_file);
     }
     printf("The number of states generated: %llu\n", (unsigned long long)r.generated);
     printf("Simulation using seed %llu generated %llu behaviours (longest %u states)\n", sim_seed,
@@ -92,6 +129,7 @@ int main(int argc, char** argv) {
   std::vector<char> buf(1 << 22);
   rmc_format_report(m, &r, buf.data(), buf.size());
   fputs(buf.data(), stdout);
+  if (!dump_fmt.empty() && (r.status == 1 || r.status == 2)) dump_trace(m, dump_fmt, dump_file);
   printf("Finished in %.3fs\n", r.seconds);
   if (json)
     printf("{\"generated\":%llu,\"distinct\":%llu,\"depth\":%u,\"left\":%llu,\"status\":%d,\"violated\":\"%s\","

@@ -280,6 +280,22 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     if (S.kind != CfgVal::SET || Vv.kind != CfgVal::SET) throw std::runtime_error("Server and Value must be sets");
     m->server_names = S.set;
     m->value_names = Vv.set;
+    for (auto& kv : c.consts) {
+      const CfgVal& v = kv.second;
+      std::string t;
+      switch (v.kind) {
+        case CfgVal::INT: t = std::to_string(v.i); break;
+        case CfgVal::BOOL: t = v.b ? "TRUE" : "FALSE"; break;
+        case CfgVal::SET:
+          t = "{";
+          for (size_t q = 0; q < v.set.size(); q++) t += (q ? ", " : "") + v.set[q];
+          t += "}";
+          break;
+        case CfgVal::OP: t = "<- " + v.s; break;
+        default: t = v.s; break;
+      }
+      m->cfg_consts.push_back({kv.first, t});
+    }
     std::sort(m->server_names.begin(), m->server_names.end());  // TLC orders model values by name
     std::sort(m->value_names.begin(), m->value_names.end());
     M.N = (int)S.set.size();
@@ -373,7 +389,7 @@ std::vector<uint32_t> init_state(const Model& M) {
 }
 
 // ------------------------------------------------------------ formatting
-std::string fmt_state(const rmc_model* m, const uint32_t* S) {
+std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, const uint32_t* S) {
   const Model& M = m->M;
   auto sv = [&](int i) { return i == NILS ? std::string("Nil") : m->server_names.at(i); };
   auto fn = [&](auto val) {
@@ -384,7 +400,7 @@ std::string fmt_state(const rmc_model* m, const uint32_t* S) {
   auto entry = [&](int t, int v) {
     return "[term |-> " + std::to_string(t) + ", value |-> " + m->value_names.at(v) + "]";
   };
-  std::string o;
+  std::vector<std::pair<std::string, std::string>> o;
   int nm = h_nmsg(S[0]);
   for (auto& var : m->var_order) {
     std::string val;
@@ -488,8 +504,14 @@ std::string fmt_state(const rmc_model* m, const uint32_t* S) {
         }
         return o2 + ")";
       });
-    o += "/\\ " + var + " = " + val + "\n";
+    o.push_back({var, val});
   }
+  return o;
+}
+
+std::string fmt_state(const rmc_model* m, const uint32_t* S) {
+  std::string o;
+  for (auto& kv : state_vars(m, S)) o += "/\\ " + kv.first + " = " + kv.second + "\n";
   return o;
 }
 
@@ -1031,6 +1053,86 @@ int rmc_trace_state(const rmc_model* m, int k, char* buf, size_t len) {
   return (int)s.size();
 }
 
+// Trace-validation module (TLC's -dumpTrace tla): the error behaviour as a
+// sequence of records, replayed by the spec's own Next.  TLC run on it with
+// the companion cfg must report "Invariant TraceAccepted is violated" -- the
+// last trace state was reached, i.e. every step of the trace is a Next step
+// from Init (Raft.tla:213, :527).  Variables in TLC's order (var_order).
+int rmc_trace_module(const rmc_model* m, const char* name, char* tla, size_t tla_len, char* cfg, size_t cfg_len) {
+  if (!m || !name || m->trace_states.empty()) return -1;
+  const std::string nm = name;
+  std::string o;
+  o += "---------------------------- MODULE " + nm + " ----------------------------\n";
+  o += "(* Written by " + std::string(rmc_version()) + ": the behaviour of " + m->module +
+       " that ends in the reported error\n";
+  o += "   (" + std::to_string(m->trace_states.size()) + " states), replayed by " + m->module +
+       "'s own Init and Next.  Check it with\n";
+  o += "       java tlc2.TLC -deadlock -config " + nm + ".cfg " + nm + ".tla\n";
+  o += "   Expected: \"Error: Invariant TraceAccepted is violated.\" -- the whole trace was\n";
+  o += "   replayed.  Any other outcome means the trace is not a behaviour of the spec. *)\n";
+  o += "EXTENDS " + m->module + ", Sequences, TLC\n\n";
+  o += "CONSTANTS ";
+  {
+    std::vector<std::string> mv = m->server_names;
+    mv.insert(mv.end(), m->value_names.begin(), m->value_names.end());
+    for (size_t q = 0; q < mv.size(); q++) o += (q ? ", " : "") + mv[q];
+  }
+  o += "\n\nVARIABLE traceIdx\n\n";
+  o += "TraceStates == <<\n";
+  for (size_t k = 0; k < m->trace_states.size(); k++) {
+    auto vars = state_vars(m, m->trace_states[k].data());
+    o += "  \\* State " + std::to_string(k + 1) + ": " +
+         (k == 0 ? std::string("<Initial predicate>") : m->trace_actions[k]) + "\n  [";
+    for (size_t q = 0; q < vars.size(); q++) o += (q ? ",\n   " : "") + vars[q].first + " |-> " + vars[q].second;
+    o += k + 1 < m->trace_states.size() ? "],\n" : "]\n";
+  }
+  o += ">>\n\n";
+  auto is = [&](const char* idx, bool primed) {
+    std::string r;
+    for (size_t q = 0; q < m->var_order.size(); q++)
+      r += std::string("    /\\ ") + m->var_order[q] + (primed ? "'" : "") + " = TraceStates[" + idx + "]." +
+           m->var_order[q] + "\n";
+    return r;
+  };
+  o += "TraceInit ==\n    /\\ traceIdx = 1\n" + is("1", false) + "    /\\ Init\n\n";
+  o += "TraceNext ==\n    /\\ traceIdx < Len(TraceStates)\n    /\\ traceIdx' = traceIdx + 1\n    /\\ Next\n" +
+       is("traceIdx + 1", true) + "\n";
+  o += "TraceAccepted == traceIdx < Len(TraceStates)\n";
+  o += "=============================================================================\n";
+  std::string c;
+  c += "\\* Companion cfg of " + nm + ".tla (raftmc -dumpTrace tla): " + m->module + "'s constants.\n";
+  c += "CONSTANTS\n";
+  for (auto& kv : m->cfg_consts)
+    c += "    " + kv.first + (kv.second.rfind("<-", 0) == 0 ? " " : " = ") + kv.second + "\n";
+  c += "INIT TraceInit\nNEXT TraceNext\nINVARIANT TraceAccepted\n";
+  if (tla && tla_len) snprintf(tla, tla_len, "%s", o.c_str());
+  if (cfg && cfg_len) snprintf(cfg, cfg_len, "%s", c.c_str());
+  return (int)o.size();
+}
+
+// The same behaviour as JSON (TLC's -dumpTrace json): {"module", "states": [{"action", var: TLA+ value text}]}.
+int rmc_trace_json(const rmc_model* m, char* buf, size_t len) {
+  if (!m || m->trace_states.empty()) return -1;
+  auto esc = [](const std::string& x) {
+    std::string r;
+    for (char ch : x) {
+      if (ch == '"' || ch == '\\') { r += '\\'; r += ch; }
+      else if (ch == '\n') r += "\\n";
+      else r += ch;
+    }
+    return r;
+  };
+  std::string o = "{\"module\": \"" + esc(m->module) + "\", \"states\": [\n";
+  for (size_t k = 0; k < m->trace_states.size(); k++) {
+    o += "  {\"action\": \"" + esc(k == 0 ? std::string("Initial predicate") : m->trace_actions[k]) + "\"";
+    for (auto& kv : state_vars(m, m->trace_states[k].data())) o += ", \"" + kv.first + "\": \"" + esc(kv.second) + "\"";
+    o += k + 1 < m->trace_states.size() ? "},\n" : "}\n";
+  }
+  o += "]}\n";
+  if (buf && len) snprintf(buf, len, "%s", o.c_str());
+  return (int)o.size();
+}
+
 int rmc_trace_action(const rmc_model* m, int k, char* buf, size_t len) {
   if (!m || k < 0 || k >= (int)m->trace_actions.size()) return -1;
   const std::string& s = m->trace_actions[k];
@@ -1103,6 +1205,43 @@ void rmc_release_device_memory(void) {
     if (hipSetDevice(kv.first) == hipSuccess) kv.second->release();
   }
   (void)hipSetDevice(cur);
+}
+
+// Test hook only (never called by rmc_check): a seeded random walk of at most
+// `steps` steps over the lowered actions on the host, replayed into the
+// model's trace (as after a violation), so the CPU tests can check the trace
+// writers (rmc_trace_module / rmc_trace_json) against the oracle's Next.
+int rmc_selftest_random_trace(rmc_model* m, uint64_t seed, int steps) {
+  try {
+    finalize_model(m, m->kmax_user ? m->kmax_user : default_kmax(m->M));
+    const Model& M = m->M;
+    std::vector<uint32_t> s = init_state(M), t(M.words, 0u);
+    std::vector<int> binds;
+    uint64_t x = seed * 0x9E3779B97F4A7C15ULL + 1;
+    for (int k = 0; k < steps; k++) {
+      std::vector<int> en;
+      for (int b = 0; b < M.nfixed + h_nmsg(s[0]); b++) {
+        int err = 0;
+        if (host_eval_apply(M, s.data(), b, t.data(), nullptr, nullptr, &err) == 1 && !err) en.push_back(b);
+      }
+      if (en.empty()) break;
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      int b = en[x % en.size()];
+      host_eval_apply(M, s.data(), b, t.data(), nullptr, nullptr, nullptr);
+      s = t;
+      binds.push_back(b);
+    }
+    m->trace_states.clear();
+    m->trace_actions.clear();
+    rmc_result res;
+    memset(&res, 0, sizeof res);
+    std::string msg;
+    replay_trace(m, binds, -1, 0, msg, &res);
+    return (int)m->trace_states.size();
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  }
 }
 
 // Test hook only (never called by rmc_check): sequential host BFS over the same

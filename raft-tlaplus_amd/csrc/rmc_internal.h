@@ -26,6 +26,7 @@ struct rmc_model {
   int fp_aux = 0;  // reserved: no VIEW -> aux vars would join the fingerprint
   std::vector<std::string> server_names, value_names, inv_names;
   std::vector<std::string> var_order;
+  std::vector<std::pair<std::string, std::string>> cfg_consts;  // cfg CONSTANTS, as written back by the trace module
   // results of the last check
   std::vector<std::pair<unsigned long long, unsigned long long>> levels;
   std::vector<std::vector<uint32_t>> trace_states;

@@ -363,7 +363,10 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
 // into an LDS list and processed lane-per-winner: regenerate the successor
 // from the LDS-staged parent and its binding, write it to its TLC-order slot
 // of the next frontier, write the trace record, check the cfg's invariants.
-constexpr int MAT_LIST = 1024;
+#ifndef RMC_MAT_LIST
+#define RMC_MAT_LIST 1024
+#endif
+constexpr int MAT_LIST = RMC_MAT_LIST;
 #ifndef RMC_MAT_WAVES
 #define RMC_MAT_WAVES 1
 #endif

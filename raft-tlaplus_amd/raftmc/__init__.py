@@ -49,7 +49,7 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
-           "rmc_simulate"]
+           "rmc_simulate", "rmc_trace_module", "rmc_trace_json"]
 
 _lib = None
 
@@ -83,6 +83,9 @@ def lib():
                                ctypes.c_uint64, ctypes.c_double, ctypes.POINTER(Result)]
     L.rmc_selftest_host_bfs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64,
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), c_int]
+    L.rmc_trace_module.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t]
+    L.rmc_trace_json.argtypes = [P, ctypes.c_char_p, c_size_t]
+    L.rmc_selftest_random_trace.argtypes = [P, ctypes.c_uint64, c_int]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
     _lib = L
     return L
@@ -177,6 +180,35 @@ class Model:
             L.rmc_trace_state(self._h, k, buf, len(buf))
             tr.append((act, buf.value.decode()))
         return tr
+
+    def trace_module(self, name):
+        """TLC -dumpTrace tla: (module text, cfg text) replaying the error trace with the spec's Next."""
+        L = lib()
+        n = L.rmc_trace_module(self._h, name.encode(), None, 0, None, 0)
+        if n < 0:
+            raise RaftmcError("no trace to dump")
+        tla = ctypes.create_string_buffer(n + 1)
+        cfg = ctypes.create_string_buffer(1 << 16)
+        L.rmc_trace_module(self._h, name.encode(), tla, len(tla), cfg, len(cfg))
+        return tla.value.decode(), cfg.value.decode()
+
+    def trace_json(self):
+        """TLC -dumpTrace json: the error trace as a dict."""
+        import json
+        L = lib()
+        n = L.rmc_trace_json(self._h, None, 0)
+        if n < 0:
+            raise RaftmcError("no trace to dump")
+        buf = ctypes.create_string_buffer(n + 1)
+        L.rmc_trace_json(self._h, buf, len(buf))
+        return json.loads(buf.value.decode())
+
+    def selftest_random_trace(self, seed, steps):
+        """TEST HOOK: a seeded host random walk replayed into the model's trace (not a product path)."""
+        n = lib().rmc_selftest_random_trace(self._h, seed, steps)
+        if n < 0:
+            raise RaftmcError(lib().rmc_last_error().decode())
+        return n
 
     def report(self):
         L = lib()
