@@ -375,6 +375,11 @@ uint32_t default_kmax(const Model& M) {
   return (uint32_t)std::min(std::max(k, 24), 120);
 }
 
+// Message slots per packed row: the largest |DOMAIN messages| the last complete
+// check of this model materialized (rows then carry no dead slots), else the
+// constants-based default.  Either way an overflow re-runs with twice the slots.
+uint32_t model_kmax(const rmc_model* m) { return m->hint_kmax ? m->hint_kmax : default_kmax(m->M); }
+
 std::vector<uint32_t> init_state(const Model& M) {
   std::vector<uint32_t> S(M.words, 0u);
   S[0] = 0;  // nmsg 0, counters 0, acked all Nil (Raft.tla:209-213)
@@ -609,7 +614,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   Model& M = m->M;
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
   if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("only 64-bit fingerprints are supported");
-  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : default_kmax(M));
+  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);
   HIPCHK(upload_model(M));
@@ -663,7 +668,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   auto reset_status = [&]() {
     hst.err_key = hst.inv_err_key = hst.viol_key = ~0ULL;
     hst.cap_flags = 0;
-    hst.pad = 0;
+    hst.max_msgs = 0;
     HIPCHK(hipMemcpyAsync(stbuf.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
   };
   reset_status();
@@ -958,7 +963,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   res->materialize_ms = mat_ms;
   res->expand_launches = expand_launches;
   res->hash_capacity = slots;
-  res->max_msgs = 0;
+  res->max_msgs = hst.max_msgs;
+  if (status == 0 && !opt->max_depth && !opt->msg_cap_K) m->hint_kmax = std::max(1u, hst.max_msgs);
   return 0;
 }
 

@@ -13,7 +13,7 @@ struct DevStatus {
   unsigned long long inv_err_key;  // first evaluation error inside an invariant
   unsigned long long viol_key;     // first new state violating an invariant
   unsigned cap_flags;              // bit e set: capacity overflow ErrCode e
-  unsigned pad;
+  unsigned max_msgs;               // largest |DOMAIN messages| of a materialized state
 };
 
 // simulation mode: the first behaviour to stop the run (violation / error)

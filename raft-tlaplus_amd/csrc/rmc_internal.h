@@ -34,6 +34,10 @@ struct rmc_model {
   uint32_t kmax_user = 0;
   // sizes the last check ended with (pre-size the next check of this model)
   unsigned long long hint_slots = 0, hint_fcap = 0, hint_trcap = 0;
+  // largest |DOMAIN messages| of the last complete check: the next check of
+  // this model packs rows to exactly that many message slots (an overflow
+  // still re-runs with a larger capacity, so the hint is never unsafe)
+  uint32_t hint_kmax = 0;
 };
 
 
@@ -195,6 +199,7 @@ struct EventTimer {
 const char* act_label(int a);
 void finalize_model(rmc_model* m, uint32_t kmax);
 uint32_t default_kmax(const rmc::Model& M);
+uint32_t model_kmax(const rmc_model* m);
 std::vector<uint32_t> init_state(const rmc::Model& M);
 std::string binding_label(const rmc_model* m, int b, int act);
 void set_last_error(const std::string& s);

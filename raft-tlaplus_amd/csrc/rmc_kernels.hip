@@ -403,6 +403,7 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
   }
   __syncthreads();
   const int total = (int)sOff[np];
+  int my_max = 0;  // largest |DOMAIN messages| this thread wrote (reduced per block below)
   for (int r0 = 0; r0 < total; r0 += MAT_LIST) {
     if (tid == 0) sCount = 0;
     __syncthreads();
@@ -433,8 +434,10 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
       eval_binding<SPEC, N>(s, cM, b, d);
       const unsigned long long dst = (unsigned long long)sPos[p] + rank;
       uint32_t* o = out + dst * (unsigned long long)words;
-      int err = apply_delta<SPEC, N>(s, cM, d, o);
+      int nn = 0;
+      int err = apply_delta<SPEC, N>(s, cM, d, o, &nn);
       if (err) atomicOr(&st->cap_flags, 1u << err);
+      my_max = nn > my_max ? nn : my_max;
       const unsigned long long pg = pbase + p0 + p;
       tr_parent[out_base_global + dst] = pg;
       tr_bind[out_base_global + dst] = (uint16_t)b;
@@ -454,6 +457,14 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
     }
     __syncthreads();
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int y = __shfl_xor(my_max, o, WAVE);
+    my_max = y > my_max ? y : my_max;
+  }
+  // one hot address for the whole grid: only a wave that raises the max pays an atomic
+  if (lane == 0 && (unsigned)my_max > __hip_atomic_load(&st->max_msgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(&st->max_msgs, (unsigned)my_max);
 }
 
 // ------------------------------------------------- sharded search

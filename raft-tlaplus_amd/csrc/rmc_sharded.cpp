@@ -205,7 +205,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   Model& M = m->M;
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
   if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("only 64-bit fingerprints are supported");
-  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : default_kmax(M));
+  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);
   HIPCHK(upload_model(M));
@@ -253,7 +253,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     B.trb.ensure(s.trcap * 2);
     s.hst.err_key = s.hst.inv_err_key = s.hst.viol_key = ~0ULL;
     s.hst.cap_flags = 0;
-    s.hst.pad = 0;
+    s.hst.max_msgs = 0;
     HIPCHK(hipMemcpyAsync(B.stbuf.p, &s.hst, sizeof s.hst, hipMemcpyHostToDevice, stream));
   }
 
@@ -306,6 +306,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     HIPCHK(hipMemcpyAsync(&s.hst, s.B->stbuf.p, sizeof s.hst, hipMemcpyDeviceToHost, stream));
   };
   bool stop = false;
+  unsigned gmax_msgs = 0;  // largest |DOMAIN messages| materialized on any shard
   while (status == 0 && P > 0 && !stop) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     const unsigned level = depth + 1;
@@ -577,7 +578,9 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       // ---- first problem in TLC order stops the search (as TLC does)
       for (Shard& s : sh) read_status(s);
       HIPCHK(hipStreamSynchronize(stream));
-      for (int i = 0; i < NL; i++) rows[i] = {sh[i].hst.err_key, sh[i].hst.inv_err_key, sh[i].hst.viol_key, sh[i].hst.cap_flags};
+      for (int i = 0; i < NL; i++)
+        rows[i] = {sh[i].hst.err_key, sh[i].hst.inv_err_key, sh[i].hst.viol_key,
+                   sh[i].hst.cap_flags | ((unsigned long long)sh[i].hst.max_msgs << 32)};
       comm.allgather(rows, all, 4);
       unsigned long long ek = ~0ULL, iek = ~0ULL, vk = ~0ULL;
       unsigned capm = 0;
@@ -586,6 +589,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         iek = std::min(iek, (unsigned long long)all[4 * r + 1]);
         vk = std::min(vk, (unsigned long long)all[4 * r + 2]);
         capm |= (unsigned)all[4 * r + 3];
+        gmax_msgs = std::max(gmax_msgs, (unsigned)(all[4 * r + 3] >> 32));
       }
       if (capm) {
         status = 3;
@@ -656,6 +660,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     std::reverse(binds.begin(), binds.end());
     replay_trace(m, binds, last_b, status, message, res);
   }
+  if (status == 0 && !opt->max_depth && !opt->msg_cap_K) m->hint_kmax = std::max(1u, gmax_msgs);
+  res->max_msgs = gmax_msgs;
   if (!opt->hash_slots) m->hint_slots = sh[0].slots;
   if (!opt->frontier_cap) m->hint_fcap = sh[0].fcap;
   m->hint_trcap = sh[0].trcap;

@@ -60,7 +60,7 @@ static int simulate_impl(rmc_model* m, const rmc_options* opt, unsigned long lon
   DevStatus hst;
   hst.err_key = hst.inv_err_key = hst.viol_key = ~0ULL;
   hst.cap_flags = 0;
-  hst.pad = 0;
+  hst.max_msgs = 0;
   HIPCHK(hipMemcpyAsync(stb.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
   unsigned long long done = 0, generated = 0;
   unsigned long long round = 0;

@@ -816,7 +816,7 @@ RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta&
 // list (with its in-place count changes); the row leaves through a 4-word
 // register window, 16 B per store on the device.  Rows are 16 B aligned.
 template <int SPEC, int N>
-RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d, uint32_t* out) {
+RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d, uint32_t* out, int* nmsg_out = nullptr) {
   constexpr uint32_t NONE = 0xFFFFFFFFu;  // never a message word (mdest would be 7)
   uint32_t ins[MAXOPS];
 #pragma unroll
@@ -836,6 +836,7 @@ RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d,
     }
   }
   const int n = s.nmsg(), nn = n + ni;
+  if (nmsg_out) *nmsg_out = nn;
   if (nn > M.kmax) return E_CAP_MSG;
   uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
   int cnt = 0;

@@ -133,7 +133,7 @@ class Model:
                    violated=r.violated.decode(), message=r.message.decode(),
                    seconds=r.seconds, expand_ms=r.expand_ms, mark_ms=r.mark_ms,
                    materialize_ms=r.materialize_ms, expand_launches=r.expand_launches,
-                   state_bytes=r.state_bytes, hash_capacity=r.hash_capacity,
+                   state_bytes=r.state_bytes, hash_capacity=r.hash_capacity, max_msgs=r.max_msgs,
                    levels=[[levels[2 * k], levels[2 * k + 1]] for k in range(min(nl, 1024))])
         self._last = r
         if r.status in (1, 2):

@@ -56,6 +56,27 @@ def test_shipped_configs_match_oracle(name):
     assert r["status"] == "ok"
 
 
+@pytest.mark.parametrize("name", sorted(SHIPPED))
+def test_tight_rows_from_the_previous_check(name):
+    """The largest |DOMAIN messages| the GPU materializes equals the oracle's;
+    a second check of the same model packs rows to exactly that many message
+    slots (smaller rows) and must reproduce every count."""
+    g = SHIPPED[name]
+    m = raftmc.Model(os.path.join(ROOT, "configs", g["module"] + ".tla"), os.path.join(ROOT, g["cfg_path"]))
+    r1 = m.check()
+    assert r1["max_msgs"] == g["max_msgs"]
+    r2 = m.check()
+    assert r2["state_bytes"] <= r1["state_bytes"]
+    words = (1 + 4 * N_SERVERS[g["module"]] + g["max_msgs"] + 3) // 4 * 4  # rows are 16 B multiples
+    assert r2["state_bytes"] == 4 * words
+    assert (r2["generated"], r2["distinct"], r2["depth"], r2["levels"]) == \
+        (g["generated"], g["distinct"], g["depth"], g["levels"])
+    assert r2["max_msgs"] == g["max_msgs"]
+
+
+N_SERVERS = {"Raft": 3, "PullRaft": 3, "RaftFsync": 3, "FlexibleRaft": 5}
+
+
 def test_report_is_tlc_format():
     g = SMALL["raft_n3v1e1"]
     m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
