@@ -636,7 +636,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
   const int maxsucc = M.nfixed + M.kmax;
   unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 21);  // 2M: 4% less kernel time than 1M
-  const unsigned long long cand_cap = chunk * (unsigned long long)std::min(maxsucc, 256);
+  // + 1024 parents of slack: each of k_expand's 8 candidate segments must hold 1/8 of the tiles, rounded up
+  const unsigned long long cand_cap = (chunk + 1024) * (unsigned long long)std::min(maxsucc, 256);
 
   // Device buffers persist per device across checks (grow-only), so repeated
   // checks do not pay hipMalloc/hipFree of tens of GB each time.
@@ -656,7 +657,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   pn.ensure(chunk * 4);
   pwin.ensure(chunk * 4);
   ppos.ensure(chunk * 4);
-  counters.ensure(64);
+  counters.ensure(1024);  // 8 per-XCD candidate counters, 128 B apart (k_expand)
   stbuf.ensure(sizeof(DevStatus));
   size_t stb = scan_temp_bytes(chunk);
   scantmp.ensure(stb ? stb : 16);
@@ -777,7 +778,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       a.counters = counters.as<unsigned long long>();
       a.cand_cap = cand_cap;
       a.st = stbuf.as<DevStatus>();
-      HIPCHK(hipMemsetAsync(counters.p, 0, 64, stream));
+      HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
       HIPCHK(hipEventRecord(te.a, stream));
       launch_expand(M.spec, M.N, a, stream);
       HIPCHK(hipGetLastError());
@@ -787,9 +788,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       launch_scan(scantmp.p, scantmp.bytes, a.par_win, a.par_pos, n, stream);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(tm.b, stream));
-      unsigned long long ncand = 0;
+      unsigned long long ncand = 0, segc[128];
       uint32_t lastpos = 0, lastwin = 0;
-      HIPCHK(hipMemcpyAsync(&ncand, counters.p, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(segc, counters.p, 1024, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&lastpos, a.par_pos + (n - 1), 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&lastwin, a.par_win + (n - 1), 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&hst, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
@@ -818,6 +819,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         break;
       }
       unsigned long long W_chunk = (unsigned long long)lastpos + lastwin;
+      for (int sg = 0; sg < 8; sg++) ncand += segc[16 * sg];
       gen_lvl += ncand;
       {
         // the next-level buffer grows in place to exactly what this chunk needs

@@ -26,6 +26,7 @@ namespace rmc {
 __constant__ Model cM;
 
 constexpr int WAVE = 64;
+constexpr int EXPAND_SEGS = 8;  // candidate-buffer segments of the single-shard k_expand (one per XCD)
 constexpr unsigned long long EMPTY = ~0ULL;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
                                                 DevStatus* st, unsigned long long* __restrict__ cand_val) {
   constexpr int PB = Tile<N>::PB;
   extern __shared__ __align__(16) unsigned char lds[];
-  __shared__ unsigned long long sG;
+  __shared__ unsigned long long sG, sSeg;
   const int tid = threadIdx.x;
   const int words = cM.words, ordw = cM.ord_words, nbind = cM.nfixed + cM.kmax;
   const ExpandLds L = expand_lds(PB, words, nbind, ordw, (int)sizeof(MsgSums<N>));
@@ -257,7 +258,17 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     if (tid < PB) sBase[tid + 1] = (uint32_t)incl;
     if (tid == 0) sBase[0] = 0;
     int total = __shfl(incl, 63, WAVE);
-    if (tid == 0) sG = total ? atomicAdd(&counters[0], (unsigned long long)total) : 0ULL;
+    // one reservation per tile.  The single-shard search spreads them over 8
+    // counters (one per XCD, 128 B apart) and 8 segments of the candidate
+    // buffer: one counter for the whole grid serialized ~3x10^4 returning
+    // atomics per launch on one address.  The sharded search needs its
+    // candidates dense, so it keeps one counter.
+    if (tid == 0) {
+      const int seg = cand_val ? 0 : (int)(blockIdx.x & (EXPAND_SEGS - 1));
+      const unsigned long long seg_cap = cand_val ? cand_cap : cand_cap / EXPAND_SEGS;
+      sSeg = seg_cap;
+      sG = seg * seg_cap + (total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL);
+    }
   }
   __syncthreads();
   const int total = (int)sBase[np];
@@ -266,7 +277,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     par_off[p0 + tid] = (uint32_t)(gbase + sBase[tid]);
     par_n[p0 + tid] = sBase[tid + 1] - sBase[tid];
   }
-  if (gbase + (unsigned long long)total > cand_cap) {
+  if (gbase % sSeg + (unsigned long long)total > sSeg) {
     if (tid == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
     return;
   }
