@@ -357,14 +357,24 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
   uint32_t off = par_off[p], n = par_n[p];
   uint32_t cnt = 0;
   unsigned long long base = ((unsigned long long)level << 48) | ((pbase + p) << 10);
-  for (uint32_t t = off; t < off + n; t++) {
-    uint32_t ob = cand_ob[t];
-    bool win = false;
-    if (!(ob & 0x8000u)) {
-      unsigned long long mine = base | (ob >> 16);
-      win = table[2 * cand_slot[t] + 1] == mine;
+  // the candidates' table reads are independent: issue up to 8 before using any
+  constexpr int U = 8;
+  for (uint32_t t0 = off; t0 < off + n; t0 += U) {
+    uint32_t ob[U];
+    unsigned long long v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = t0 + u;
+      ob[u] = t < off + n ? cand_ob[t] : 0x8000u;
+      v[u] = (ob[u] & 0x8000u) ? 0ULL : table[2 * cand_slot[t] + 1];
     }
-    cand_win[t] = win ? (uint16_t)(++cnt) : (uint16_t)0;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = t0 + u;
+      if (t >= off + n) break;
+      const bool win = !(ob[u] & 0x8000u) && v[u] == (base | (ob[u] >> 16));
+      cand_win[t] = win ? (uint16_t)(++cnt) : (uint16_t)0;
+    }
   }
   par_win[p] = cnt;
 }
@@ -567,10 +577,21 @@ __global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, c
   unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= nparents) return;
   uint32_t off = par_off[p], n = par_n[p], cnt = 0;
-  for (uint32_t t = off; t < off + n; t++) {
-    uint32_t q = perm[t];
-    bool win = q != 0xFFFFFFFFu && flag_back[q];
-    cand_win[t] = win ? (uint16_t)(++cnt) : (uint16_t)0;
+  constexpr int U = 8;  // independent flag reads issued together, as in k_mark
+  for (uint32_t t0 = off; t0 < off + n; t0 += U) {
+    bool w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = t0 + u;
+      const uint32_t q = t < off + n ? perm[t] : 0xFFFFFFFFu;
+      w[u] = q != 0xFFFFFFFFu && flag_back[q];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = t0 + u;
+      if (t >= off + n) break;
+      cand_win[t] = w[u] ? (uint16_t)(++cnt) : (uint16_t)0;
+    }
   }
   par_win[p] = cnt;
 }
