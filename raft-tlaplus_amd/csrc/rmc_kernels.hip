@@ -403,7 +403,9 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
                                                      uint16_t* __restrict__ tr_bind, DevStatus* st) {
   constexpr int PB = Tile<N>::PB;
   extern __shared__ __align__(16) unsigned char lds[];
-  __shared__ uint32_t sOff[PB + 1], sPos[PB], sList[MAT_LIST];
+  // winner list: (rank << 16 | candidate index in the tile) and the candidate's ordinal/binding word,
+  // both read coalesced in the compaction pass instead of per winner later
+  __shared__ uint32_t sOff[PB + 1], sPos[PB], sList[MAT_LIST], sListOb[MAT_LIST];
   __shared__ int sCount;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int words = cM.words, Wp = words | 1;
@@ -430,26 +432,31 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
     __syncthreads();
     const int rn = total - r0 < MAT_LIST ? total - r0 : MAT_LIST;
     for (int idx = tid; idx < ((rn + 255) & ~255); idx += 256) {
-      bool w = idx < rn && cand_win[start + r0 + idx] != 0;
+      const uint32_t cw = idx < rn ? (uint32_t)cand_win[start + r0 + idx] : 0u;
+      const bool w = cw != 0;
       unsigned long long m = __ballot(w);
       int base = 0;
       if (lane == 0 && m) base = atomicAdd(&sCount, __popcll(m));
       base = __shfl(base, 0, WAVE);
-      if (w) sList[base + __popcll(m & lanemask_lt())] = (uint32_t)(r0 + idx);
+      if (w) {
+        const int at = base + __popcll(m & lanemask_lt());
+        sList[at] = ((cw - 1u) << 16) | (uint32_t)(r0 + idx);
+        sListOb[at] = cand_ob[start + r0 + idx];
+      }
     }
     __syncthreads();
     const int nw = sCount;
     for (int e = tid; e < nw; e += 256) {
-      const int idx = (int)sList[e];
+      const int idx = (int)(sList[e] & 0xFFFFu);
       int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
       while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
         if ((int)sOff[mid] <= idx) lo = mid; else hi = mid - 1;
       }
       const int p = lo;
-      const uint32_t ob = cand_ob[start + idx];
+      const uint32_t ob = sListOb[e];
       const int b = (int)(ob & 0x3FFu);
-      const int rank = (int)cand_win[start + idx] - 1;
+      const int rank = (int)(sList[e] >> 16);
       PState<SPEC, N> s{sS + p * Wp};
       Delta d;
       eval_binding<SPEC, N>(s, cM, b, d);
