@@ -385,14 +385,21 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
 // from the LDS-staged parent and its binding, write it to its TLC-order slot
 // of the next frontier, write the trace record, check the cfg's invariants.
 #ifndef RMC_MAT_LIST
-#define RMC_MAT_LIST 1024
+#define RMC_MAT_LIST 512
 #endif
 constexpr int MAT_LIST = RMC_MAT_LIST;
-#ifndef RMC_MAT_WAVES
-#define RMC_MAT_WAVES 1
+// Threads per k_materialize block.  A tile of PB = 64 parents yields about
+// PB winners on average (every distinct state is a parent once), so 256
+// threads left most lanes idle in the winner loop.  Measured on the bench
+// workload (k_materialize ms per check): 256 thr/1024-entry list 585, 128/512
+// 539, 128/256 544, 64/256 627 (LDS-limited blocks, slower tile staging).
+#ifndef RMC_MAT_THREADS
+#define RMC_MAT_THREADS 128
 #endif
+constexpr int MAT_T = RMC_MAT_THREADS;
+static_assert(MAT_T % 64 == 0 && MAT_T >= 64, "one thread per tile parent");
 template <int SPEC, int N>
-__global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+__global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                      unsigned long long pbase, const uint32_t* __restrict__ cand_ob,
                                                      const uint16_t* __restrict__ cand_win,
                                                      const uint32_t* __restrict__ par_off,
@@ -401,7 +408,7 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
                                                      unsigned long long out_base_global,
                                                      unsigned long long* __restrict__ tr_parent,
                                                      uint16_t* __restrict__ tr_bind, DevStatus* st) {
-  constexpr int PB = Tile<N>::PB;
+  constexpr int PB = Tile<N>::PB;  // must be k_expand's tile: a tile's candidates are contiguous only within one expand tile
   extern __shared__ __align__(16) unsigned char lds[];
   // winner list: (rank << 16 | candidate index in the tile) and the candidate's ordinal/binding word,
   // both read coalesced in the compaction pass instead of per winner later
@@ -415,7 +422,7 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
   const uint32_t start = par_off[p0];
   const uint32_t* src = frontier + p0 * (unsigned long long)words;
-  for (int q = tid; q < np * words; q += 256) {
+  for (int q = tid; q < np * words; q += MAT_T) {
     int p = q / words;
     sS[p * Wp + (q - p * words)] = src[q];
   }
@@ -431,7 +438,7 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
     if (tid == 0) sCount = 0;
     __syncthreads();
     const int rn = total - r0 < MAT_LIST ? total - r0 : MAT_LIST;
-    for (int idx = tid; idx < ((rn + 255) & ~255); idx += 256) {
+    for (int idx = tid; idx < ((rn + MAT_T - 1) / MAT_T) * MAT_T; idx += MAT_T) {
       const uint32_t cw = idx < rn ? (uint32_t)cand_win[start + r0 + idx] : 0u;
       const bool w = cw != 0;
       unsigned long long m = __ballot(w);
@@ -446,7 +453,7 @@ __global__ __launch_bounds__(256, RMC_MAT_WAVES) void k_materialize(const uint32
     }
     __syncthreads();
     const int nw = sCount;
-    for (int e = tid; e < nw; e += 256) {
+    for (int e = tid; e < nw; e += MAT_T) {
       const int idx = (int)(sList[e] & 0xFFFFu);
       int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
       while (lo < hi) {
@@ -651,10 +658,10 @@ struct Launch {
   }
   template <int SPEC, int N>
   static void materialize(const LevelArgs& a, hipStream_t s) {
-    constexpr int PB = Tile<N>::PB;
+    constexpr int PB = Tile<N>::PB;  // must be k_expand's tile: a tile's candidates are contiguous only within one expand tile
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
-    size_t lds_bytes = ((size_t)PB * (a.model->words | 1) + 256 * (1 + 4 * N)) * 4;
-    hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(256), lds_bytes, s, a.frontier, a.nparents,
+    size_t lds_bytes = ((size_t)PB * (a.model->words | 1) + MAT_T * (1 + 4 * N)) * 4;
+    hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(MAT_T), lds_bytes, s, a.frontier, a.nparents,
                        a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
                        a.tr_parent, a.tr_bind, a.st);
   }

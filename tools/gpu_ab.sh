@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 CFG=${CFG:-Raft_n3v2e2}
 for i in 1 2; do
-  for v in build build_b; do
+  for v in ${BUILDS:-build build_b}; do
     timeout -k 10 120 ./raft-tlaplus_amd/$v/raftmc -deadlock -json configs/Raft.tla -config configs/$CFG.cfg > gpurun_out/ab_$v.txt 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab_$v.txt; exit 1; }
     echo "$v $(tail -1 gpurun_out/ab_$v.txt)"
   done
