@@ -556,10 +556,23 @@ std::string def_location(const rmc_model* m, const std::string& op) {
 // ----------------------------------------------------------- BFS driver
 namespace rmcx {
 
+// Per-chunk readbacks land in pinned host memory, so they are true async
+// copies: one stream sync per chunk (after the mark/scan), none after
+// k_materialize — its status is snapshotted into `mat` in stream order and
+// examined at the next sync.
+struct HostReadback {
+  unsigned long long segc[128];  // k_expand's 8 per-XCD candidate counters, 128 B apart
+  uint32_t lastpos, lastwin;     // the chunk's last parent: scan position and winner count
+  DevStatus st;                  // status after the chunk's mark/scan
+  DevStatus mat;                 // status after the chunk's k_materialize
+};
 struct Arena {
   DevBuf table, table2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
+  HostReadback* hrb = nullptr;
   void release() {
+    if (hrb) (void)hipHostFree(hrb);
+    hrb = nullptr;
     for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
       b->release();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
@@ -659,6 +672,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   ppos.ensure(chunk * 4);
   counters.ensure(1024);  // 8 per-XCD candidate counters, 128 B apart (k_expand)
   stbuf.ensure(sizeof(DevStatus));
+  if (!A.hrb) HIPCHK(hipHostMalloc((void**)&A.hrb, sizeof(HostReadback), hipHostMallocDefault));
+  HostReadback* const hrb = A.hrb;
   size_t stb = scan_temp_bytes(chunk);
   scantmp.ensure(stb ? stb : 16);
   unsigned long long trcap = std::max(fcap * 4, m->hint_trcap);
@@ -724,12 +739,33 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     unsigned long long next_n = 0, gen_lvl = 0;
+    // the last k_materialize's snapshot (hrb->mat) is not examined yet; call
+    // after a stream sync.  True when it ended the search (status 3 set, or
+    // hst holds the error/violation keys).
+    bool mat_pending = false;
+    auto finish_mat = [&]() -> bool {
+      mat_pending = false;
+      float mms = 0;
+      HIPCHK(hipEventElapsedTime(&mms, tz.a, tz.b));
+      mat_ms += mms;
+      hst = hrb->mat;
+      if (hst.cap_flags) {
+        status = 3;
+        message = "capacity overflow while materializing";
+        return true;
+      }
+      return hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL;
+    };
     for (unsigned long long c0 = 0; c0 < cur_n; c0 += chunk) {
       unsigned long long n = std::min(chunk, cur_n - c0);
       // grow the table before it passes 1/2 load (worst case: every candidate
       // new).  If HBM cannot hold the doubled table, carry on at up to 0.9 load.
       const unsigned long long need = entries_hint + n * (unsigned long long)maxsucc;
       if (need * 2 > slots && !table_full_ok) {
+        if (mat_pending) {  // the previous chunk may have ended the search: no growth for nothing
+          HIPCHK(hipStreamSynchronize(stream));
+          if (finish_mat()) break;
+        }
         unsigned long long nslots = slots;
         while (need * 2 > nslots) nslots <<= 1;
         if (opt->hash_slots) throw std::runtime_error("fingerprint set full (raise hash_slots)");
@@ -788,13 +824,16 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       launch_scan(scantmp.p, scantmp.bytes, a.par_win, a.par_pos, n, stream);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(tm.b, stream));
-      unsigned long long ncand = 0, segc[128];
-      uint32_t lastpos = 0, lastwin = 0;
-      HIPCHK(hipMemcpyAsync(segc, counters.p, 1024, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(&lastpos, a.par_pos + (n - 1), 4, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(&lastwin, a.par_win + (n - 1), 4, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(&hst, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
+      unsigned long long ncand = 0;
+      HIPCHK(hipMemcpyAsync(hrb->segc, counters.p, 1024, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&hrb->lastpos, a.par_pos + (n - 1), 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&hrb->lastwin, a.par_win + (n - 1), 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&hrb->st, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
+      // the previous chunk's k_materialize outcome first: if it stopped the
+      // search, this chunk's expand never happened as far as the counts go
+      if (mat_pending && finish_mat()) break;
+      hst = hrb->st;
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
       expand_ms += ms;
@@ -818,8 +857,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         message = std::string("capacity overflow: ") + names[e];
         break;
       }
-      unsigned long long W_chunk = (unsigned long long)lastpos + lastwin;
-      for (int sg = 0; sg < 8; sg++) ncand += segc[16 * sg];
+      unsigned long long W_chunk = (unsigned long long)hrb->lastpos + hrb->lastwin;
+      for (int sg = 0; sg < 8; sg++) ncand += hrb->segc[16 * sg];
       gen_lvl += ncand;
       {
         // the next-level buffer grows in place to exactly what this chunk needs
@@ -854,18 +893,19 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       launch_materialize(M.spec, M.N, a, stream);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(tz.b, stream));
-      HIPCHK(hipMemcpyAsync(&hst, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-      HIPCHK(hipEventElapsedTime(&ms, tz.a, tz.b));
-      mat_ms += ms;
+      HIPCHK(hipMemcpyAsync(&hrb->mat, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
+      mat_pending = true;
       next_n += W_chunk;
       entries_hint += W_chunk;
-      if (hst.cap_flags) {
-        status = 3;
-        message = "capacity overflow while materializing";
+      if (hst.err_key != ~0ULL) {  // this chunk's expand hit an evaluation error: the search stops here
+        HIPCHK(hipStreamSynchronize(stream));
+        finish_mat();
         break;
       }
-      if (hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL) break;
+    }
+    if (mat_pending) {
+      HIPCHK(hipStreamSynchronize(stream));
+      finish_mat();
     }
     generated += gen_lvl;
     distinct += next_n;
