@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--logical-shards", type=int, default=0)
+    ap.add_argument("--chunk", type=int, default=0, help="parents per k_expand launch (0 = librmc's default)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -118,7 +119,7 @@ def main():
     elif args.logical_shards:
         run_check = lambda: model.check_logical(args.logical_shards)  # noqa: E731
     else:
-        run_check = model.check
+        run_check = lambda: model.check(chunk_parents=args.chunk)  # noqa: E731
 
     def barrier():
         if dist is not None:

@@ -693,27 +693,32 @@ void launch_mark(const LevelArgs& a, hipStream_t s) {
                      a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.cand_win, a.par_win);
 }
 // Move every entry of the old fingerprint set into a larger one (values kept).
+// Grid-stride: a table of 2^32 slots or more would need a grid of 2^32
+// threads or more, past HIP's launch limit.
 __global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __restrict__ old, unsigned long long nold,
                                                 unsigned long long* __restrict__ nt, unsigned long long mask,
                                                 DevStatus* st) {
-  unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nold) return;
-  unsigned long long k = old[2 * e];
-  if (k == EMPTY) return;
-  unsigned long long slot = (k ^ (k >> 29)) & mask;
-  for (unsigned long long probe = 0; probe <= mask; probe++) {
-    unsigned long long prev = atomicCAS(nt + 2 * slot, EMPTY, k);
-    if (prev == EMPTY) {
-      nt[2 * slot + 1] = old[2 * e + 1];
-      return;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; e < nold; e += stride) {
+    unsigned long long k = old[2 * e];
+    if (k == EMPTY) continue;
+    unsigned long long slot = (k ^ (k >> 29)) & mask;
+    unsigned long long probe = 0;
+    for (; probe <= mask; probe++) {
+      unsigned long long prev = atomicCAS(nt + 2 * slot, EMPTY, k);
+      if (prev == EMPTY) {
+        nt[2 * slot + 1] = old[2 * e + 1];
+        break;
+      }
+      slot = (slot + 1) & mask;
     }
-    slot = (slot + 1) & mask;
+    if (probe > mask) atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
   }
-  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
 }
 void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
                    unsigned long long nmask, DevStatus* st, hipStream_t s) {
   unsigned long long blocks = (nold + 255) / 256;
+  if (blocks > (1ULL << 22)) blocks = 1ULL << 22;  // 2^30 threads, each striding
   hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, s, old, nold, nt, nmask, st);
 }
 size_t scan_temp_bytes(unsigned long long n) {
