@@ -178,6 +178,20 @@ def main():
             "kernel_ms": {"expand": res["expand_ms"], "mark_scan": res["mark_ms"],
                           "materialize": res["materialize_ms"]},
         }
+        # atomic throughput of the fingerprint-set inserts (each
+        # successor: one returning CAS per probe + one atomicMin), over k_expand's time
+        if res["expand_ms"] > 0:
+            line["fpset_inserts"] = {"count": res["generated"] - 1,
+                                     "per_s": (res["generated"] - 1) / (res["expand_ms"] * 1e-3),
+                                     "atomics_per_insert": ">= 2 (CAS per probe + atomicMin)"}
+        if world > 1:
+            # exchange volume of the sharded protocol: 16 B (fp, key) records,
+            # 1 B win flags, rows + 10 B trace records; the off-GPU fraction is (W-1)/W,
+            # point-to-point over xGMI (7 links x ~153 GB/s per MI355X)
+            G, D, S = res["generated"] - 1, res["distinct"], res["state_bytes"]
+            xb = (G * 17 + D * (S + 10)) * (world - 1) / world
+            line["xgmi"] = {"bytes": xb, "per_gpu_GBps": xb / world / per_step / 1e9,
+                            "peak_per_gpu_GBps": 7 * 153.0}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(module, cfg_rel, args.cpu_seconds)
