@@ -778,17 +778,21 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         } catch (OutOfDeviceMemory&) {
           grown = false;
         }
+        const double t_alloc = secs(tr0, now());
         if (grown) {
           HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
           launch_rehash(table.as<unsigned long long>(), slots, nt.as<unsigned long long>(), nslots - 1,
                         stbuf.as<DevStatus>(), stream);
           HIPCHK(hipGetLastError());
           HIPCHK(hipStreamSynchronize(stream));
+          const double t_fill = secs(tr0, now()) - t_alloc;
           std::swap(table.p, nt.p);
           std::swap(table.bytes, nt.bytes);
           slots = nslots;
           if (nt.bytes >= (1ULL << 30)) nt.release();  // large searches need the HBM more than a spare table
-          if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots\n", __builtin_ctzll(slots));
+          if (opt->verbose)
+            fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (alloc %.3fs, fill+rehash %.3fs, free %.3fs)\n",
+                    __builtin_ctzll(slots), t_alloc, t_fill, secs(tr0, now()) - t_alloc - t_fill);
         } else {
           table_full_ok = true;
           if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(slots));
