@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 #include "rmc_spec.h"
 #include "rmc_engine.h"
+#include "rmc_fpset.h"
 
 namespace rmc {
 
@@ -27,7 +28,6 @@ __constant__ Model cM;
 
 constexpr int WAVE = 64;
 constexpr int EXPAND_SEGS = 8;  // candidate-buffer segments of the single-shard k_expand (one per XCD)
-constexpr unsigned long long EMPTY = ~0ULL;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -38,30 +38,6 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
 // first-in-TLC-order error / violation keys: (parent_global << 20) | (ordinal << 10) | binding
 __device__ __forceinline__ unsigned long long order_key(unsigned long long pg, int ordinal, int b) {
   return (pg << 20) | ((unsigned long long)ordinal << 10) | (unsigned long long)b;
-}
-
-// Insert fp with value val; returns the slot.  val = (level << 48) | rank.
-// One returning atomic per probe: the CAS doubles as the read (measured
-// faster than a 16 B load first: 976 vs 989 ms of k_expand on the bench cfg).
-// An entry from an earlier level has a smaller val, so the atomicMin that
-// claims first-in-TLC-order within the level never changes it.
-__device__ __forceinline__ unsigned long long table_insert(unsigned long long* T, unsigned long long mask,
-                                                           unsigned long long fp, unsigned long long val,
-                                                           unsigned level, DevStatus* st) {
-  (void)level;
-  if (fp == EMPTY) fp = EMPTY - 1;
-  unsigned long long slot = (fp ^ (fp >> 29)) & mask;
-  for (unsigned long long probe = 0; probe <= mask; probe++) {
-    unsigned long long* e = T + 2 * slot;
-    unsigned long long prev = atomicCAS(e, EMPTY, fp);
-    if (prev == EMPTY || prev == fp) {
-      atomicMin(e + 1, val);
-      return slot;
-    }
-    slot = (slot + 1) & mask;
-  }
-  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
-  return 0;
 }
 
 // Diagnostic build only (-DRMC_STAMPS): per-phase block time of k_expand,
