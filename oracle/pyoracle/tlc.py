@@ -250,8 +250,6 @@ def bfs(spec, max_states=None, keep_states=False, progress=False):
                     break
             if res.status != "ok":
                 break
-            if max_states and len(states) >= max_states:
-                break
         if res.status != "ok":
             res.levels.append((gen_lvl, len(nxt)))
             res.depth = depth + (1 if nxt else 0)

@@ -52,6 +52,30 @@ MEDIUM = [
     ("raft_n4v1e1", "Raft", dict(n=4, v=1, E=1)),
 ]
 
+# 5-server cases (the N=5 kernels: 120-permutation symmetry).  Exhaustive runs
+# take the C oracle minutes to hours, so these are pinned level by level up to
+# the first level at which the oracle has found >= max_distinct states
+# (truncated at a level boundary; the GPU runs the same number of levels).
+# (name, module, kwargs, C oracle max_distinct, Python oracle max_states)
+N5 = [
+    ("flex_n5v1e1_eq3rq3", "FlexibleRaft", dict(n=5, v=1, E=1, ElectionQuorumSize=3, ReplicationQuorumSize=3),
+     400000, 3000),
+    ("flex_n5v1e1_eq3rq4", "FlexibleRaft", dict(n=5, v=1, E=1, ElectionQuorumSize=3, ReplicationQuorumSize=4),
+     400000, 3000),
+    ("flex_n5v1e1_eq2rq4", "FlexibleRaft", dict(n=5, v=1, E=1, ElectionQuorumSize=2, ReplicationQuorumSize=4),
+     400000, 3000),
+    # FlexibleRaft.cfg's constants (BASELINE config 3), first levels
+    ("flex_n5v2e2_cfg", "FlexibleRaft", dict(n=5, v=2, E=2, ElectionQuorumSize=3, ReplicationQuorumSize=4),
+     1000000, 3000),
+    ("raft_n5v1e1", "Raft", dict(n=5, v=1, E=1), 400000, 3000),
+    ("pull_n5v1e1", "PullRaft", dict(n=5, v=1, E=1), 400000, 3000),
+    ("fsync_n5v1e1r1", "RaftFsync", dict(n=5, v=1, E=1, R=1), 400000, 3000),
+]
+# 5 servers, election quorums of 2 (two disjoint quorums elect two leaders of one term)
+N5_UNSAFE = [
+    ("flex_n5v1e2_eq2rq2_unsafe", "FlexibleRaft", dict(n=5, v=1, E=2, ElectionQuorumSize=2, ReplicationQuorumSize=2)),
+]
+
 # known-unsafe configs (violations reachable): Flexible
 # with quorums of 1 (FlexibleRaft.tla:16-24 lists the valid pairs; these are not)
 UNSAFE = [

@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import MEDIUM, SMALL, UNSAFE, cfg_text  # noqa: E402
+from cfgs import MEDIUM, N5, N5_UNSAFE, SMALL, UNSAFE, cfg_text  # noqa: E402
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
     ("Raft_cfg", "Raft", "configs/Raft.cfg"),
@@ -47,11 +47,45 @@ def unsafe():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def n5():
+    """--n5: 5-server cases, level-truncated (cfgs.N5).  The C oracle runs to the
+    first level boundary past max_distinct; the Python oracle runs a shorter
+    prefix and must agree with the C oracle on every level it completed."""
+    only_unsafe = "--n5-unsafe" in sys.argv
+    out = json.load(open(os.path.join(HERE, "n5.json"))) if only_unsafe else {}
+    for name, module, kw, c_max, py_max in ([] if only_unsafe else N5):
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=8,
+                      extra=["--max-distinct", str(c_max)])
+        p = bfs(make_spec(module, cfg), max_states=py_max)
+        pl = [list(x) for x in p.levels]
+        if pl != c["levels"][:len(pl)]:
+            raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pl, c["levels"][:len(pl)]))
+        out[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"],
+                         depth=c["depth"], status=c["status"], levels=c["levels"], max_distinct=c_max,
+                         max_msgs=c["max_msgs"], hidden_same_level=c["hidden_same_level"],
+                         pyoracle_levels=len(pl), pinned_by="coracle; first %d levels pyoracle==coracle" % len(pl))
+        print(name, c["generated"], c["distinct"], c["depth"], "py levels", len(pl), flush=True)
+    for name, module, kw in N5_UNSAFE:  # C oracle only (the Python oracle would take hours)
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=1, extra=["--trace"])
+        out[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], violated=c["violated"], levels=c["levels"],
+                         trace_len=len(c.get("trace", [])), pinned_by="coracle")
+        print(name, c["generated"], c["distinct"], c["depth"], c["status"], c["violated"], flush=True)
+    with open(os.path.join(HERE, "n5.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     if "--shipped-one" in sys.argv:
         return shipped()
     if "--unsafe" in sys.argv:
         return unsafe()
+    if "--n5" in sys.argv or "--n5-unsafe" in sys.argv:
+        return n5()
     out = {}
     for name, module, kw in SMALL:
         txt = cfg_text(module, **kw)
