@@ -43,12 +43,14 @@ typedef struct {
   int deadlock_check;  /* 0 = TLC -deadlock (the reference's mode); 1 is rejected */
   int fp_bits;         /* 64 (default) */
   int tlc_order;       /* 1 (default): first successor in TLC order wins per fingerprint */
-  uint64_t hash_slots; /* fingerprint-set capacity (power of two); 0 = auto */
+  uint64_t hash_slots; /* initial fingerprint-set capacity, main tier (power of two; grows on demand); 0 = auto */
   uint32_t msg_cap_K;  /* message slots per packed state; 0 = auto */
   uint64_t frontier_cap; /* max states per BFS level; 0 = auto */
   uint32_t chunk_parents; /* parents expanded per launch; 0 = auto */
   int verbose;         /* per-level progress on stderr */
   int max_depth;       /* stop after this many levels (0 = exhaustive) */
+  uint64_t level_slots; /* tuning/test: level-tier slots at every level start, no pre-chunk growth, so an
+                           overflow takes the grow-and-redo path (power of two; 0 = auto) */
 } rmc_options;
 
 typedef struct {
@@ -57,7 +59,9 @@ typedef struct {
   int status; /* 0 ok, 1 invariant violated, 2 evaluation error, 3 capacity overflow, 4 stopped (max_depth) */
   char violated[64];
   char message[256];
-  uint64_t hidden_var_collisions; /* reserved */
+  uint64_t hidden_var_collisions; /* same-level duplicates whose VIEW-hidden variables (acked, electionCtr,
+                                     restartCtr; Pull: the counters) differ from the first-in-TLC-order winner's
+                                     (SURVEY.md §7 hard part 1); equal to the oracle's hidden_same_level */
   double seconds;
   /* measurement (filled by rmc_check) */
   double expand_ms, mark_ms, materialize_ms; /* summed device time per kernel family */

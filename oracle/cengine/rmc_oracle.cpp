@@ -984,6 +984,7 @@ struct Checker {
   uint64_t max_distinct = 0;
   double max_seconds = 0;
   int threads = 1;
+  bool reverse_order = false;
   FILE* fpdump = nullptr;
   int64_t bad_index = -1;
 
@@ -1083,8 +1084,13 @@ void Checker::run() {
       for (auto& x : th) x.join();
       for (int w = 0; w < T; w++) st.max_msgs = std::max(st.max_msgs, mm[w]);
       // sequential first-wins insertion in (parent, ordinal) order
-      for (int w = 0; w < T && !stop; w++) {
-        for (size_t q = 0; q < cands[w].size() && !stop; q++) {
+      for (int w0 = 0; w0 < T && !stop; w0++) {
+        // --reverse-order (probe only): the LAST successor in TLC order wins
+        // within a chunk -- a fixture whose counts change under it is one where
+        // TLC's first-wins rule matters
+        const int w = reverse_order ? T - 1 - w0 : w0;
+        for (size_t q0 = 0; q0 < cands[w].size() && !stop; q0++) {
+          const size_t q = reverse_order ? cands[w].size() - 1 - q0 : q0;
           const Cand& c = cands[w][q];
           if (!errs[w].empty() && c.parent_local >= errp[w]) break;
           gen_lvl++;
@@ -1255,6 +1261,7 @@ int main(int argc, char** argv) {
     else if (k == "--max-seconds") ck.max_seconds = std::stod(val());
     else if (k == "--threads") ck.threads = std::stoi(val());
     else if (k == "--trace") print_trace = true;
+    else if (k == "--reverse-order") ck.reverse_order = true;
     else if (k == "--dump-fps") fpdump = val();
     else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
   }

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -17,6 +18,7 @@
 #include <string>
 #include <vector>
 #include "rmc_internal.h"
+#include "rmc_fpset.h"
 
 using namespace rmc;
 using namespace rmcx;
@@ -362,8 +364,10 @@ void finalize_model(rmc_model* m, uint32_t kmax) {
   Model& M = m->M;
   // rows are a multiple of 4 words (16 B aligned for the kernels' vector
   // stores); the padding becomes message capacity
+  // (padding can give up to 123 slots for a request of 120: never round a
+  // request down below itself -- the regrow path asks for exactly 120)
   int words = (1 + 4 * M.N + (int)kmax + 3) & ~3;
-  if (words - 1 - 4 * M.N > 120) words -= 4;
+  if (words - 1 - 4 * M.N > 124) words -= 4;
   M.words = words;
   M.kmax = words - 1 - 4 * M.N;
   build_actions(M);
@@ -567,13 +571,16 @@ struct HostReadback {
   DevStatus mat;                 // status after the chunk's k_materialize
 };
 struct Arena {
-  DevBuf table, table2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  // table/table2: fingerprint set main tier (8 B keys) and its growth target;
+  // ltab/ltab2: level tier (16 B (fp, val) entries) and its growth target
+  DevBuf table, table2, ltab, ltab2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   HostReadback* hrb = nullptr;
   void release() {
     if (hrb) (void)hipHostFree(hrb);
     hrb = nullptr;
-    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
+    for (DevBuf* b : {&table, &table2, &ltab, &ltab2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
+                      &scantmp})
       b->release();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
@@ -637,21 +644,22 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   res->state_bytes = (uint32_t)(W * 4);
 
   // ---- sizing
-  size_t freeb = 0, totalb = 0;
-  HIPCHK(hipMemGetInfo(&freeb, &totalb));
-  unsigned long long slots = opt->hash_slots;
-  if (!slots) {
-    // 1 GiB table grown on demand; a model checked before starts at the size
-    // its last check ended with (TLC's preallocated FPSet, -fpmem, in spirit)
-    slots = std::max(1ULL << 26, m->hint_slots);
-  }
-  if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
+  // Fingerprint set, main tier: starts at hash_slots (or at the size the last
+  // check of this model ended with -- TLC's preallocated FPSet, -fpmem, in
+  // spirit) and doubles at level ends past 0.6 load.  The level tier is sized
+  // per level from the previous level's growth (below).
+  unsigned long long mslots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 24, m->hint_slots);
+  if (mslots & (mslots - 1)) throw std::runtime_error("hash_slots must be a power of two");
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
   const int maxsucc = M.nfixed + M.kmax;
   // 4M parents per launch: 4% less k_expand time than 2M on the bench cfg (2M: 4% less than 1M)
   unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 22);
   // + 1024 parents of slack: each of k_expand's 8 candidate segments must hold 1/8 of the tiles, rounded up
   const unsigned long long cand_cap = (chunk + 1024) * (unsigned long long)std::min(maxsucc, 256);
+  // candidate indices (par_off, k_mark, k_materialize's winner list) are 32-bit
+  if (cand_cap > 0xFFFFFFFFULL)
+    throw std::runtime_error("chunk_parents too large: " + std::to_string(chunk) + " parents x " +
+                             std::to_string(std::min(maxsucc, 256)) + " bindings exceeds 2^32 candidates per launch");
 
   // Device buffers persist per device across checks (grow-only), so repeated
   // checks do not pay hipMalloc/hipFree of tens of GB each time.
@@ -660,8 +668,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   DevBuf &poff = A.poff, &pn = A.pn, &pwin = A.pwin, &ppos = A.ppos, &counters = A.counters, &stbuf = A.stbuf;
   DevBuf& scantmp = A.scantmp;
   GrowBuf &fa = A.fa, &fb = A.fb, &trp = A.trp, &trb = A.trb;
-  table.ensure(slots * 16);
-  HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * 16, stream));
+  table.ensure(mslots * 8);
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, mslots * 8, stream));
   fa.ensure(fcap * W * 4);
   fb.ensure(fcap * W * 4);
   cslot.ensure(cand_cap * 8);
@@ -686,9 +694,83 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     hst.err_key = hst.inv_err_key = hst.viol_key = ~0ULL;
     hst.cap_flags = 0;
     hst.max_msgs = 0;
+    hst.hidden_coll = 0;
     HIPCHK(hipMemcpyAsync(stbuf.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
   };
   reset_status();
+
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  double rehash_s = 0, grow_s = 0;
+
+  // ---- level tier: [0, lclean) of A.ltab is known empty; lact = slots in use
+  // this level (a power of two).  k_merge empties the used slots at each level
+  // end, so only the growth of the used range is ever cleared by a memset.
+  unsigned long long lact = 0, lclean = 0, lmax = 0;
+  auto l_begin_level = [&](unsigned long long slots) {  // the tier is empty between levels
+    if (A.ltab.bytes < slots * 16) {
+      A.ltab.ensure(slots * 16);
+      HIPCHK(hipMemsetAsync(A.ltab.p, 0xFF, A.ltab.bytes, stream));
+      lclean = A.ltab.bytes / 16;
+    } else if (lclean < slots) {
+      HIPCHK(hipMemsetAsync(A.ltab.as<unsigned long long>() + 2 * lclean, 0xFF, (slots - lclean) * 16, stream));
+      lclean = slots;
+    }
+    lact = slots;
+    lmax = std::max(lmax, lact);
+  };
+  auto l_grow = [&](unsigned long long nslots) {  // mid-level: rehash the level's entries into nslots
+    auto tg0 = now();
+    HIPCHK(hipStreamSynchronize(stream));
+    A.ltab2.ensure(nslots * 16);
+    HIPCHK(hipMemsetAsync(A.ltab2.p, 0xFF, nslots * 16, stream));
+    launch_rehash(A.ltab.as<unsigned long long>(), lact, A.ltab2.as<unsigned long long>(), nslots - 1,
+                  stbuf.as<DevStatus>(), stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(stream));
+    std::swap(A.ltab.p, A.ltab2.p);
+    std::swap(A.ltab.bytes, A.ltab2.bytes);
+    if (A.ltab2.bytes >= (1ULL << 30)) A.ltab2.release();  // large searches need the HBM more than a spare
+    lclean = lact = nslots;
+    lmax = std::max(lmax, lact);
+    rehash_s += secs(tg0, now());
+    if (opt->verbose) fprintf(stderr, "[rmc] level tier grown to 2^%d slots\n", __builtin_ctzll(nslots));
+  };
+  // ---- main tier: room for `need` keys at <= 0.6 load (0.9 once HBM is full)
+  bool mfull_ok = false;
+  auto m_fit = [&](unsigned long long need) {
+    if (need * 5 <= mslots * 3) return;
+    if (!mfull_ok) {
+      unsigned long long nslots = mslots;
+      while (need * 5 > nslots * 3) nslots <<= 1;
+      auto tr0 = now();
+      try {
+        A.table2.ensure(nslots * 8);
+      } catch (OutOfDeviceMemory&) {
+        mfull_ok = true;
+      }
+      if (!mfull_ok) {
+        HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * 8, stream));
+        launch_rehash_main(table.as<unsigned long long>(), mslots, A.table2.as<unsigned long long>(), nslots - 1,
+                           stbuf.as<DevStatus>(), stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(stream));
+        std::swap(table.p, A.table2.p);
+        std::swap(table.bytes, A.table2.bytes);
+        mslots = nslots;
+        if (A.table2.bytes >= (1ULL << 30)) A.table2.release();
+        rehash_s += secs(tr0, now());
+        if (opt->verbose)
+          fprintf(stderr, "[rmc] fingerprint set (main tier) grown to 2^%d slots (%.3fs)\n", __builtin_ctzll(mslots),
+                  secs(tr0, now()));
+        return;
+      }
+      if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(mslots));
+    }
+    if (need * 10 > mslots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
+  };
 
   // ---- level 1: Init (Raft.tla:213-218)
   std::vector<uint32_t> init = init_state(M);
@@ -696,9 +778,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   {
     unsigned long long fp = host_fingerprint(M, init.data());
     if (fp == ~0ULL) fp--;
-    unsigned long long slot = (fp ^ (fp >> 29)) & (slots - 1);
-    unsigned long long ent[2] = {fp, (1ULL << 48)};
-    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + 2 * slot, ent, 16, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + fp_slot(fp, mslots - 1), &fp, 8, hipMemcpyHostToDevice, stream));
     unsigned long long root = ~0ULL;
     uint16_t zero = 0;
     HIPCHK(hipMemcpyAsync(trp.p, &root, 8, hipMemcpyHostToDevice, stream));
@@ -723,23 +803,56 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     else if (bad >= 0) { status = 1; snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str()); bad_state = 0; }
   }
   EventTimer te, tm, tz;
-  double rehash_s = 0, grow_s = 0;
-  auto now = [] { return std::chrono::steady_clock::now(); };
-  auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-    return std::chrono::duration<double>(b - a).count();
-  };
   double expand_ms = 0, mark_ms = 0, mat_ms = 0;
-  unsigned long long expand_launches = 0;
+  unsigned long long expand_launches = 0, redos = 0;
   uint32_t* cur = fa.as<uint32_t>();
   uint32_t* nxt = fb.as<uint32_t>();
-  unsigned long long entries_hint = 1;
-  bool table_full_ok = false;
+  double rate = 4.0;  // new states per parent of the previous level (sizes the level tier)
+  // the level that stopped the search (exact counts at the failing state, below)
+  struct ChunkLog { unsigned long long c0, gen_before, new_before; };
+  std::vector<ChunkLog> chunk_log;
+  unsigned long long stop_level_base = 0, stop_level_n = 0, stop_gen_before = 0, stop_dist_before = 0;
+  const uint32_t* stop_front = nullptr;
+  unsigned stop_level = 0;
+  auto fill_args = [&](LevelArgs& a, unsigned long long c0, unsigned long long n, unsigned level) {
+    memset(&a, 0, sizeof a);
+    a.model = &M;
+    a.frontier = cur + c0 * W;
+    a.nparents = n;
+    a.pbase = cur_base + c0;
+    a.level = level;
+    a.mkeys = table.as<unsigned long long>();
+    a.mmask = mslots - 1;
+    a.table = A.ltab.as<unsigned long long>();
+    a.mask = lact - 1;
+    a.cand_slot = cslot.as<unsigned long long>();
+    a.cand_ob = cob.as<uint32_t>();
+    a.cand_win = cwin.as<uint16_t>();
+    a.par_off = poff.as<uint32_t>();
+    a.par_n = pn.as<uint32_t>();
+    a.par_win = pwin.as<uint32_t>();
+    a.par_pos = ppos.as<uint32_t>();
+    a.counters = counters.as<unsigned long long>();
+    a.cand_cap = cand_cap;
+    a.st = stbuf.as<DevStatus>();
+  };
   try {
   while (status == 0 && cur_n > 0) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
+    if (cur_base + cur_n >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
     unsigned long long next_n = 0, gen_lvl = 0;
+    chunk_log.clear();
+    if (opt->level_slots) {  // fixed start, growth only through the overflow-and-redo path
+      if (opt->level_slots & (opt->level_slots - 1)) throw std::runtime_error("level_slots must be a power of two");
+      l_begin_level(opt->level_slots);
+    } else {  // level tier for this level: twice the expected new states
+      const unsigned long long est = (unsigned long long)((double)cur_n * rate * 1.25) + 1024;
+      unsigned long long ls = 1ULL << 16;
+      while (ls < 2 * est) ls <<= 1;
+      l_begin_level(ls);
+    }
     // the last k_materialize's snapshot (hrb->mat) is not examined yet; call
     // after a stream sync.  True when it ended the search (status 3 set, or
     // hst holds the error/violation keys).
@@ -757,68 +870,24 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       }
       return hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL;
     };
-    for (unsigned long long c0 = 0; c0 < cur_n; c0 += chunk) {
+    unsigned long long c0 = 0;
+    while (c0 < cur_n) {
       unsigned long long n = std::min(chunk, cur_n - c0);
-      // grow the table before it passes 1/2 load (worst case: every candidate
-      // new).  If HBM cannot hold the doubled table, carry on at up to 0.9 load.
-      const unsigned long long need = entries_hint + n * (unsigned long long)maxsucc;
-      if (need * 2 > slots && !table_full_ok) {
-        if (mat_pending) {  // the previous chunk may have ended the search: no growth for nothing
-          HIPCHK(hipStreamSynchronize(stream));
-          if (finish_mat()) break;
+      {  // room in the level tier for this chunk's new states (at the highest rate seen)
+        const double r = std::max(rate, c0 ? (double)next_n / (double)c0 : 0.0);
+        const unsigned long long needL = next_n + (unsigned long long)((double)n * r * 1.25) + 1024;
+        if (needL * 2 > lact && !opt->level_slots) {
+          if (mat_pending) {  // the previous chunk may have ended the search: no growth for nothing
+            HIPCHK(hipStreamSynchronize(stream));
+            if (finish_mat()) break;
+          }
+          unsigned long long nl = lact;
+          while (needL * 3 > nl) nl <<= 1;
+          l_grow(nl);
         }
-        unsigned long long nslots = slots;
-        while (need * 2 > nslots) nslots <<= 1;
-        if (opt->hash_slots) throw std::runtime_error("fingerprint set full (raise hash_slots)");
-        auto tr0 = now();
-        DevBuf& nt = A.table2;
-        bool grown = true;
-        try {
-          nt.ensure(nslots * 16);
-        } catch (OutOfDeviceMemory&) {
-          grown = false;
-        }
-        const double t_alloc = secs(tr0, now());
-        if (grown) {
-          HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
-          launch_rehash(table.as<unsigned long long>(), slots, nt.as<unsigned long long>(), nslots - 1,
-                        stbuf.as<DevStatus>(), stream);
-          HIPCHK(hipGetLastError());
-          HIPCHK(hipStreamSynchronize(stream));
-          const double t_fill = secs(tr0, now()) - t_alloc;
-          std::swap(table.p, nt.p);
-          std::swap(table.bytes, nt.bytes);
-          slots = nslots;
-          if (nt.bytes >= (1ULL << 30)) nt.release();  // large searches need the HBM more than a spare table
-          if (opt->verbose)
-            fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (alloc %.3fs, fill+rehash %.3fs, free %.3fs)\n",
-                    __builtin_ctzll(slots), t_alloc, t_fill, secs(tr0, now()) - t_alloc - t_fill);
-        } else {
-          table_full_ok = true;
-          if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(slots));
-        }
-        rehash_s += secs(tr0, now());
       }
-      if (table_full_ok && need * 10 > slots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
       LevelArgs a;
-      memset(&a, 0, sizeof a);
-      a.model = &M;
-      a.frontier = cur + c0 * W;
-      a.nparents = n;
-      a.pbase = cur_base + c0;
-      a.level = level;
-      a.table = table.as<unsigned long long>();
-      a.mask = slots - 1;
-      a.cand_slot = cslot.as<unsigned long long>();
-      a.cand_ob = cob.as<uint32_t>();
-      a.cand_win = cwin.as<uint16_t>();
-      a.par_off = poff.as<uint32_t>();
-      a.par_n = pn.as<uint32_t>();
-      a.par_win = pwin.as<uint32_t>();
-      a.par_pos = ppos.as<uint32_t>();
-      a.counters = counters.as<unsigned long long>();
-      a.cand_cap = cand_cap;
-      a.st = stbuf.as<DevStatus>();
+      fill_args(a, c0, n, level);
       HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
       HIPCHK(hipEventRecord(te.a, stream));
       launch_expand(M.spec, M.N, a, stream);
@@ -845,23 +914,35 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       expand_launches++;
       HIPCHK(hipEventElapsedTime(&ms, te.b, tm.b));
       mark_ms += ms;
+      if (hst.cap_flags == (1u << E_CAP_LEVEL)) {
+        // the level tier filled up under this chunk: grow it and redo the
+        // chunk (its level-tier inserts are idempotent; the main tier and the
+        // next frontier were not touched)
+        l_grow(lact * 4);
+        const unsigned zero = 0;
+        HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, cap_flags), &zero, 4, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        redos++;
+        continue;
+      }
       if (hst.cap_flags) {
         int e = 0;
         while (!((hst.cap_flags >> e) & 1)) e++;
-        if (e == E_CAP_MSG && !opt->msg_cap_K && kmax < 120) {
+        if (e == E_CAP_MSG && !opt->msg_cap_K && M.kmax < 120) {
           // the caller re-runs with a larger message capacity
-          m->kmax_user = std::min(120u, kmax * 2);
+          m->kmax_user = std::min(120u, (uint32_t)M.kmax * 2);
           HIPCHK(hipStreamDestroy(stream));
           return 1;
         }
         static const char* names[] = {"", "", "log longer than the packed layout (5 entries)",
                                       "message capacity msg_cap_K exceeded", "message multiplicity > 7",
                                       "term > 15", "index field > 7", "successor buffer", "fingerprint set full",
-                                      "frontier capacity"};
+                                      "frontier capacity", "fingerprint set level tier full"};
         status = 3;
         message = std::string("capacity overflow: ") + names[e];
         break;
       }
+      chunk_log.push_back({c0, gen_lvl, next_n});
       unsigned long long W_chunk = (unsigned long long)hrb->lastpos + hrb->lastwin;
       for (int sg = 0; sg < 8; sg++) ncand += hrb->segc[16 * sg];
       gen_lvl += ncand;
@@ -901,7 +982,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       HIPCHK(hipMemcpyAsync(&hrb->mat, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
       mat_pending = true;
       next_n += W_chunk;
-      entries_hint += W_chunk;
+      c0 += n;
       if (hst.err_key != ~0ULL) {  // this chunk's expand hit an evaluation error: the search stops here
         HIPCHK(hipStreamSynchronize(stream));
         finish_mat();
@@ -912,6 +993,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       HIPCHK(hipStreamSynchronize(stream));
       finish_mat();
     }
+    const unsigned long long gen_before = generated, dist_before = distinct;
     generated += gen_lvl;
     distinct += next_n;
     if (next_n || gen_lvl) m->levels.push_back({gen_lvl, next_n});
@@ -930,11 +1012,25 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         status = 1;
         bad_key = hst.viol_key;
       }
+      stop_level = level;
+      stop_level_base = cur_base;
+      stop_level_n = cur_n;
+      stop_front = cur;
+      stop_gen_before = gen_before;
+      stop_dist_before = dist_before;
       cur_base += cur_n;
       cur_n = next_n;
       std::swap(cur, nxt);
       break;
     }
+    // this level's fingerprints join the main tier; the level tier is emptied
+    if (next_n) {
+      m_fit(distinct);
+      launch_merge(A.ltab.as<unsigned long long>(), lact, table.as<unsigned long long>(), mslots - 1,
+                   stbuf.as<DevStatus>(), stream);
+      HIPCHK(hipGetLastError());
+    }
+    rate = (double)next_n / (double)cur_n;
     cur_base += cur_n;
     cur_n = next_n;
     std::swap(cur, nxt);
@@ -943,10 +1039,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       (void)hipMemGetInfo(&fr, &tot);
       fprintf(stderr,
               "[rmc] depth %u: %llu new, %llu distinct, %llu generated, t=%.3fs (rehash %.3fs, grow %.3fs) "
-              "HBM GiB: table %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f\n",
+              "HBM GiB: fp-set %.1f+%.1f level tier %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f\n",
               depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s, table.bytes / 1073741824.0,
-              A.table2.bytes / 1073741824.0, fa.bytes / 1073741824.0, fb.bytes / 1073741824.0,
-              trp.bytes / 1073741824.0, trb.bytes / 1073741824.0, fr / 1073741824.0);
+              A.table2.bytes / 1073741824.0, A.ltab.bytes / 1073741824.0, A.ltab2.bytes / 1073741824.0,
+              fa.bytes / 1073741824.0, fb.bytes / 1073741824.0, trp.bytes / 1073741824.0, trb.bytes / 1073741824.0,
+              fr / 1073741824.0);
     }
   }
   } catch (OutOfDeviceMemory& oom) {
@@ -960,6 +1057,59 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     HIPCHK(hipDeviceSynchronize());
   }
   HIPCHK(hipStreamSynchronize(stream));
+  // ---- exact counts at the failing state.  TLC stops at the first violating
+  // (or erroring) state in its exploration order; the chunks run whole, so
+  // the failing chunk is expanded and marked again (its level-tier inserts are
+  // idempotent: the tier still holds this level's entries) and the counts are
+  // taken up to the failing candidate -- generated: every successor of the
+  // parents before it plus the failing parent's up to the failing one; distinct:
+  // the winners among those.  An evaluation error in Next drops the failing
+  // parent's successors (as the oracle's convention does).
+  if ((status == 1 || status == 2) && bad_key != ~0ULL && stop_front) {
+    const unsigned long long pg = bad_key >> 20, li = pg - stop_level_base;
+    const int ordv = (int)((bad_key >> 10) & 0x3FF);
+    const ChunkLog* cl = nullptr;
+    for (const ChunkLog& c : chunk_log)
+      if (c.c0 <= li) cl = &c;
+    if (cl && li < stop_level_n) {
+      const unsigned long long c0 = cl->c0, n = std::min(chunk, stop_level_n - c0);
+      uint32_t* save_cur = cur;
+      unsigned long long save_base = cur_base;
+      cur = const_cast<uint32_t*>(stop_front);
+      cur_base = stop_level_base;
+      LevelArgs a;
+      fill_args(a, c0, n, stop_level);
+      cur = save_cur;
+      cur_base = save_base;
+      HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
+      launch_expand(M.spec, M.N, a, stream);
+      HIPCHK(hipGetLastError());
+      launch_mark(a, stream);
+      HIPCHK(hipGetLastError());
+      std::vector<uint32_t> h_n(n), h_w(n);
+      HIPCHK(hipMemcpyAsync(h_n.data(), a.par_n, n * 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(h_w.data(), a.par_win, n * 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      const unsigned long long pl = li - c0;
+      unsigned long long g = cl->gen_before, d = cl->new_before;
+      for (unsigned long long p = 0; p < pl; p++) { g += h_n[p]; d += h_w[p]; }
+      if (!bad_is_parent_key) {  // the failing state itself is new: count up to and including it
+        uint32_t off = 0;
+        HIPCHK(hipMemcpy(&off, a.par_off + pl, 4, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> ob(h_n[pl]);
+        std::vector<uint16_t> win(h_n[pl]);
+        if (h_n[pl]) {
+          HIPCHK(hipMemcpy(ob.data(), a.cand_ob + off, h_n[pl] * 4, hipMemcpyDeviceToHost));
+          HIPCHK(hipMemcpy(win.data(), a.cand_win + off, h_n[pl] * 2, hipMemcpyDeviceToHost));
+        }
+        for (uint32_t k = 0; k < h_n[pl]; k++)
+          if ((int)(ob[k] >> 16) == ordv) { g += k + 1; d += win[k]; break; }
+      }
+      generated = stop_gen_before + g;
+      distinct = stop_dist_before + d;
+      if (!m->levels.empty()) m->levels.back() = {g, d};
+    }
+  }
   // ---- trace reconstruction: walk parent records, replay bindings on the host
   if (status == 1 || status == 2) {
     std::vector<std::pair<unsigned long long, int>> chain;  // (global state index or parent, binding)
@@ -984,6 +1134,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     std::reverse(binds.begin(), binds.end());
     replay_trace(m, binds, last_b, status, message, res);
   }
+  {
+    DevStatus fin;
+    HIPCHK(hipMemcpy(&fin, stbuf.p, sizeof fin, hipMemcpyDeviceToHost));
+    res->hidden_var_collisions = fin.hidden_coll;
+  }
   if (opt->verbose) {
     unsigned long long stp[8];
     read_stamps(stp);
@@ -993,9 +1148,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
               "(the same without inserts: %.1f%%); "
               "fingerprints %llu, with signature ties %llu, permutations hashed under ties %llu\n",
               100 * stp[0] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot, 100 * stp[7] / tot, stp[4], stp[5], stp[6]);
+    fprintf(stderr, "[rmc] level tier: up to 2^%d slots, %llu chunk redos; main tier 2^%d slots, load %.3f\n",
+            lmax ? __builtin_ctzll(lmax) : 0, redos, __builtin_ctzll(mslots), (double)distinct / (double)mslots);
   }
   HIPCHK(hipStreamDestroy(stream));
-  if (!opt->hash_slots) m->hint_slots = slots;
+  if (!opt->hash_slots) m->hint_slots = mslots;
   if (!opt->frontier_cap) m->hint_fcap = fcap;
   m->hint_trcap = trcap;
   res->generated = generated;
@@ -1009,7 +1166,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   res->mark_ms = mark_ms;
   res->materialize_ms = mat_ms;
   res->expand_launches = expand_launches;
-  res->hash_capacity = slots;
+  res->hash_capacity = mslots;
   res->max_msgs = hst.max_msgs;
   if (status == 0 && !opt->max_depth && !opt->msg_cap_K) m->hint_kmax = std::max(1u, hst.max_msgs);
   return 0;
@@ -1258,6 +1415,12 @@ void rmc_release_device_memory(void) {
     if (hipSetDevice(kv.first) == hipSuccess) kv.second->release();
   }
   (void)hipSetDevice(cur);
+}
+
+// Test hook only: the row packing the next check of m starts from (as if its
+// last complete check had materialized at most k messages per state).
+void rmc_selftest_set_hint_kmax(rmc_model* m, uint32_t k) {
+  if (m) m->hint_kmax = k;
 }
 
 // Test hook only (never called by rmc_check): a seeded random walk of at most

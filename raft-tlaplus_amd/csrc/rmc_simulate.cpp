@@ -83,8 +83,8 @@ static int simulate_impl(rmc_model* m, const rmc_options* opt, unsigned long lon
     if (hst.cap_flags) {
       int e = 0;
       while (!((hst.cap_flags >> e) & 1)) e++;
-      if (e == E_CAP_MSG && !opt->msg_cap_K && kmax < 120) {
-        m->kmax_user = std::min(120u, kmax * 2);
+      if (e == E_CAP_MSG && !opt->msg_cap_K && M.kmax < 120) {
+        m->kmax_user = std::min(120u, (uint32_t)M.kmax * 2);
         HIPCHK(hipStreamDestroy(stream));
         return 1;
       }

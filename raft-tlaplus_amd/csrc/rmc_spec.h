@@ -58,7 +58,8 @@ enum ErrCode {
   E_CAP_FIELD = 6,  // an index field > 7
   E_CAP_SUCC = 7,   // more successors for one state than the candidate buffer holds
   E_CAP_TABLE = 8,  // fingerprint set full
-  E_CAP_FRONTIER = 9
+  E_CAP_FRONTIER = 9,
+  E_CAP_LEVEL = 10   // fingerprint set: level tier full (the driver grows it and redoes the chunk)
 };
 constexpr int NILS = 7;
 constexpr int MAXN = 7, MAXV = 4, MAXLOG = 5, MAXOPS = 7, MAXPERM = 120, MAXACT = 16, MAXFIXED = 192;
@@ -97,6 +98,11 @@ RMC_HD int a_commit(uint32_t a) { return (int)getb(a, 12, 3); }
 RMC_HD int a_fsync(uint32_t a) { return (int)getb(a, 15, 3); }
 RMC_HD int a_votes(uint32_t a) { return (int)getb(a, 18, 7); }
 RMC_HD int a_pending(uint32_t a) { return (int)getb(a, 25, 7); }
+// The variables VIEW drops, from a header word (16 bits): electionCtr,
+// restartCtr and acked (Raft.tla:115, FlexibleRaft.tla:117, RaftFsync.tla:117);
+// PullRaft's view keeps acked, so only the counters (PullRaft.tla:123).
+template <int SPEC>
+RMC_HD uint32_t hidden_of(uint32_t h) { return SPEC == 3 /* PULL */ ? (h >> 8) & 0xFFu : (h >> 8) & 0xFFFFu; }
 // log word B
 RMC_HD int e_term(uint32_t b, int x) { return (int)getb(b, 6 * x, 4); }
 RMC_HD int e_value(uint32_t b, int x) { return (int)getb(b, 6 * x + 4, 2); }

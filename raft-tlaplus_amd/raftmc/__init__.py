@@ -29,7 +29,7 @@ class Options(ctypes.Structure):
                 ("tlc_order", ctypes.c_int), ("hash_slots", ctypes.c_uint64),
                 ("msg_cap_K", ctypes.c_uint32), ("frontier_cap", ctypes.c_uint64),
                 ("chunk_parents", ctypes.c_uint32), ("verbose", ctypes.c_int),
-                ("max_depth", ctypes.c_int)]
+                ("max_depth", ctypes.c_int), ("level_slots", ctypes.c_uint64)]
 
 
 class Result(ctypes.Structure):
@@ -86,6 +86,7 @@ def lib():
     L.rmc_trace_module.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t]
     L.rmc_trace_json.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_selftest_random_trace.argtypes = [P, ctypes.c_uint64, c_int]
+    L.rmc_selftest_set_hint_kmax.argtypes = [P, ctypes.c_uint32]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
     _lib = L
     return L
@@ -113,13 +114,14 @@ class Model:
             self._h = None
 
     def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
-                 chunk_parents=0, verbose=False, max_depth=0, workers=0):
+                 chunk_parents=0, verbose=False, max_depth=0, workers=0, level_slots=0):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
         o.deadlock_check = 1 if deadlock else 0
         o.hash_slots, o.msg_cap_K, o.frontier_cap = hash_slots, msg_cap_K, frontier_cap
         o.chunk_parents, o.verbose, o.max_depth, o.cpu_workers = chunk_parents, int(verbose), max_depth, workers
+        o.level_slots = level_slots
         return o
 
     def _result(self, rc, r):
@@ -134,6 +136,7 @@ class Model:
                    seconds=r.seconds, expand_ms=r.expand_ms, mark_ms=r.mark_ms,
                    materialize_ms=r.materialize_ms, expand_launches=r.expand_launches,
                    state_bytes=r.state_bytes, hash_capacity=r.hash_capacity, max_msgs=r.max_msgs,
+                   hidden_var_collisions=r.hidden_var_collisions,
                    levels=[[levels[2 * k], levels[2 * k + 1]] for k in range(min(nl, 1024))])
         self._last = r
         if r.status in (1, 2):
@@ -215,6 +218,11 @@ class Model:
         buf = ctypes.create_string_buffer(1 << 22)
         L.rmc_format_report(self._h, ctypes.byref(self._last), buf, len(buf))
         return buf.value.decode()
+
+    def selftest_set_hint_kmax(self, k):
+        """TEST HOOK: pretend the last check saw at most k messages per state, so the
+        next check packs rows to k slots (an overflow must take the re-run path)."""
+        lib().rmc_selftest_set_hint_kmax(self._h, int(k))
 
     def selftest_host_bfs(self, kmax=0, max_distinct=0):
         """TEST HOOK: sequential host BFS over the same lowered actions (not a product path)."""

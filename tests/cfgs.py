@@ -82,3 +82,16 @@ UNSAFE = [
     ("flex_n3v1e2_q1", "FlexibleRaft", dict(n=3, v=1, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=1)),
     ("flex_n3v2e2_eq1", "FlexibleRaft", dict(n=3, v=2, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=2)),
 ]
+
+# TLC-order first-wins sensitivity (SURVEY.md §7 hard part 1): configs with
+# same-level hidden-variable collisions (VIEW drops acked/electionCtr/restartCtr
+# which gate actions).  For the first three, letting the LAST successor in TLC
+# order win (the C oracle's --reverse-order probe) changes the counts, so only
+# the first-in-TLC-order winner reproduces them.
+ORDER = [
+    ("fsync_n2v1e3_order", "RaftFsync", dict(n=2, v=1, E=3, R=0)),
+    ("raft_n2v2e2r2_order", "Raft", dict(n=2, v=2, E=2, R=2)),
+    ("fsync_n2v1e3r1_order", "RaftFsync", dict(n=2, v=1, E=3, R=1)),
+    ("fsync_n2v2e1r1_hidden", "RaftFsync", dict(n=2, v=2, E=1, R=1)),
+    ("fsync_n2v2e2r1_hidden", "RaftFsync", dict(n=2, v=2, E=2, R=1)),
+]

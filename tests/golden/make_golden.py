@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import MEDIUM, N5, N5_UNSAFE, SMALL, UNSAFE, cfg_text  # noqa: E402
+from cfgs import MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, cfg_text  # noqa: E402
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
     ("Raft_cfg", "Raft", "configs/Raft.cfg"),
@@ -79,7 +79,37 @@ def n5():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def order():
+    """--order: TLC-order first-wins fixtures (cfgs.ORDER).  Both oracles where the
+    Python one finishes in minutes; the C oracle's --reverse-order counts are
+    recorded beside them (different counts = the winner choice matters)."""
+    out = {}
+    for name, module, kw in ORDER:
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=4)
+        rv = run_c.run(module, cfg["constants"], cfg["invariants"], threads=1, extra=["--reverse-order"])
+        pinned = "coracle"
+        if c["distinct"] <= 400000:
+            p = bfs(make_spec(module, cfg))
+            pr = (p.generated, p.distinct, p.depth, p.status, [list(x) for x in p.levels], p.hidden_same_level)
+            cr = (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"], c["hidden_same_level"])
+            if pr != cr:
+                raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pr[:4] + pr[5:], cr[:4] + cr[5:]))
+            pinned = "pyoracle==coracle"
+        out[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], levels=c["levels"], max_msgs=c["max_msgs"],
+                         hidden_same_level=c["hidden_same_level"], hidden_cross_level=c["hidden_cross_level"],
+                         reverse_order=dict(generated=rv["generated"], distinct=rv["distinct"]), pinned_by=pinned)
+        print(name, c["generated"], c["distinct"], c["hidden_same_level"], "reverse:", rv["generated"], rv["distinct"],
+              pinned, flush=True)
+    with open(os.path.join(HERE, "order.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--order" in sys.argv:
+        return order()
     if "--shipped-one" in sys.argv:
         return shipped()
     if "--unsafe" in sys.argv:

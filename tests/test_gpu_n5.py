@@ -32,7 +32,9 @@ def levels_match(r, g):
 def test_n5_levels_match_oracle(name):
     g = N5[name]
     m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
-    levels_match(m.check(max_depth=0 if g["status"] == "ok" else g["depth"]), g)
+    r = m.check(max_depth=0 if g["status"] == "ok" else g["depth"])
+    levels_match(r, g)
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
 
 
 @pytest.mark.parametrize("name", CASES[:3])
@@ -60,3 +62,5 @@ def test_n5_unsafe_violation(name):
     assert r["status"] == "violation" and r["violated"] == g["violated"]
     assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]
     assert r["trace"][0][0] == "Initial predicate"
+    assert (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])
+    assert r["levels"] == g["levels"]

@@ -28,6 +28,7 @@ def test_small_configs_match_oracle(name):
     assert r["status"] == g["status"]
     assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
     assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
 
 
 @pytest.mark.parametrize("name", sorted(SMALL)[:3])
@@ -39,14 +40,6 @@ def test_tiny_chunks_and_table_growth(name):
     assert r["levels"] == g["levels"]
 
 
-def test_message_capacity_regrow():
-    """A message capacity far too small triggers the automatic re-run with a larger one."""
-    g = SMALL["raft_n3v1e1"]
-    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
-    r = m.check(msg_cap_K=0)
-    assert r["distinct"] == g["distinct"]
-
-
 @pytest.mark.parametrize("name", sorted(SHIPPED))
 def test_shipped_configs_match_oracle(name):
     g = SHIPPED[name]
@@ -54,6 +47,7 @@ def test_shipped_configs_match_oracle(name):
     assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
     assert r["levels"] == g["levels"]
     assert r["status"] == "ok"
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
 
 
 @pytest.mark.parametrize("name", sorted(SHIPPED))
@@ -97,31 +91,39 @@ def test_medium_configs_match_oracle(name):
     r = raftmc.check_text(g["module"], g["cfg"])
     assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
     assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
 
 
 @pytest.mark.parametrize("name", sorted(k for k in MEDIUM if MEDIUM[k]["status"] == "violation"))
-def test_violation_found_with_trace(name):
+@pytest.mark.parametrize("chunk", [0, 1000])
+def test_violation_found_with_trace(name, chunk):
     """An unsafe config (RaftFsync.tla:14-24 policy) must report the same
-    invariant, at the same depth, with a behaviour that starts at Init."""
+    invariant, at the same depth, with a behaviour that starts at Init, and
+    TLC's counts at the first violating state in TLC order (Appendix A.7: the
+    counts at a violation are comparable in TLC order)."""
     g = MEDIUM[name]
-    r = raftmc.check_text(g["module"], g["cfg"])
+    r = raftmc.check_text(g["module"], g["cfg"], chunk_parents=chunk)
     assert r["status"] == "violation"
     assert r["violated"] == g["violated"]
     tr = r["trace"]
     assert tr[0][0] == "Initial predicate"
     assert len(tr) == g["trace_len"]
+    assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
+    assert r["levels"] == g["levels"]
 
 
 UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
 
 
 @pytest.mark.parametrize("name", sorted(UNSAFE))
-def test_unsafe_flexible_violation(name):
-    """Non-intersecting Flexible quorums: same invariant, same depth and a
-    trace of the oracle's length (counts at a violation depend on how much of
-    the level was expanded, so they are not compared)."""
+@pytest.mark.parametrize("chunk", [0, 9])
+def test_unsafe_flexible_violation(name, chunk):
+    """Non-intersecting Flexible quorums: same invariant, same depth, a trace of
+    the oracle's length, and the oracle's counts at the first violating state
+    in TLC order."""
     g = UNSAFE[name]
-    r = raftmc.check_text(g["module"], g["cfg"])
+    r = raftmc.check_text(g["module"], g["cfg"], chunk_parents=chunk)
     assert r["status"] == "violation" and r["violated"] == g["violated"]
     assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]
     assert r["trace"][0][0] == "Initial predicate"
+    assert (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])
