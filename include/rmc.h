@@ -49,8 +49,9 @@ typedef struct {
   uint32_t chunk_parents; /* parents expanded per launch; 0 = auto */
   int verbose;         /* per-level progress on stderr */
   int max_depth;       /* stop after this many levels (0 = exhaustive) */
-  uint64_t level_slots; /* tuning/test: level-tier slots at every level start, no pre-chunk growth, so an
-                           overflow takes the grow-and-redo path (power of two; 0 = auto) */
+  int grow_on_overflow; /* test: no fingerprint-set growth ahead of a chunk; a chunk that overflows the set
+                           grows it and is redone (the safety net behind the pre-sizing) */
+  double time_limit;    /* stop (status 4) at the first level boundary after this many seconds (0 = none) */
 } rmc_options;
 
 typedef struct {
@@ -120,6 +121,10 @@ int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result
  * rmc_check.  The same seed gives the same run. */
 int rmc_simulate(rmc_model* m, const rmc_options* o, uint64_t walkers, uint32_t depth, uint64_t seed,
                  uint64_t behaviors, double seconds, rmc_result* out);
+/* The CPU engine: TLC's -workers N on host threads (o->cpu_workers; 0 = every hardware thread), over the
+ * same packed layout, lowered actions, fingerprint and first-in-TLC-order rule as rmc_check, with the same
+ * results.  Explicitly requested (raftmc -cpu); rmc_check never falls back to it.  BASELINE.md's CPU baseline. */
+int rmc_check_cpu(rmc_model* m, const rmc_options* o, rmc_result* out);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
 int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
 

@@ -571,16 +571,14 @@ struct HostReadback {
   DevStatus mat;                 // status after the chunk's k_materialize
 };
 struct Arena {
-  // table/table2: fingerprint set main tier (8 B keys) and its growth target;
-  // ltab/ltab2: level tier (16 B (fp, val) entries) and its growth target
-  DevBuf table, table2, ltab, ltab2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  // table/table2: the fingerprint set and its growth target
+  DevBuf table, table2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   HostReadback* hrb = nullptr;
   void release() {
     if (hrb) (void)hipHostFree(hrb);
     hrb = nullptr;
-    for (DevBuf* b : {&table, &table2, &ltab, &ltab2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
-                      &scantmp})
+    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
       b->release();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
@@ -644,12 +642,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   res->state_bytes = (uint32_t)(W * 4);
 
   // ---- sizing
-  // Fingerprint set, main tier: starts at hash_slots (or at the size the last
-  // check of this model ended with -- TLC's preallocated FPSet, -fpmem, in
-  // spirit) and doubles at level ends past 0.6 load.  The level tier is sized
-  // per level from the previous level's growth (below).
-  unsigned long long mslots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 24, m->hint_slots);
-  if (mslots & (mslots - 1)) throw std::runtime_error("hash_slots must be a power of two");
+  // Fingerprint set: starts at hash_slots (or at the size the last check of
+  // this model ended with -- TLC's preallocated FPSet, -fpmem, in spirit) and
+  // doubles before a chunk whose new states could take it past 0.75 load.
+  unsigned long long slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 24, m->hint_slots);
+  if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
   const int maxsucc = M.nfixed + M.kmax;
   // 4M parents per launch: 4% less k_expand time than 2M on the bench cfg (2M: 4% less than 1M)
@@ -668,8 +665,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   DevBuf &poff = A.poff, &pn = A.pn, &pwin = A.pwin, &ppos = A.ppos, &counters = A.counters, &stbuf = A.stbuf;
   DevBuf& scantmp = A.scantmp;
   GrowBuf &fa = A.fa, &fb = A.fb, &trp = A.trp, &trb = A.trb;
-  table.ensure(mslots * 8);
-  HIPCHK(hipMemsetAsync(table.p, 0xFF, mslots * 8, stream));
+  table.ensure(slots * 16);
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * 16, stream));
   fa.ensure(fcap * W * 4);
   fb.ensure(fcap * W * 4);
   cslot.ensure(cand_cap * 8);
@@ -705,71 +702,44 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   };
   double rehash_s = 0, grow_s = 0;
 
-  // ---- level tier: [0, lclean) of A.ltab is known empty; lact = slots in use
-  // this level (a power of two).  k_merge empties the used slots at each level
-  // end, so only the growth of the used range is ever cleared by a memset.
-  unsigned long long lact = 0, lclean = 0, lmax = 0;
-  auto l_begin_level = [&](unsigned long long slots) {  // the tier is empty between levels
-    if (A.ltab.bytes < slots * 16) {
-      A.ltab.ensure(slots * 16);
-      HIPCHK(hipMemsetAsync(A.ltab.p, 0xFF, A.ltab.bytes, stream));
-      lclean = A.ltab.bytes / 16;
-    } else if (lclean < slots) {
-      HIPCHK(hipMemsetAsync(A.ltab.as<unsigned long long>() + 2 * lclean, 0xFF, (slots - lclean) * 16, stream));
-      lclean = slots;
-    }
-    lact = slots;
-    lmax = std::max(lmax, lact);
-  };
-  auto l_grow = [&](unsigned long long nslots) {  // mid-level: rehash the level's entries into nslots
-    auto tg0 = now();
+  // ---- growth: room for `need` entries at <= 0.75 load (0.9 once HBM is full)
+  bool full_ok = false;
+  unsigned long long grows = 0;
+  auto t_grow = [&](unsigned long long nslots) {  // rehash into nslots (entries and values kept)
+    auto tr0 = now();
     HIPCHK(hipStreamSynchronize(stream));
-    A.ltab2.ensure(nslots * 16);
-    HIPCHK(hipMemsetAsync(A.ltab2.p, 0xFF, nslots * 16, stream));
-    launch_rehash(A.ltab.as<unsigned long long>(), lact, A.ltab2.as<unsigned long long>(), nslots - 1,
+    bool grown = true;
+    try {
+      A.table2.ensure(nslots * 16);
+    } catch (OutOfDeviceMemory&) {
+      grown = false;
+    }
+    if (!grown) return false;
+    HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * 16, stream));
+    launch_rehash(table.as<unsigned long long>(), slots, A.table2.as<unsigned long long>(), nslots - 1,
                   stbuf.as<DevStatus>(), stream);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(stream));
-    std::swap(A.ltab.p, A.ltab2.p);
-    std::swap(A.ltab.bytes, A.ltab2.bytes);
-    if (A.ltab2.bytes >= (1ULL << 30)) A.ltab2.release();  // large searches need the HBM more than a spare
-    lclean = lact = nslots;
-    lmax = std::max(lmax, lact);
-    rehash_s += secs(tg0, now());
-    if (opt->verbose) fprintf(stderr, "[rmc] level tier grown to 2^%d slots\n", __builtin_ctzll(nslots));
+    std::swap(table.p, A.table2.p);
+    std::swap(table.bytes, A.table2.bytes);
+    slots = nslots;
+    if (A.table2.bytes >= (1ULL << 30)) A.table2.release();  // large searches need the HBM more than a spare
+    grows++;
+    rehash_s += secs(tr0, now());
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs)\n", __builtin_ctzll(slots), secs(tr0, now()));
+    return true;
   };
-  // ---- main tier: room for `need` keys at <= 0.6 load (0.9 once HBM is full)
-  bool mfull_ok = false;
-  auto m_fit = [&](unsigned long long need) {
-    if (need * 5 <= mslots * 3) return;
-    if (!mfull_ok) {
-      unsigned long long nslots = mslots;
-      while (need * 5 > nslots * 3) nslots <<= 1;
-      auto tr0 = now();
-      try {
-        A.table2.ensure(nslots * 8);
-      } catch (OutOfDeviceMemory&) {
-        mfull_ok = true;
-      }
-      if (!mfull_ok) {
-        HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * 8, stream));
-        launch_rehash_main(table.as<unsigned long long>(), mslots, A.table2.as<unsigned long long>(), nslots - 1,
-                           stbuf.as<DevStatus>(), stream);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(stream));
-        std::swap(table.p, A.table2.p);
-        std::swap(table.bytes, A.table2.bytes);
-        mslots = nslots;
-        if (A.table2.bytes >= (1ULL << 30)) A.table2.release();
-        rehash_s += secs(tr0, now());
-        if (opt->verbose)
-          fprintf(stderr, "[rmc] fingerprint set (main tier) grown to 2^%d slots (%.3fs)\n", __builtin_ctzll(mslots),
-                  secs(tr0, now()));
-        return;
-      }
-      if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(mslots));
+  auto t_fit = [&](unsigned long long need) {
+    if (need * 4 <= slots * 3) return;
+    if (!full_ok) {
+      unsigned long long nslots = slots;
+      while (need * 2 > nslots) nslots <<= 1;  // to <= 0.5 after growing
+      if (t_grow(nslots)) return;
+      full_ok = true;
+      if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(slots));
     }
-    if (need * 10 > mslots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
+    if (need * 10 > slots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
   };
 
   // ---- level 1: Init (Raft.tla:213-218)
@@ -778,7 +748,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   {
     unsigned long long fp = host_fingerprint(M, init.data());
     if (fp == ~0ULL) fp--;
-    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + fp_slot(fp, mslots - 1), &fp, 8, hipMemcpyHostToDevice, stream));
+    const unsigned long long ent[2] = {fp, 0ULL};  // val 0: older than every successor
+    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + 2 * fp_slot(fp, slots - 1), ent, 16, hipMemcpyHostToDevice,
+                          stream));
     unsigned long long root = ~0ULL;
     uint16_t zero = 0;
     HIPCHK(hipMemcpyAsync(trp.p, &root, 8, hipMemcpyHostToDevice, stream));
@@ -807,7 +779,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   unsigned long long expand_launches = 0, redos = 0;
   uint32_t* cur = fa.as<uint32_t>();
   uint32_t* nxt = fb.as<uint32_t>();
-  double rate = 4.0;  // new states per parent of the previous level (sizes the level tier)
+  double rate = 4.0;  // new states per parent of the previous level (pre-sizes the table per chunk)
   // the level that stopped the search (exact counts at the failing state, below)
   struct ChunkLog { unsigned long long c0, gen_before, new_before; };
   std::vector<ChunkLog> chunk_log;
@@ -821,10 +793,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     a.nparents = n;
     a.pbase = cur_base + c0;
     a.level = level;
-    a.mkeys = table.as<unsigned long long>();
-    a.mmask = mslots - 1;
-    a.table = A.ltab.as<unsigned long long>();
-    a.mask = lact - 1;
+    a.floor = (cur_base + 1) << VAL_FLOOR_SHIFT;
+    a.table = table.as<unsigned long long>();
+    a.mask = slots - 1;
     a.cand_slot = cslot.as<unsigned long long>();
     a.cand_ob = cob.as<uint32_t>();
     a.cand_win = cwin.as<uint16_t>();
@@ -841,18 +812,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
-    if (cur_base + cur_n >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
+    if (cur_base + cur_n + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
     unsigned long long next_n = 0, gen_lvl = 0;
     chunk_log.clear();
-    if (opt->level_slots) {  // fixed start, growth only through the overflow-and-redo path
-      if (opt->level_slots & (opt->level_slots - 1)) throw std::runtime_error("level_slots must be a power of two");
-      l_begin_level(opt->level_slots);
-    } else {  // level tier for this level: twice the expected new states
-      const unsigned long long est = (unsigned long long)((double)cur_n * rate * 1.25) + 1024;
-      unsigned long long ls = 1ULL << 16;
-      while (ls < 2 * est) ls <<= 1;
-      l_begin_level(ls);
-    }
     // the last k_materialize's snapshot (hrb->mat) is not examined yet; call
     // after a stream sync.  True when it ended the search (status 3 set, or
     // hst holds the error/violation keys).
@@ -873,17 +835,15 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     unsigned long long c0 = 0;
     while (c0 < cur_n) {
       unsigned long long n = std::min(chunk, cur_n - c0);
-      {  // room in the level tier for this chunk's new states (at the highest rate seen)
+      if (!opt->grow_on_overflow) {  // room for this chunk's new states (at the highest rate seen)
         const double r = std::max(rate, c0 ? (double)next_n / (double)c0 : 0.0);
-        const unsigned long long needL = next_n + (unsigned long long)((double)n * r * 1.25) + 1024;
-        if (needL * 2 > lact && !opt->level_slots) {
+        const unsigned long long need = distinct + next_n + (unsigned long long)((double)n * r * 1.25) + 1024;
+        if (need * 4 > slots * 3) {
           if (mat_pending) {  // the previous chunk may have ended the search: no growth for nothing
             HIPCHK(hipStreamSynchronize(stream));
             if (finish_mat()) break;
           }
-          unsigned long long nl = lact;
-          while (needL * 3 > nl) nl <<= 1;
-          l_grow(nl);
+          t_fit(need);
         }
       }
       LevelArgs a;
@@ -914,11 +874,15 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       expand_launches++;
       HIPCHK(hipEventElapsedTime(&ms, te.b, tm.b));
       mark_ms += ms;
-      if (hst.cap_flags == (1u << E_CAP_LEVEL)) {
-        // the level tier filled up under this chunk: grow it and redo the
-        // chunk (its level-tier inserts are idempotent; the main tier and the
-        // next frontier were not touched)
-        l_grow(lact * 4);
+      if (hst.cap_flags == (1u << E_CAP_TABLE) && !full_ok) {
+        // the table filled up under this chunk: grow it and redo the chunk
+        // (its inserts are idempotent; the next frontier was not touched)
+        if (!t_grow(slots * 2)) {
+          full_ok = true;
+          status = 3;
+          message = "capacity overflow: fingerprint set full and HBM exhausted";
+          break;
+        }
         const unsigned zero = 0;
         HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, cap_flags), &zero, 4, hipMemcpyHostToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
@@ -937,7 +901,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         static const char* names[] = {"", "", "log longer than the packed layout (5 entries)",
                                       "message capacity msg_cap_K exceeded", "message multiplicity > 7",
                                       "term > 15", "index field > 7", "successor buffer", "fingerprint set full",
-                                      "frontier capacity", "fingerprint set level tier full"};
+                                      "frontier capacity"};
         status = 3;
         message = std::string("capacity overflow: ") + names[e];
         break;
@@ -1023,13 +987,6 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       std::swap(cur, nxt);
       break;
     }
-    // this level's fingerprints join the main tier; the level tier is emptied
-    if (next_n) {
-      m_fit(distinct);
-      launch_merge(A.ltab.as<unsigned long long>(), lact, table.as<unsigned long long>(), mslots - 1,
-                   stbuf.as<DevStatus>(), stream);
-      HIPCHK(hipGetLastError());
-    }
     rate = (double)next_n / (double)cur_n;
     cur_base += cur_n;
     cur_n = next_n;
@@ -1039,10 +996,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       (void)hipMemGetInfo(&fr, &tot);
       fprintf(stderr,
               "[rmc] depth %u: %llu new, %llu distinct, %llu generated, t=%.3fs (rehash %.3fs, grow %.3fs) "
-              "HBM GiB: fp-set %.1f+%.1f level tier %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f\n",
+              "HBM GiB: fp-set %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f\n",
               depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s, table.bytes / 1073741824.0,
-              A.table2.bytes / 1073741824.0, A.ltab.bytes / 1073741824.0, A.ltab2.bytes / 1073741824.0,
-              fa.bytes / 1073741824.0, fb.bytes / 1073741824.0, trp.bytes / 1073741824.0, trb.bytes / 1073741824.0,
+              A.table2.bytes / 1073741824.0, fa.bytes / 1073741824.0, fb.bytes / 1073741824.0, trp.bytes / 1073741824.0, trb.bytes / 1073741824.0,
               fr / 1073741824.0);
     }
   }
@@ -1059,8 +1015,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   HIPCHK(hipStreamSynchronize(stream));
   // ---- exact counts at the failing state.  TLC stops at the first violating
   // (or erroring) state in its exploration order; the chunks run whole, so
-  // the failing chunk is expanded and marked again (its level-tier inserts are
-  // idempotent: the tier still holds this level's entries) and the counts are
+  // the failing chunk is expanded and marked again (its inserts are idempotent)
+  // and the counts are
   // taken up to the failing candidate -- generated: every successor of the
   // parents before it plus the failing parent's up to the failing one; distinct:
   // the winners among those.  An evaluation error in Next drops the failing
@@ -1148,11 +1104,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
               "(the same without inserts: %.1f%%); "
               "fingerprints %llu, with signature ties %llu, permutations hashed under ties %llu\n",
               100 * stp[0] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot, 100 * stp[7] / tot, stp[4], stp[5], stp[6]);
-    fprintf(stderr, "[rmc] level tier: up to 2^%d slots, %llu chunk redos; main tier 2^%d slots, load %.3f\n",
-            lmax ? __builtin_ctzll(lmax) : 0, redos, __builtin_ctzll(mslots), (double)distinct / (double)mslots);
+    fprintf(stderr, "[rmc] fingerprint set: 2^%d slots, load %.3f, %llu growths, %llu chunk redos\n",
+            __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);
   }
   HIPCHK(hipStreamDestroy(stream));
-  if (!opt->hash_slots) m->hint_slots = mslots;
+  if (!opt->hash_slots) m->hint_slots = slots;
   if (!opt->frontier_cap) m->hint_fcap = fcap;
   m->hint_trcap = trcap;
   res->generated = generated;
@@ -1166,7 +1122,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   res->mark_ms = mark_ms;
   res->materialize_ms = mat_ms;
   res->expand_launches = expand_launches;
-  res->hash_capacity = mslots;
+  res->hash_capacity = slots;
   res->max_msgs = hst.max_msgs;
   if (status == 0 && !opt->max_depth && !opt->msg_cap_K) m->hint_kmax = std::max(1u, hst.max_msgs);
   return 0;

@@ -29,12 +29,12 @@ struct LevelArgs {
   const uint32_t* frontier;
   unsigned long long nparents, pbase;
   unsigned level;  // level of the successors (parents are level-1)
-  const unsigned long long* mkeys;  // fingerprint set, main tier (earlier levels; read-only here)
-  unsigned long long mmask;
-  unsigned long long* table;        // fingerprint set, level tier (this level's (fp, val) entries)
+  unsigned long long floor;  // (first global index of the parents' level) << 26: entries below are older
+  int sharded;               // 1: k_expand leaves the fingerprint-set insert to the fp's owner
+  unsigned long long* table;  // fingerprint set: (fp, val) entries
   unsigned long long mask;
-  unsigned long long* cand_slot;  // single shard: CAND_DUP or hidden|L slot; sharded: the candidate's fp
-  unsigned long long* cand_val;   // sharded only (else nullptr): the candidate's (level, parent, ordinal) key
+  unsigned long long* cand_slot;  // single shard: CAND_DUP or hidden << 47 | slot; sharded: the candidate's fp
+  unsigned long long* cand_val;   // sharded: the candidate's TLC-order rank << 16 | hidden variables (rmc_fpset.h)
   uint32_t* cand_ob;
   uint16_t* cand_win;
   uint32_t *par_off, *par_n, *par_win, *par_pos;
@@ -52,11 +52,7 @@ void launch_mark(const LevelArgs& a, hipStream_t s);
 void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s);
 void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
                    unsigned long long nmask, DevStatus* st, hipStream_t s);
-// main tier: move (and clear) the level tier's nl entries into M; rehash M into a larger M
-void launch_merge(unsigned long long* L, unsigned long long nl, unsigned long long* M, unsigned long long mmask,
-                  DevStatus* st, hipStream_t s);
-void launch_rehash_main(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
-                        unsigned long long nmask, DevStatus* st, hipStream_t s);
+
 size_t scan_temp_bytes(unsigned long long n);
 void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
                  hipStream_t s);
@@ -70,12 +66,12 @@ void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_
 void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
                    unsigned long long n, int W, const unsigned int* blk_off, unsigned long long* send, uint32_t* perm,
                    hipStream_t s);
-void launch_insert_recv(const unsigned long long* recv, unsigned long long n, const unsigned long long* mkeys,
-                        unsigned long long mmask, unsigned long long* table, unsigned long long mask,
-                        unsigned long long* recv_slot, DevStatus* st, hipStream_t s);
+void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
+                        unsigned long long mask, unsigned long long floor, unsigned long long* recv_slot, DevStatus* st,
+                        hipStream_t s);
 void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
-                      const unsigned long long* table, uint8_t* flag, unsigned long long* newcount, DevStatus* st,
-                      hipStream_t s);
+                      const unsigned long long* table, unsigned long long floor, uint8_t* flag,
+                      unsigned long long* newcount, DevStatus* st, hipStream_t s);
 void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
                      const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s);
 int host_fp_owner(unsigned long long fp, int W);

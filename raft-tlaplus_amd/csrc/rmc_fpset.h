@@ -2,21 +2,22 @@
 // shared by the BFS kernels (rmc_kernels.hip) and the insert microbenchmark
 // (rmc_fpset_bench.hip).
 //
-// Two tiers:
-//   main  M: the fingerprints of every COMPLETED level.  8 B keys, open
-//            addressing, linear probing.  Read-only while a level is
-//            expanded, so the 70% of successors that are duplicates of older
-//            states cost one plain (non-atomic, never-dirtying) probe.
-//   level L: the fingerprints first seen in the CURRENT level, 16 B entries
-//            (fp, val) with val = parent global index << 26 | ordinal << 16 |
-//            hidden.  atomicMin on val keeps the successor first in TLC order
-//            (parent position in the level, then the action's ordinal in Next:
-//            TLC -workers 1 first-wins under VIEW, SURVEY.md §7 hard part 1);
-//            hidden = the variables VIEW drops (electionCtr, restartCtr, acked;
-//            Pull: the counters), carried so losers can count same-level
-//            hidden-variable collisions.
-// At the end of a level k_merge moves L's keys into M and L is cleared.  Empty
-// slots hold ~0 (a fingerprint of ~0 is mapped to ~0 - 1 by canon_from_sums).
+// Open addressing, linear probing, 16 B entries (fp, val), empty = both ~0.
+//   val = rank << 16 | hidden,  rank = (parent global index + 1) << 10 | ordinal
+// rank orders successors as TLC -workers 1 generates them (parent position in
+// BFS order, then the action's ordinal in Next); atomicMin on val keeps the
+// first one (TLC's first-wins under VIEW, SURVEY.md §7 hard part 1).  hidden =
+// the variables VIEW drops (electionCtr, restartCtr, acked; Pull: the
+// counters), carried so that same-level losers can count hidden-variable
+// collisions.  The initial state's val is 0, below every rank.
+//
+// No level field is needed: parents of level L+1's states are level L's, and
+// global indices grow level by level, so an entry is from an EARLIER level iff
+// its val < floor = (first global index of the parents' level + 1) << 26.  An
+// insert that finds its fingerprint from an earlier level (most successors:
+// 72% on the bench workload) therefore leaves the entry untouched -- one CAS
+// that fails (and a read of the same, L2-resident line) and no write -- and
+// only new fingerprints and same-level duplicates pay the atomicMin.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "rmc_engine.h"
@@ -24,71 +25,93 @@
 namespace rmc {
 
 constexpr unsigned long long EMPTY = ~0ULL;
-// candidate slot word: bit 63 = found in M (a state of an earlier level);
-// else hidden << 47 | L slot
+// candidate slot word: CAND_DUP = no entry (error / failed insert); else
+// hidden << 47 | slot
 constexpr unsigned long long CAND_DUP = 1ULL << 63;
 constexpr unsigned long long CAND_SLOT_MASK = (1ULL << 47) - 1;
-constexpr int VAL_RANK_SHIFT = 16;  // val = rank << 16 | hidden; rank = pg << 10 | ordinal
+constexpr int VAL_RANK_SHIFT = 16;   // val = rank << 16 | hidden
+constexpr int VAL_FLOOR_SHIFT = 26;  // floor = (global index + 1) << 26 (rank << 16 with ordinal 0)
 
+// Home slot: the TOP bits of fp times an odd constant (a bijection, so as
+// uniform as fp, and independent of fp_owner's raw high word).  With top bits
+// a key's home slot in a table of 2^a slots is the prefix of its home slot in
+// one of 2^b >= 2^a slots, so a rehash into a larger table walks the new table
+// in address order.
 __host__ __device__ __forceinline__ unsigned long long fp_slot(unsigned long long fp, unsigned long long mask) {
-  return (fp ^ (fp >> 29)) & mask;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int sh = __clzll((long long)mask);
+#else
+  const int sh = __builtin_clzll(mask);
+#endif
+  return ((fp * 0x9E3779B97F4A7C15ULL) >> sh) & mask;
 }
 
-// Is fp in M?  M is never more than 0.9 full, so the probe meets an empty slot.
-__device__ __forceinline__ bool main_contains(const unsigned long long* __restrict__ Mk, unsigned long long mask,
-                                              unsigned long long fp) {
-  unsigned long long slot = fp_slot(fp, mask);
-  for (unsigned long long probe = 0; probe <= mask; probe++) {
-    const unsigned long long k = Mk[slot];
-    if (k == fp) return true;
-    if (k == EMPTY) return false;
-    slot = (slot + 1) & mask;
-  }
-  return false;
-}
-
-// Insert fp with value val into L; returns the slot (EMPTY if L is too full: the
-// driver grows L and redoes the chunk, whose L inserts are idempotent).  One
-// returning atomic per probe: the CAS doubles as the read.
-__device__ __forceinline__ unsigned long long level_insert(unsigned long long* L, unsigned long long mask,
+// Insert fp with value val; returns the slot, or EMPTY when the probe run is
+// too long (the table is too full: the driver grows it and redoes the chunk,
+// whose inserts are idempotent).
+//
+// Fast path: the first 4 entries of the probe run are read with plain 16 B
+// loads (issued together: one memory round trip).  Keys are never removed or
+// moved while a level is expanded, so a key seen there is really there: an
+// earlier level's copy of fp is final (no atomic, no write -- most
+// successors), and a same-level copy only needs its atomicMin.  A slot seen
+// empty may have been claimed since (the load can be stale), so the run goes
+// on from there with the CAS protocol, one returning atomic per probe.
+__device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T, unsigned long long mask,
                                                            unsigned long long fp, unsigned long long val,
-                                                           DevStatus* st) {
+                                                           unsigned long long floor, DevStatus* st) {
   unsigned long long slot = fp_slot(fp, mask);
-  // a probe run this long means the level tier is (nearly) full: give up and
-  // let the driver grow it rather than walk the whole table
+  if (slot + 3 <= mask) {
+    const ulonglong2* E = reinterpret_cast<const ulonglong2*>(T) + slot;
+    const ulonglong2 e0 = E[0], e1 = E[1], e2 = E[2], e3 = E[3];
+    int k = 4;
+    unsigned long long kv = 0;
+    bool found = false;
+    if (e0.x == fp || e0.x == EMPTY) { k = 0; kv = e0.y; found = e0.x == fp; }
+    else if (e1.x == fp || e1.x == EMPTY) { k = 1; kv = e1.y; found = e1.x == fp; }
+    else if (e2.x == fp || e2.x == EMPTY) { k = 2; kv = e2.y; found = e2.x == fp; }
+    else if (e3.x == fp || e3.x == EMPTY) { k = 3; kv = e3.y; found = e3.x == fp; }
+    slot += (unsigned long long)k;
+    if (found) {
+      if (kv >= floor) atomicMin(T + 2 * slot + 1, val);  // same level (or its claimer's min in flight)
+      return slot;
+    }
+  }
   const unsigned long long limit = mask < 4096 ? mask : 4096;
   for (unsigned long long probe = 0; probe <= limit; probe++) {
-    unsigned long long* e = L + 2 * slot;
+    unsigned long long* e = T + 2 * slot;
     const unsigned long long prev = atomicCAS(e, EMPTY, fp);
-    if (prev == EMPTY || prev == fp) {
+    if (prev == EMPTY) {
       atomicMin(e + 1, val);
+      return slot;
+    }
+    if (prev == fp) {
+      // an earlier level's entry is final: leave its line clean.  (A value of
+      // ~0 is an entry being claimed this level, whose claimer's atomicMin is
+      // still in flight: >= floor, so this one takes part.)
+      const unsigned long long cur = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur >= floor) atomicMin(e + 1, val);
       return slot;
     }
     slot = (slot + 1) & mask;
   }
-  atomicOr(&st->cap_flags, 1u << E_CAP_LEVEL);
+  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
   return EMPTY;
 }
 
-// Insert a key known to be absent (merge, rehash) into M.
-__device__ __forceinline__ bool main_insert_new(unsigned long long* Mk, unsigned long long mask, unsigned long long fp) {
-  unsigned long long slot = fp_slot(fp, mask);
-  for (unsigned long long probe = 0; probe <= mask; probe++) {
-    if (atomicCAS(Mk + slot, EMPTY, fp) == EMPTY) return true;
-    slot = (slot + 1) & mask;
-  }
-  return false;
+// The candidate word: CAND_DUP, or hidden << 47 | slot.
+__device__ __forceinline__ unsigned long long cand_word(unsigned long long slot, unsigned long long val) {
+  return slot == EMPTY ? CAND_DUP : (((val & 0xFFFFULL) << 47) | slot);
 }
 
-// The candidate's probe: CAND_DUP if an earlier level holds its fingerprint,
-// else its L slot with its hidden variables (for the collision count).
-__device__ __forceinline__ unsigned long long fpset_probe(const unsigned long long* __restrict__ Mk,
-                                                          unsigned long long mmask, unsigned long long* L,
-                                                          unsigned long long lmask, unsigned long long fp,
-                                                          unsigned long long val, DevStatus* st) {
-  if (main_contains(Mk, mmask, fp)) return CAND_DUP;
-  const unsigned long long slot = level_insert(L, lmask, fp, val, st);
-  return slot == EMPTY ? CAND_DUP : (((val & 0xFFFFULL) << 47) | slot);
+// After every insert of the round: did the candidate (rank; its hidden
+// variables in the low 16 bits of `hidden`) win the entry whose value is v?
+// A same-level loser with other hidden variables is a hidden-variable collision.
+__device__ __forceinline__ bool fpset_won(unsigned long long v, unsigned long long rank, unsigned long long floor,
+                                          unsigned long long hidden, bool& collision) {
+  const bool win = (v >> VAL_RANK_SHIFT) == rank;
+  collision = !win && v >= floor && ((v ^ hidden) & 0xFFFFULL) != 0;
+  return win;
 }
 
 }  // namespace rmc

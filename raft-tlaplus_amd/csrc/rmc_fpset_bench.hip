@@ -1,13 +1,13 @@
 // rmc_fpset_bench.hip — fingerprint-set insert microbenchmark.
 //
-// The BFS's own probe (rmc_fpset.h fpset_probe: a read-only lookup in the
-// main tier, then for keys it lacks a CAS + atomicMin of the TLC-order key in
-// the level tier) on a main tier of 2^S slots.  Keys are splitmix64(42 + i).
-// For each target load L the main tier is prefilled (untimed) to L, then a
-// batch of B probes is timed with HIP events: a fraction `dup` of them look up
-// an already present key (default 1 - D/G of the bench workload: 1 - 1/3.58),
-// the rest are new keys and go to a level tier sized 2x the batch's new keys.
-// One line of JSON per load: probes/s and line-granular bytes/s.
+// The BFS's own insert (rmc_fpset.h fpset_insert: a CAS per probe; an
+// atomicMin of the TLC-order rank unless the key is an earlier level's) on a
+// table of 2^S slots.  Keys are splitmix64(42 + i).  For each target load L
+// the table is prefilled (untimed, as an earlier level) to L minus the timed
+// batch's new keys, then a batch of B inserts is timed with HIP events: a
+// fraction `dup` of them re-insert an already present key (default 1 - D/G
+// of the bench workload: 1 - 1/3.58), the rest are new, so the table ends at
+// load L.  One line of JSON per load: inserts/s and line-granular bytes/s.
 //
 //   fpset_bench [-slots_log2 S] [-batch B] [-dup F] [-loads 0.25,0.5,0.75]
 #include <hip/hip_runtime.h>
@@ -37,19 +37,18 @@ __device__ __forceinline__ unsigned long long sm64(unsigned long long x) {
 }
 __device__ __forceinline__ unsigned long long key_of(unsigned long long i) { return sm64(42 + i); }
 
-// keys [first, first + n) into the main tier (prefill)
+// keys [first, first + n) as an earlier level's entries (prefill; floor 0)
 __global__ __launch_bounds__(256) void k_fill(unsigned long long* T, unsigned long long mask, unsigned long long first,
                                               unsigned long long n, DevStatus* st) {
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride)
-    if (!main_insert_new(T, mask, key_of(first + j))) atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+    (void)fpset_insert(T, mask, key_of(first + j), (first + j) << VAL_RANK_SHIFT, 0ULL, st);
 }
 
 // the timed batch (level 2): insert j re-inserts a present key when its hash
 // falls below dup_thresh, else inserts the new key present + j.  One slot written per insert,
 // as k_expand writes cand_slot.
-__global__ __launch_bounds__(256) void k_batch(const unsigned long long* T, unsigned long long mask,
-                                               unsigned long long* Lt, unsigned long long lmask,
+__global__ __launch_bounds__(256) void k_batch(unsigned long long* T, unsigned long long mask,
                                                unsigned long long present, unsigned long long nb,
                                                unsigned long long dup_thresh, unsigned long long* new_ctr,
                                                unsigned long long* out_slot, DevStatus* st) {
@@ -60,7 +59,9 @@ __global__ __launch_bounds__(256) void k_batch(const unsigned long long* T, unsi
     const unsigned long long i = fresh ? present + j : sm64(h) % present;  // new keys: distinct indices
     const unsigned long long m = __ballot(fresh);  // one counter atomic per wave, not per key
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(new_ctr, (unsigned long long)__popcll(m));
-    out_slot[j] = fpset_probe(T, mask, Lt, lmask, key_of(i), j << VAL_RANK_SHIFT, st);
+    // the batch is the next level: floor above every prefilled rank
+    out_slot[j] = fpset_insert(T, mask, key_of(i), (present + 1 + j) << VAL_RANK_SHIFT,
+                               present << VAL_RANK_SHIFT, st);
   }
 }
 
@@ -91,12 +92,9 @@ int main(int argc, char** argv) {
     return 2;
   }
   const unsigned long long slots = 1ULL << slots_log2, mask = slots - 1;
-  unsigned long long *T = nullptr, *Lt = nullptr, *slot = nullptr, *ctr = nullptr;
+  unsigned long long *T = nullptr, *slot = nullptr, *ctr = nullptr;
   rmc::DevStatus* st = nullptr;
-  unsigned long long lslots = 1ULL << 16;
-  while (lslots < 2 * (unsigned long long)((1.0 - dup) * (double)batch) + 1024) lslots <<= 1;
-  CK(hipMalloc(&T, slots * 8));
-  CK(hipMalloc(&Lt, lslots * 16));
+  CK(hipMalloc(&T, slots * 16));
   CK(hipMalloc(&slot, batch * 8));
   CK(hipMalloc(&ctr, 8));
   CK(hipMalloc(&st, sizeof(rmc::DevStatus)));
@@ -105,13 +103,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   const unsigned grid = 256 * 64;  // grid-stride: 64 blocks per CU
   for (double L : loads) {
-    const unsigned long long present = (unsigned long long)(L * (double)slots);
-    if (present < 1024 || L >= 0.95) {
-      fprintf(stderr, "fpset_bench: load %.2f out of range\n", L);
+    const unsigned long long target = (unsigned long long)(L * (double)slots);
+    const unsigned long long nb_new = (unsigned long long)((1.0 - dup) * (double)batch);
+    if (target <= nb_new + 1 || L >= 0.95) {
+      fprintf(stderr, "fpset_bench: load %.2f too small for the batch (or too close to full)\n", L);
       return 2;
     }
-    CK(hipMemset(T, 0xFF, slots * 8));
-    CK(hipMemset(Lt, 0xFF, lslots * 16));
+    const unsigned long long present = target - nb_new;
+    CK(hipMemset(T, 0xFF, slots * 16));
     CK(hipMemset(ctr, 0, 8));
     CK(hipMemset(st, 0, sizeof(rmc::DevStatus)));
     hipLaunchKernelGGL(rmc::k_fill, dim3(grid), dim3(256), 0, 0, T, mask, 0ULL, present, st);
@@ -119,8 +118,7 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     const unsigned long long thresh = (unsigned long long)(dup * 18446744073709551615.0);
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(rmc::k_batch, dim3(grid), dim3(256), 0, 0, T, mask, Lt, lslots - 1, present, batch, thresh, ctr,
-                       slot, st);
+    hipLaunchKernelGGL(rmc::k_batch, dim3(grid), dim3(256), 0, 0, T, mask, present, batch, thresh, ctr, slot, st);
     CK(hipGetLastError());
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
@@ -131,16 +129,15 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(&added, ctr, 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(&hs, st, sizeof hs, hipMemcpyDeviceToHost));
     const double s = ms * 1e-3;
-    // line-granular traffic: every probe reads one 128 B line of the main
-    // tier; a new key also reads and dirties one line of the level tier
-    printf("{\"slots_log2\": %d, \"main_load\": %.3f, \"batch\": %llu, \"dup\": %.3f, \"new\": %llu, \"ms\": %.3f, "
-           "\"probes_per_s\": %.4g, \"line_GBps_min\": %.1f, \"level_slots_log2\": %d, \"full\": %d}\n",
-           slots_log2, (double)present / (double)slots, batch, dup, added, ms, batch / s,
-           (batch * 128.0 + added * 256.0) / s / 1e9, __builtin_ctzll(lslots), hs.cap_flags != 0);
+    // line-granular traffic: every insert reads one 128 B line; a new key
+    // also writes it back (duplicates of earlier levels leave it clean)
+    printf("{\"slots_log2\": %d, \"load\": %.3f, \"batch\": %llu, \"dup\": %.3f, \"new\": %llu, \"ms\": %.3f, "
+           "\"inserts_per_s\": %.4g, \"line_GBps_min\": %.1f, \"table_full\": %d}\n",
+           slots_log2, (double)(present + added) / (double)slots, batch, dup, added, ms, batch / s,
+           (batch * 128.0 + added * 128.0) / s / 1e9, hs.cap_flags != 0);
     fflush(stdout);
   }
   CK(hipFree(T));
-  CK(hipFree(Lt));
   CK(hipFree(slot));
   CK(hipFree(ctr));
   CK(hipFree(st));

@@ -8,14 +8,12 @@
 //                  (one binding per wave step, so fixed actions are wave-
 //                  uniform); then lane-per-successor: rebuild the delta,
 //                  compute the canonical fingerprint incrementally from H_pi,
-//                  probe the main tier of the fingerprint set (earlier levels,
-//                  read-only) and insert the rest into the level tier with
-//                  first-in-TLC-order-wins semantics (atomicMin on (parent,
-//                  ordinal)); rmc_fpset.h.
+//                  insert it into the HBM fingerprint set with first-in-TLC-
+//                  order-wins semantics (atomicMin on (parent, ordinal)),
+//                  leaving entries of earlier levels unwritten (rmc_fpset.h).
 //   k_mark         one thread per parent: which of its candidates won, and
 //                  each winner's rank in TLC order; same-level hidden-variable
 //                  collisions are counted here.
-//   k_merge        (per level) the level tier's fingerprints into the main tier.
 //   (scan)         exclusive scan of winners per parent -> output positions.
 //   k_materialize  same tiling: compact the tile's winners in LDS, regenerate
 //                  each lane-per-winner, write it to its TLC-order slot of the
@@ -32,6 +30,8 @@ __constant__ Model cM;
 
 constexpr int WAVE = 64;
 constexpr int EXPAND_SEGS = 8;  // candidate-buffer segments of the single-shard k_expand (one per XCD)
+// cand_ob = ordinal << 16 | flags | binding (10 bits)
+constexpr uint32_t OB_ERR = 0x8000u;  // evaluation error: no successor
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -137,8 +137,7 @@ __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set 
 #endif
 template <int SPEC, int N>
 __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
-                                                unsigned long long pbase, unsigned level,
-                                                const unsigned long long* __restrict__ mkeys, unsigned long long mmask,
+                                                unsigned long long pbase, unsigned long long floor, int sharded,
                                                 unsigned long long* __restrict__ table, unsigned long long mask,
                                                 unsigned long long* __restrict__ cand_slot,
                                                 uint32_t* __restrict__ cand_ob, uint32_t* __restrict__ par_off,
@@ -245,8 +244,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     // atomics per launch on one address.  The sharded search needs its
     // candidates dense, so it keeps one counter.
     if (tid == 0) {
-      const int seg = cand_val ? 0 : (int)(blockIdx.x & (EXPAND_SEGS - 1));
-      const unsigned long long seg_cap = cand_val ? cand_cap : cand_cap / EXPAND_SEGS;
+      const int seg = sharded ? 0 : (int)(blockIdx.x & (EXPAND_SEGS - 1));
+      const unsigned long long seg_cap = sharded ? cand_cap : cand_cap / EXPAND_SEGS;
       sSeg = seg_cap;
       sG = seg * seg_cap + (total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL);
     }
@@ -307,21 +306,21 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     eval_binding<SPEC, N>(s, cM, b, d);
     const unsigned long long t = gbase + sBase[p] + rank_below(sOrd + p * ordw, d.ordinal);
     const unsigned long long pg = pbase + p0 + p;
-    unsigned long long slot = 0;
+    unsigned long long slot = CAND_DUP;
     if (!d.err) {
       unsigned long long fp = delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
       // TLC-order rank (parent global index, Next ordinal) above the hidden variables
-      unsigned long long val = (((pg << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
+      unsigned long long val = ((((pg + 1) << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
                                (unsigned long long)hidden_of<SPEC>(d.hdr);
-      if (cand_val) {  // sharded search: the fp's owner inserts it (k_insert_recv)
-        slot = fp == EMPTY ? EMPTY - 1 : fp;
+      if (sharded) {  // the fp's owner inserts it (k_insert_recv)
+        slot = fp;
         cand_val[t] = val;
       } else {
-        slot = fpset_probe(mkeys, mmask, table, mask, fp, val, st);
+        slot = cand_word(fpset_insert(table, mask, fp, val, floor, st), val);
       }
     }
     cand_slot[t] = slot;
-    cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? 0x8000u : 0u);
+    cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : 0u);
   }
   STAMP(3);
 }
@@ -329,12 +328,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
 // One thread per parent: which of its candidates won their fingerprint, and
 // each winner's rank among the parent's winners (candidates are stored in TLC
 // ordinal order, so the rank is the output order).  cand_win = 1 + rank, 0 =
-// lost.  A candidate found in the main tier lost to an earlier level; one in
-// the level tier won iff the slot's minimum rank is its own.  A same-level
-// loser whose hidden variables differ from the winner's is a hidden-variable
-// collision (SURVEY.md §7 hard part 1): counted, as the oracle counts them.
+// lost.  A same-level loser whose hidden variables differ from the winner's is
+// a hidden-variable collision (SURVEY.md §7 hard part 1), counted as the
+// oracles count them.
 __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsigned long long pbase,
-                                              const unsigned long long* __restrict__ table,
+                                              unsigned long long floor, const unsigned long long* __restrict__ table,
                                               const unsigned long long* __restrict__ cand_slot,
                                               const uint32_t* __restrict__ cand_ob,
                                               const uint32_t* __restrict__ par_off, const uint32_t* __restrict__ par_n,
@@ -344,7 +342,7 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
   if (p >= nparents) return;
   uint32_t off = par_off[p], n = par_n[p];
   uint32_t cnt = 0, coll = 0;
-  const unsigned long long base = (pbase + p) << 10;
+  const unsigned long long base = (pbase + p + 1) << 10;  // ranks count parents from 1 (Init's val is 0)
   // the candidates' table reads are independent: issue up to 8 before using any
   constexpr int U = 8;
   for (uint32_t t0 = off; t0 < off + n; t0 += U) {
@@ -353,17 +351,17 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t t = t0 + u;
-      ob[u] = t < off + n ? cand_ob[t] : 0x8000u;
-      sl[u] = (ob[u] & 0x8000u) ? CAND_DUP : cand_slot[t];
-      v[u] = (sl[u] & CAND_DUP) ? 0ULL : table[2 * (sl[u] & CAND_SLOT_MASK) + 1];
+      ob[u] = t < off + n ? cand_ob[t] : OB_ERR;
+      sl[u] = (ob[u] & OB_ERR) ? CAND_DUP : cand_slot[t];
+      v[u] = (sl[u] & CAND_DUP) ? ~0ULL : table[2 * (sl[u] & CAND_SLOT_MASK) + 1];
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t t = t0 + u;
       if (t >= off + n) break;
-      const bool lvl = !(sl[u] & CAND_DUP);
-      const bool win = lvl && (v[u] >> VAL_RANK_SHIFT) == (base | (ob[u] >> 16));
-      coll += (lvl && !win && ((v[u] ^ (sl[u] >> 47)) & 0xFFFFULL)) ? 1u : 0u;
+      bool c = false;
+      const bool win = !(sl[u] & CAND_DUP) && fpset_won(v[u], base | (ob[u] >> 16), floor, sl[u] >> 47, c);
+      coll += c ? 1u : 0u;
       cand_win[t] = win ? (uint16_t)(++cnt) : (uint16_t)0;
     }
   }
@@ -513,7 +511,7 @@ __global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* _
   if (threadIdx.x < W) h[threadIdx.x] = 0;
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n && !(cand_ob[t] & 0x8000u)) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
+  if (t < n && !(cand_ob[t] & OB_ERR)) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
   __syncthreads();
   if (threadIdx.x < W) blk_counts[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
@@ -531,7 +529,7 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  if (cand_ob[t] & 0x8000u) {
+  if (cand_ob[t] & OB_ERR) {
     perm[t] = 0xFFFFFFFFu;
     return;
   }
@@ -542,33 +540,34 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
   perm[t] = pos;
 }
 
-// Owner side: probe every received (fp, val); first in TLC order wins.
+// Owner side: insert every received (fp, val); first in TLC order wins.
 __global__ __launch_bounds__(256) void k_insert_recv(const unsigned long long* __restrict__ recv, unsigned long long n,
-                                                     const unsigned long long* __restrict__ mkeys,
-                                                     unsigned long long mmask, unsigned long long* __restrict__ table,
-                                                     unsigned long long mask, unsigned long long* __restrict__ recv_slot,
-                                                     DevStatus* st) {
+                                                     unsigned long long* __restrict__ table, unsigned long long mask,
+                                                     unsigned long long floor,
+                                                     unsigned long long* __restrict__ recv_slot, DevStatus* st) {
   unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  recv_slot[j] = fpset_probe(mkeys, mmask, table, mask, recv[2 * j], recv[2 * j + 1], st);
+  const unsigned long long v = recv[2 * j + 1];
+  recv_slot[j] = cand_word(fpset_insert(table, mask, recv[2 * j], v, floor, st), v);
 }
 
 // Owner side, after all of the round's inserts: did the record win its fp?
-// newcount += number of winners (= entries added to the level tier this round);
+// newcount += number of winners (= entries added to the table this round);
 // same-level losers with other hidden variables are counted as in k_mark.
 __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __restrict__ recv,
                                                    const unsigned long long* __restrict__ recv_slot,
                                                    unsigned long long n, const unsigned long long* __restrict__ table,
-                                                   uint8_t* __restrict__ flag, unsigned long long* __restrict__ newcount,
-                                                   DevStatus* st) {
+                                                   unsigned long long floor, uint8_t* __restrict__ flag,
+                                                   unsigned long long* __restrict__ newcount, DevStatus* st) {
   unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   bool w = false;
   if (j < n) {
     const unsigned long long rs = recv_slot[j];
     if (!(rs & CAND_DUP)) {
-      const unsigned long long v = table[2 * (rs & CAND_SLOT_MASK) + 1], mine = recv[2 * j + 1];
-      w = v == mine;
-      if (!w && ((v ^ mine) & 0xFFFFULL)) atomicAdd(&st->hidden_coll, 1ULL);
+      const unsigned long long mine = recv[2 * j + 1];
+      bool c = false;
+      w = fpset_won(table[2 * (rs & CAND_SLOT_MASK) + 1], mine >> VAL_RANK_SHIFT, floor, mine, c);
+      if (c) atomicAdd(&st->hidden_coll, 1ULL);
     }
     flag[j] = w ? 1 : 0;
   }
@@ -623,19 +622,19 @@ void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* 
   hipLaunchKernelGGL(k_bucket, dim3((unsigned)bucket_blocks(n)), dim3(256), 0, s, cand_fp, cand_val, cand_ob, n, W,
                      blk_off, send, perm);
 }
-void launch_insert_recv(const unsigned long long* recv, unsigned long long n, const unsigned long long* mkeys,
-                        unsigned long long mmask, unsigned long long* table, unsigned long long mask,
-                        unsigned long long* recv_slot, DevStatus* st, hipStream_t s) {
+void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
+                        unsigned long long mask, unsigned long long floor, unsigned long long* recv_slot, DevStatus* st,
+                        hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_insert_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, n, mkeys, mmask, table,
-                     mask, recv_slot, st);
+  hipLaunchKernelGGL(k_insert_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, n, table, mask, floor,
+                     recv_slot, st);
 }
 void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
-                      const unsigned long long* table, uint8_t* flag, unsigned long long* newcount, DevStatus* st,
-                      hipStream_t s) {
+                      const unsigned long long* table, unsigned long long floor, uint8_t* flag,
+                      unsigned long long* newcount, DevStatus* st, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, recv_slot, n, table, flag,
-                     newcount, st);
+  hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, recv_slot, n, table, floor,
+                     flag, newcount, st);
 }
 void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
                      const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s) {
@@ -654,7 +653,7 @@ struct Launch {
     const Model& M = *a.model;
     ExpandLds L = expand_lds(PB, M.words, M.nfixed + M.kmax, M.ord_words, (int)sizeof(MsgSums<N>));
     hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
-                       a.level, a.mkeys, a.mmask, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
+                       a.floor, a.sharded, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);
   }
   template <int SPEC, int N>
@@ -690,10 +689,10 @@ void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatc
 void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, false, a, s); }
 void launch_mark(const LevelArgs& a, hipStream_t s) {
   unsigned long long blocks = (a.nparents + 255) / 256;
-  hipLaunchKernelGGL(k_mark, dim3((unsigned)blocks), dim3(256), 0, s, a.nparents, a.pbase, a.table,
+  hipLaunchKernelGGL(k_mark, dim3((unsigned)blocks), dim3(256), 0, s, a.nparents, a.pbase, a.floor, a.table,
                      a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.cand_win, a.par_win, a.st);
 }
-// Move every entry of the old fingerprint set into a larger one (values kept).
+// Move every entry of the fingerprint set into a larger one (values kept).
 // Grid-stride: a table of 2^32 slots or more would need a grid of 2^32
 // threads or more, past HIP's launch limit.
 __global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __restrict__ old, unsigned long long nold,
@@ -703,7 +702,7 @@ __global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __rest
   for (unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; e < nold; e += stride) {
     unsigned long long k = old[2 * e];
     if (k == EMPTY) continue;
-    unsigned long long slot = (k ^ (k >> 29)) & mask;
+    unsigned long long slot = fp_slot(k, mask);
     unsigned long long probe = 0;
     for (; probe <= mask; probe++) {
       unsigned long long prev = atomicCAS(nt + 2 * slot, EMPTY, k);
@@ -721,43 +720,6 @@ void launch_rehash(const unsigned long long* old, unsigned long long nold, unsig
   unsigned long long blocks = (nold + 255) / 256;
   if (blocks > (1ULL << 22)) blocks = 1ULL << 22;  // 2^30 threads, each striding
   hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, s, old, nold, nt, nmask, st);
-}
-// End of a level: every fingerprint of the level tier joins the main tier (it
-// is absent there: the level tier holds only fingerprints the main tier did
-// not), and the level tier's slots are reset to empty for the next level --
-// one pass, reading and rewriting each entry's line once.
-__global__ __launch_bounds__(256) void k_merge(unsigned long long* __restrict__ L, unsigned long long nl,
-                                               unsigned long long* __restrict__ M, unsigned long long mmask,
-                                               DevStatus* st) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; e < nl; e += stride) {
-    const ulonglong2 ent = reinterpret_cast<const ulonglong2*>(L)[e];
-    if (ent.x == EMPTY && ent.y == EMPTY) continue;
-    reinterpret_cast<ulonglong2*>(L)[e] = make_ulonglong2(EMPTY, EMPTY);
-    if (ent.x != EMPTY && !main_insert_new(M, mmask, ent.x)) atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
-  }
-}
-void launch_merge(unsigned long long* L, unsigned long long nl, unsigned long long* M, unsigned long long mmask,
-                  DevStatus* st, hipStream_t s) {
-  unsigned long long blocks = (nl + 255) / 256;
-  if (blocks > (1ULL << 20)) blocks = 1ULL << 20;
-  hipLaunchKernelGGL(k_merge, dim3((unsigned)blocks), dim3(256), 0, s, L, nl, M, mmask, st);
-}
-// Main-tier growth: every key into a table of twice (or more) the slots.
-__global__ __launch_bounds__(256) void k_rehash_main(const unsigned long long* __restrict__ old, unsigned long long nold,
-                                                     unsigned long long* __restrict__ nt, unsigned long long mask,
-                                                     DevStatus* st) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; e < nold; e += stride) {
-    const unsigned long long k = old[e];
-    if (k != EMPTY && !main_insert_new(nt, mask, k)) atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
-  }
-}
-void launch_rehash_main(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
-                        unsigned long long nmask, DevStatus* st, hipStream_t s) {
-  unsigned long long blocks = (nold + 255) / 256;
-  if (blocks > (1ULL << 22)) blocks = 1ULL << 22;
-  hipLaunchKernelGGL(k_rehash_main, dim3((unsigned)blocks), dim3(256), 0, s, old, nold, nt, nmask, st);
 }
 size_t scan_temp_bytes(unsigned long long n) {
   size_t bytes = 0;

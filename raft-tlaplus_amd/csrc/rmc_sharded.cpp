@@ -123,13 +123,11 @@ struct RcclComm : Comm {
 
 // ---------------------------------------------------------- shard buffers
 struct ShardBufs {
-  // table/table2: fingerprint set main tier (8 B keys) and its growth target;
-  // ltab/ltab2: level tier (16 B (fp, val) entries) and its growth target
-  DevBuf table, table2, ltab, ltab2, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  DevBuf table, table2, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, small, bcnt, boff, btmp;
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   void release() {
-    for (DevBuf* b : {&table, &table2, &ltab, &ltab2, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
+    for (DevBuf* b : {&table, &table2, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
                       &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &small, &bcnt,
                       &boff, &btmp})
       b->release();
@@ -158,9 +156,7 @@ void release_shard_buffers() {
 struct Shard {
   int id = 0;
   ShardBufs* B = nullptr;
-  unsigned long long slots = 0, entries = 0;  // main tier: slots, keys (states of completed levels)
-  unsigned long long lact = 0, lclean = 0, lentries = 0;  // level tier: slots in use, known-empty prefix, keys
-  unsigned long long lentries_prev = 1024;                 // the previous level's (sizes the next level's tier)
+  unsigned long long slots = 0, entries = 0;  // fingerprint set of this owner: slots, entries
   uint32_t *cur = nullptr, *nxt = nullptr;
   unsigned long long fcap = 0;       // states per frontier buffer
   unsigned long long ncur = 0;       // local states of the current level
@@ -179,56 +175,21 @@ static unsigned long long local_count(unsigned long long P, int W, unsigned long
   return full * CH + (unsigned long long)part;
 }
 
-// Main tier: room for `need` keys at <= 0.6 load (OutOfDeviceMemory ends the
-// check with status 3).
-static void main_fit(Shard& s, unsigned long long need, hipStream_t stream) {
-  if (need * 5 <= s.slots * 3) return;
+// Room for need_entries at <= 0.5 load (OutOfDeviceMemory ends the check with status 3).
+static void table_grow(Shard& s, unsigned long long need_entries, hipStream_t stream) {
+  if (need_entries * 2 <= s.slots) return;
   unsigned long long nslots = s.slots;
-  while (need * 5 > nslots * 3) nslots <<= 1;
+  while (need_entries * 2 > nslots) nslots <<= 1;
   DevBuf& nt = s.B->table2;
-  nt.ensure(nslots * 8);
-  HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 8, stream));
-  launch_rehash_main(s.B->table.as<unsigned long long>(), s.slots, nt.as<unsigned long long>(), nslots - 1,
-                     s.B->stbuf.as<DevStatus>(), stream);
+  nt.ensure(nslots * 16);
+  HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
+  launch_rehash(s.B->table.as<unsigned long long>(), s.slots, nt.as<unsigned long long>(), nslots - 1,
+                s.B->stbuf.as<DevStatus>(), stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(stream));
   std::swap(s.B->table.p, nt.p);
   std::swap(s.B->table.bytes, nt.bytes);
   s.slots = nslots;
-  if (nt.bytes >= (1ULL << 30)) nt.release();
-}
-
-// Level tier at a level start (it is empty between levels): `slots` in use.
-static void level_begin(Shard& s, unsigned long long slots, hipStream_t stream) {
-  DevBuf& L = s.B->ltab;
-  if (L.bytes < slots * 16) {
-    L.ensure(slots * 16);
-    HIPCHK(hipMemsetAsync(L.p, 0xFF, L.bytes, stream));
-    s.lclean = L.bytes / 16;
-  } else if (s.lclean < slots) {
-    HIPCHK(hipMemsetAsync(L.as<unsigned long long>() + 2 * s.lclean, 0xFF, (slots - s.lclean) * 16, stream));
-    s.lclean = slots;
-  }
-  s.lact = slots;
-  s.lentries = 0;
-}
-
-// Level tier: room for `need` entries at <= 0.5 load, keeping this level's entries.
-static void level_fit(Shard& s, unsigned long long need, hipStream_t stream) {
-  if (need * 2 <= s.lact) return;
-  unsigned long long nslots = s.lact;
-  while (need * 3 > nslots) nslots <<= 1;
-  HIPCHK(hipStreamSynchronize(stream));
-  DevBuf& nt = s.B->ltab2;
-  nt.ensure(nslots * 16);
-  HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
-  launch_rehash(s.B->ltab.as<unsigned long long>(), s.lact, nt.as<unsigned long long>(), nslots - 1,
-                s.B->stbuf.as<DevStatus>(), stream);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(stream));
-  std::swap(s.B->ltab.p, nt.p);
-  std::swap(s.B->ltab.bytes, nt.bytes);
-  s.lact = s.lclean = nslots;
   if (nt.bytes >= (1ULL << 30)) nt.release();
 }
 
@@ -267,9 +228,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     ShardBufs& B = *s.B;
     s.slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 22, m->hint_slots);
     if (s.slots & (s.slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
-    B.table.ensure(s.slots * 8);
-    HIPCHK(hipMemsetAsync(B.table.p, 0xFF, s.slots * 8, stream));
-    s.lclean = 0;
+    B.table.ensure(s.slots * 16);
+    HIPCHK(hipMemsetAsync(B.table.p, 0xFF, s.slots * 16, stream));
     s.fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 20, m->hint_fcap);
     B.fa.ensure(s.fcap * WD * 4);
     B.fb.ensure(s.fcap * WD * 4);
@@ -316,7 +276,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       HIPCHK(hipMemcpyAsync(s.B->trb.p, &zero, 2, hipMemcpyHostToDevice, stream));
     }
     if (s.id == owner0) {
-      HIPCHK(hipMemcpyAsync(s.B->table.as<unsigned long long>() + fp_slot(fp0, s.slots - 1), &fp0, 8,
+      const unsigned long long ent[2] = {fp0, 0ULL};  // val 0: older than every successor
+      HIPCHK(hipMemcpyAsync(s.B->table.as<unsigned long long>() + 2 * fp_slot(fp0, s.slots - 1), ent, 16,
                             hipMemcpyHostToDevice, stream));
       s.entries = 1;
     }
@@ -355,13 +316,9 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     const unsigned long long rounds = (P + W * CH - 1) / (W * CH);
     const unsigned long long lbase = level_base[depth];
     unsigned long long GW = 0, gen_lvl = 0;
-    if (lbase + P >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
-    for (Shard& s : sh) {
-      s.next_fill = 0;
-      unsigned long long ls = 1ULL << 16;
-      while (ls < 2 * s.lentries_prev + 1024) ls <<= 1;
-      level_begin(s, ls, stream);
-    }
+    if (lbase + P + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
+    for (Shard& s : sh) s.next_fill = 0;
+    const unsigned long long floor = (lbase + 1) << VAL_FLOOR_SHIFT;  // entries below: earlier levels
     for (unsigned long long c = 0; c < rounds && !stop; c++) {
       // ---- expand: fp + key per candidate
       for (Shard& s : sh) {
@@ -375,6 +332,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           a.nparents = s.n;
           a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
           a.level = level;
+          a.sharded = 1;
           a.cand_slot = s.B->cfp.as<unsigned long long>();
           a.cand_val = s.B->cval.as<unsigned long long>();
           a.cand_ob = s.B->cob.as<uint32_t>();
@@ -473,17 +431,16 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       }
       // ---- owners insert, then mark
       for (Shard& s : sh) {
-        level_fit(s, s.lentries + s.nrecv, stream);  // exact bound: every received record new
+        table_grow(s, s.entries + s.nrecv, stream);  // exact bound: every received record new
         launch_insert_recv(s.B->recv.as<unsigned long long>(), s.nrecv, s.B->table.as<unsigned long long>(),
-                           s.slots - 1, s.B->ltab.as<unsigned long long>(), s.lact - 1,
-                           s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
+                           s.slots - 1, floor, s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
         HIPCHK(hipGetLastError());
       }
       for (Shard& s : sh) {
         unsigned long long* nc = s.B->counters.as<unsigned long long>() + 1;
         launch_mark_recv(s.B->recv.as<unsigned long long>(), s.B->rslot.as<unsigned long long>(), s.nrecv,
-                         s.B->ltab.as<unsigned long long>(), s.B->rflag.as<uint8_t>(), nc, s.B->stbuf.as<DevStatus>(),
-                         stream);
+                         s.B->table.as<unsigned long long>(), floor, s.B->rflag.as<uint8_t>(), nc,
+                         s.B->stbuf.as<DevStatus>(), stream);
         HIPCHK(hipGetLastError());
       }
       // ---- win flags back to the generators (reverse of the record exchange)
@@ -526,7 +483,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       HIPCHK(hipStreamSynchronize(stream));
       for (int i = 0; i < NL; i++) {
         sh[i].nwin = (unsigned long long)lastpos[i] + lastwin[i];
-        sh[i].lentries += newc[i];
+        sh[i].entries += newc[i];
         HIPCHK(hipMemsetAsync(sh[i].B->counters.as<unsigned long long>() + 1, 0, 8, stream));
         rows[i] = {sh[i].nwin};
       }
@@ -661,19 +618,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     generated += gen_lvl;
     distinct += GW;
     if (GW || gen_lvl) m->levels.push_back({gen_lvl, GW});
-    if (!stop && status == 0) {
-      // this level's fingerprints join each owner's main tier; level tiers emptied
-      for (Shard& s : sh) {
-        if (s.lentries) {
-          main_fit(s, s.entries + s.lentries, stream);
-          launch_merge(s.B->ltab.as<unsigned long long>(), s.lact, s.B->table.as<unsigned long long>(), s.slots - 1,
-                       s.B->stbuf.as<DevStatus>(), stream);
-          HIPCHK(hipGetLastError());
-        }
-        s.entries += s.lentries;
-        s.lentries_prev = std::max(1024ULL, s.lentries);
-      }
-    }
+
     level_base.push_back(lbase + P);
     level_size.push_back(GW);
     if (GW) depth++;

@@ -29,7 +29,8 @@ class Options(ctypes.Structure):
                 ("tlc_order", ctypes.c_int), ("hash_slots", ctypes.c_uint64),
                 ("msg_cap_K", ctypes.c_uint32), ("frontier_cap", ctypes.c_uint64),
                 ("chunk_parents", ctypes.c_uint32), ("verbose", ctypes.c_int),
-                ("max_depth", ctypes.c_int), ("level_slots", ctypes.c_uint64)]
+                ("max_depth", ctypes.c_int), ("grow_on_overflow", ctypes.c_int),
+                ("time_limit", ctypes.c_double)]
 
 
 class Result(ctypes.Structure):
@@ -49,7 +50,7 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
-           "rmc_simulate", "rmc_trace_module", "rmc_trace_json"]
+           "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu"]
 
 _lib = None
 
@@ -79,6 +80,7 @@ def lib():
     L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                     ctypes.POINTER(Result)]
     L.rmc_check_logical.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(Result)]
+    L.rmc_check_cpu.argtypes = [P, ctypes.POINTER(Options), ctypes.POINTER(Result)]
     L.rmc_simulate.argtypes = [P, ctypes.POINTER(Options), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                ctypes.c_uint64, ctypes.c_double, ctypes.POINTER(Result)]
     L.rmc_selftest_host_bfs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64,
@@ -114,14 +116,16 @@ class Model:
             self._h = None
 
     def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
-                 chunk_parents=0, verbose=False, max_depth=0, workers=0, level_slots=0):
+                 chunk_parents=0, verbose=False, max_depth=0, workers=0, grow_on_overflow=False,
+                 time_limit=0.0):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
         o.deadlock_check = 1 if deadlock else 0
         o.hash_slots, o.msg_cap_K, o.frontier_cap = hash_slots, msg_cap_K, frontier_cap
         o.chunk_parents, o.verbose, o.max_depth, o.cpu_workers = chunk_parents, int(verbose), max_depth, workers
-        o.level_slots = level_slots
+        o.grow_on_overflow = int(grow_on_overflow)
+        o.time_limit = float(time_limit)
         return o
 
     def _result(self, rc, r):
@@ -147,6 +151,11 @@ class Model:
         """Run the model check on this process's GPU; returns a dict of TLC's results."""
         o, r = self._options(**kw), Result()
         return self._result(lib().rmc_check(self._h, ctypes.byref(o), ctypes.byref(r)), r)
+
+    def check_cpu(self, workers=0, **kw):
+        """The CPU engine (TLC -workers N on host threads; same results as check)."""
+        o, r = self._options(workers=workers, **kw), Result()
+        return self._result(lib().rmc_check_cpu(self._h, ctypes.byref(o), ctypes.byref(r)), r)
 
     def check_logical(self, shards, **kw):
         """The fingerprint-sharded protocol with `shards` logical shards on this GPU."""

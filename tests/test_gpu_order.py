@@ -1,5 +1,5 @@
 """GPU: TLC-order first-wins under VIEW, hidden-variable collision counts, and
-the fingerprint set's growth / redo safety nets.
+the fingerprint set's growth / redo / message-capacity safety nets.
 
 VIEW view drops acked, electionCtr and restartCtr (Raft.tla:115), which gate
 ClientRequest (:306) and RequestVote (:243): two successors with one view but
@@ -60,8 +60,8 @@ def test_first_wins_across_shards(name, shards, chunk):
 
 
 @pytest.mark.parametrize("name", ["pull_n3v1e2r1", "raft_n4v1e1"])
-def test_main_tier_grows_from_tiny(name):
-    """The main tier starts at 2^10 slots and must double many times at level ends."""
+def test_fpset_grows_from_tiny(name):
+    """The fingerprint set starts at 2^10 slots and must double many times ahead of chunks."""
     g = MEDIUM[name]
     r = raftmc.check_text(g["module"], g["cfg"], hash_slots=1 << 10)
     assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
@@ -71,13 +71,14 @@ def test_main_tier_grows_from_tiny(name):
 
 @pytest.mark.parametrize("name", ["pull_n3v1e2r1", "raft_n4v1e1"])
 @pytest.mark.parametrize("chunk", [0, 333])
-def test_level_tier_overflow_redo(name, chunk):
-    """A 64-slot level tier at every level start and no pre-chunk growth: chunks
-    overflow it, the driver grows it and redoes the chunk; counts unchanged."""
+def test_fpset_overflow_redo(name, chunk):
+    """A 64-slot set and no growth ahead of chunks: chunks overflow it, the
+    driver grows it and redoes the chunk (inserts are idempotent); counts unchanged."""
     g = MEDIUM[name]
-    r = raftmc.check_text(g["module"], g["cfg"], level_slots=64, chunk_parents=chunk)
+    r = raftmc.check_text(g["module"], g["cfg"], hash_slots=64, grow_on_overflow=True, chunk_parents=chunk)
     assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
         (g["generated"], g["distinct"], g["depth"], g["levels"])
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
 
 
 @pytest.mark.parametrize("name", ["raft_n3v1e1", "pull_n3v2e1", "fsync_n3v1e1"])
