@@ -28,62 +28,76 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raft-tlaplus_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-# name -> (module, cfg path relative to ROOT, BASELINE config index, description)
+# name -> (module, cfg path relative to ROOT, BASELINE config label, description)
 WORKLOADS = {
-    "raft_cfg": ("Raft", "configs/Raft.cfg", 1,
+    "raft_cfg": ("Raft", "configs/Raft.cfg", "1",
                  "standard-raft Raft.cfg: 3 servers, Value={v1}, MaxElections=2, MaxRestarts=0"),
-    "raft_n3v2e2": ("Raft", "configs/Raft_n3v2e2.cfg", 2,
-                    "standard-raft: 3 servers, Value={v1,v2} (log bound 2), MaxElections=2 (term bound 3), "
-                    "MaxRestarts=0"),
-    "raft_n3v1e3": ("Raft", "configs/Raft_n3v1e3.cfg", 2,
-                    "standard-raft: 3 servers, Value={v1}, MaxElections=3, MaxRestarts=0"),
-    "raft_n3v2e3": ("Raft", "configs/Raft_n3v2e3.cfg", 2,
-                    "standard-raft: 3 servers, Value={v1,v2}, MaxElections=3, MaxRestarts=0"),
+    "raft_n3v2e2": ("Raft", "configs/Raft_n3v2e2.cfg",
+                    "2 ladder, rung below config 2 (config 2 itself, MaxElections=3, stops at HBM capacity on one "
+                    "GPU: profiles/r02/ladder_Raft_n3v2e3*.txt)",
+                    "standard-raft: 3 servers, Value={v1,v2} (logs <= 2 entries), MaxElections=2 (terms <= 3), "
+                    "MaxRestarts=0; the largest config-2 rung that exhausts on one MI355X"),
+    "raft_n3v1e3": ("Raft", "configs/Raft_n3v1e3.cfg", "2 ladder (Value={v1})",
+                    "standard-raft: 3 servers, Value={v1}, MaxElections=3 (terms <= 4), MaxRestarts=0"),
+    "raft_n3v2e3": ("Raft", "configs/Raft_n3v2e3.cfg", "2",
+                    "standard-raft: 3 servers, Value={v1,v2}, MaxElections=3 (terms <= 4), MaxRestarts=0"),
 }
 DEFAULT_WORKLOAD = "raft_n3v2e2"
 HBM_PEAK = 8.0e12  # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
 
 
 def algorithmic_bytes(res):
-    """Bytes the expand kernel must move per run (SURVEY.md §8d terms it owns):
-    every parent state read once (D*S), one fingerprint-set probe per
-    successor (G*8), one 12-byte candidate record written per successor."""
+    """B = D*S (read each parent once) + G*8 (fp probe) + D*8 (fp
+    store) + D*S (write new state) + D*12 (trace record), for the whole check."""
     D, G, S = res["distinct"], res["generated"] - 1, res["state_bytes"]
-    return D * S + G * 8 + G * 12
+    return 2 * D * S + 8 * G + 20 * D
 
 
-def pmc_traffic(workload):
-    """Per-launch HBM bytes of k_expand from the committed rocprofv3 --pmc summary
-    of this workload (tools/gpu_profile.sh -> profiles/<round>/pmc_summary_<workload>.json),
-    priced (2*FETCH_SIZE + WRITE_SIZE) KiB as MI355X_MICROARCH.md prescribes for gfx950."""
+def pmc_summary(workload):
+    """The committed rocprofv3 --pmc summary of this workload (newest round first):
+    per-kernel HBM traffic per dispatch, priced as tools/pmc_summary.py states."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_%s.json" % workload)), reverse=True):
         try:
-            d = json.load(open(path))
-            for k, v in d["kernels"].items():
-                if k.startswith("rmc::k_expand") and "traffic_bytes_per_dispatch" in v:
-                    return v["traffic_bytes_per_dispatch"], os.path.relpath(path, ROOT)
+            return json.load(open(path)), os.path.relpath(path, ROOT)
         except Exception:
             continue
     return None, None
 
 
-def cpu_baseline(module, cfg_path, seconds=20.0):
-    """The C oracle (oracle/_build/rmc_oracle, a port) timed on this host for a
-    bounded wall budget on the same config; returns distinct states/s."""
-    from oracle import run_c
-    from oracle.pyoracle.cfg import load_cfg
-    exe = run_c.BIN
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
-    cfg = load_cfg(os.path.join(ROOT, cfg_path))
-    threads = max(1, min(16, os.cpu_count() or 1))
-    r = run_c.run(module, cfg["constants"], cfg["invariants"], threads=threads,
-                  extra=["--max-seconds", str(seconds)])
-    return dict(value=r["distinct"] / max(r["seconds"], 1e-9), unit="distinct states/s", cores=threads,
-                kind="port",
-                sample="C oracle (oracle/cengine) BFS of the same cfg for ~%.0fs wall: %d distinct, %d generated, "
-                       "status %s" % (seconds, r["distinct"], r["generated"], r["status"]))
+def host_cores():
+    """CPU threads this process may use: its affinity set, capped by the box's
+    OMP_NUM_THREADS share when set (the GPU box exports 16), and the CPU model."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit():
+        n = min(n, int(cap))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return max(1, n), model
+
+
+def cpu_baseline(module, cfg_path, seconds=15.0):
+    """BASELINE.md's CPU baseline: the build's own multi-threaded C++ BFS
+    (rmc_check_cpu -- same packed layout, lowered actions, fingerprint and
+    first-in-TLC-order rule as the GPU path) on this host's cores, on the same
+    config for a bounded wall budget (it stops at the first level boundary past
+    it); rate = distinct states / seconds of the levels it completed."""
+    import raftmc
+    cores, model = host_cores()
+    m = raftmc.Model(os.path.join(ROOT, "configs", module + ".tla"), os.path.join(ROOT, cfg_path))
+    r = m.check_cpu(workers=cores, time_limit=seconds)
+    return dict(value=r["distinct"] / max(r["seconds"], 1e-9), unit="distinct states/s", cores=cores,
+                kind="port", cpu_model=model,
+                sample="librmc CPU engine (rmc_check_cpu, %d threads) on the same cfg until the first level boundary "
+                       "past %.0f s: %d levels, %d distinct, %d generated in %.1f s (status %s)"
+                       % (cores, seconds, r["depth"], r["distinct"], r["generated"], r["seconds"], r["status"]))
 
 
 def main():
@@ -93,7 +107,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default=os.environ.get("RMC_WORKLOAD", DEFAULT_WORKLOAD))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--logical-shards", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0, help="parents per k_expand launch (0 = librmc's default)")
     args = ap.parse_args()
@@ -145,9 +159,26 @@ def main():
     res = results[-1]
     per_step = elapsed / args.steps
     value = res["distinct"] / per_step
-    exp_bytes = algorithmic_bytes(res)
-    achieved = exp_bytes / (res["expand_ms"] * 1e-3) if res["expand_ms"] > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(args.workload)
+    B = algorithmic_bytes(res)
+    launches = max(1, res["expand_launches"])
+    G, D, S = res["generated"] - 1, res["distinct"], res["state_bytes"]
+    pmc, pmc_src = pmc_summary(args.workload)
+    kpmc = {}
+    if pmc:
+        for k, v in pmc.get("kernels", {}).items():
+            for short in ("k_expand", "k_mark", "k_materialize"):
+                if k.startswith("rmc::" + short) and "traffic_bytes_per_dispatch" in v:
+                    kpmc[short] = v["traffic_bytes_per_dispatch"]
+    # per-kernel shares of SURVEY §8d's bytes, per launch (every kernel runs
+    # once per chunk): k_expand reads the parents and probes / stores the
+    # fingerprints; k_materialize writes the new states and trace records
+    kern = {}
+    for name, bytes_check, ms in (("k_expand", D * S + 8 * G + 8 * D, res["expand_ms"]),
+                                  ("k_materialize", D * S + 12 * D, res["materialize_ms"])):
+        avg = ms / launches
+        ach = bytes_check / launches / (avg * 1e-3) if avg > 0 else 0.0
+        kern[name] = {"bytes_per_launch": bytes_check / launches, "avg_launch_ms": avg, "achieved": ach / 1e9,
+                      "frac": ach / HBM_PEAK, "traffic": kpmc.get(name)}
     if rank == 0:
         line = {
             "metric": "distinct states/sec + time-to-exhaust, standard-raft",
@@ -169,21 +200,28 @@ def main():
                         else "single")},
             "result": {"generated": res["generated"], "distinct": res["distinct"], "depth": res["depth"],
                        "status": res["status"], "time_to_exhaust_s": per_step,
-                       "first_check_s": cold[0] if cold else None},
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
-                         "kernel": "k_expand", "launches": res["expand_launches"],
-                         "avg_launch_ms": res["expand_ms"] / max(1, res["expand_launches"]),
-                         "bytes_per_launch": exp_bytes / max(1, res["expand_launches"])},
+                       "first_check_s": cold[0] if cold else None,
+                       "hidden_var_collisions": res["hidden_var_collisions"],
+                       "fpset_slots": res["hash_capacity"], "state_bytes": S},
+            # achieved = B / t_wall with B = 2DS + 8G + 20D per check;
+            # the dominant kernels' own shares per launch under "kernels"
+            # (HIP-event launch times inside librmc)
+            "roofline": {"bound": "hbm", "achieved": B / per_step / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": B / per_step / HBM_PEAK,
+                         "traffic": sum(kpmc.values()) * launches if len(kpmc) == 3 else None,
+                         "traffic_unit": "HBM bytes per check (PMC: k_expand + k_mark + k_materialize)",
+                         "traffic_source": pmc_src,
+                         "formula": "B = 2*D*S + 8*G + 20*D per check (SURVEY.md 8d) over the check's wall time",
+                         "bytes_per_check": B, "kernel": "k_expand", "launches": launches, "kernels": kern,
+                         "candidate_bytes_per_check": G * (8 + 4 + 2)},
             "kernel_ms": {"expand": res["expand_ms"], "mark_scan": res["mark_ms"],
                           "materialize": res["materialize_ms"]},
         }
-        # atomic throughput of the fingerprint-set inserts (each
-        # successor: one returning CAS per probe + one atomicMin), over k_expand's time
+        # atomic throughput of the fingerprint-set inserts over k_expand's time
         if res["expand_ms"] > 0:
-            line["fpset_inserts"] = {"count": res["generated"] - 1,
-                                     "per_s": (res["generated"] - 1) / (res["expand_ms"] * 1e-3),
-                                     "atomics_per_insert": ">= 2 (CAS per probe + atomicMin)"}
+            line["fpset_inserts"] = {"count": G, "per_s": G / (res["expand_ms"] * 1e-3),
+                                     "atomics": "duplicates of earlier levels: none (plain loads); new "
+                                                "fingerprints: CAS + atomicMin; same-level duplicates: atomicMin"}
         if world > 1:
             # exchange volume of the sharded protocol: 16 B (fp, key) records,
             # 1 B win flags, rows + 10 B trace records; the off-GPU fraction is (W-1)/W,

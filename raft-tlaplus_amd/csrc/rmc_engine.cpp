@@ -232,6 +232,12 @@ void build_actions(Model& M) {
   }
   M.nfixed = nf;
   M.ordinal_limit = off;
+  if (off > 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");
+  for (int q = 0; q < 1024; q++) M.ord2b[q] = 0xFFFF;
+  for (int b = 0; b < nf; b++) M.ord2b[M.act_off[M.fb_act[b]] + M.fb_x[b]] = (uint16_t)b;
+  for (int sl = 0; sl < M.nact; sl++)
+    if (M.act_kind[sl] == K_MSG)
+      for (int k = 0; k < M.kmax; k++) M.ord2b[M.act_off[sl] + k] = (uint16_t)(nf + k);
   M.bind_words = (M.nfixed + M.kmax + 31) / 32;
   M.ord_words = (off + 31) / 32;
   if (off >= 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");
@@ -249,6 +255,41 @@ void build_perms(Model& M, bool symmetry) {
   } while (std::next_permutation(p.begin(), p.end()));
 }
 
+// The drop-in boundary lowers four specs by hand, so the .tla it is given must
+// BE one of them: its text, with comments and whitespace removed, hashed
+// (FNV-1a 64) against the reference's specifications (tools/spec_hashes.py
+// regenerates the table).  Comment and layout edits pass; any edit to the
+// TLA+ itself (e.g. re-enabling DuplicateMessage in Raft's Next,
+// standard-raft/Raft.tla:540) is refused rather than silently checked as the
+// built-in lowering.
+std::string normalise_tla(const std::string& t) {
+  std::string out;
+  int depth = 0;
+  for (size_t i = 0; i < t.size();) {
+    if (t.compare(i, 2, "(*") == 0) { depth++; i += 2; }
+    else if (depth && t.compare(i, 2, "*)") == 0) { depth--; i += 2; }
+    else if (depth) i++;
+    else if (t.compare(i, 2, "\\*") == 0) { while (i < t.size() && t[i] != '\n') i++; }
+    else { if (!isspace((unsigned char)t[i])) out += t[i]; i++; }
+  }
+  return out;
+}
+unsigned long long fnv1a64(const std::string& s) {
+  unsigned long long h = 0xcbf29ce484222325ULL;
+  for (unsigned char c : s) h = (h ^ c) * 0x100000001b3ULL;
+  return h;
+}
+unsigned long long known_spec_hash(const std::string& module) {
+  static const std::map<std::string, unsigned long long> k = {
+      {"Raft", 0x83a8af2f23ec2fd5ULL},          // specifications/standard-raft/Raft.tla
+      {"FlexibleRaft", 0xc4f3c1e150bbc233ULL},  // specifications/flexible-raft/FlexibleRaft.tla
+      {"PullRaft", 0x158f1b6f8dd861a3ULL},      // specifications/pull-raft/PullRaft.tla
+      {"RaftFsync", 0x8135c01b3aedbce3ULL},     // specifications/raft-and-fsync/RaftFsync.tla
+  };
+  auto it = k.find(module);
+  return it == k.end() ? 0 : it->second;
+}
+
 rmc_model* load_model(const std::string& module, const std::string& cfg_text, const std::string& tla_text) {
   auto m = new rmc_model();
   try {
@@ -260,6 +301,17 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
                                "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft)");
     if (!tla_text.empty() && tla_text.find("MODULE " + module) == std::string::npos)
       throw std::runtime_error("the .tla file does not declare MODULE " + module);
+    if (!tla_text.empty()) {
+      const unsigned long long h = fnv1a64(normalise_tla(tla_text));
+      if (h != known_spec_hash(module)) {
+        char hb[32];
+        snprintf(hb, sizeof hb, "%016llx", h);
+        throw std::runtime_error("the TLA+ text of " + module + ".tla (normalised hash " + hb +
+                                 ") is not the reference spec this checker lowers (Vanlightly/raft-tlaplus " +
+                                 module + ".tla; comments and layout may differ, the definitions may not); "
+                                 "checking an edited spec needs a TLA+ front end (SURVEY.md 8f rank 4)");
+      }
+    }
     Cfg c = parse_cfg(cfg_text);
     if (!c.spec.empty()) throw std::runtime_error("SPECIFICATION is not supported; use INIT Init / NEXT Next");
     if (c.init != "Init" || c.next != "Next")

@@ -61,17 +61,21 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
                                                            unsigned long long fp, unsigned long long val,
                                                            unsigned long long floor, DevStatus* st) {
   unsigned long long slot = fp_slot(fp, mask);
-  if (slot + 3 <= mask) {
+#ifndef RMC_FP_FAST
+#define RMC_FP_FAST 4
+#endif
+  if (RMC_FP_FAST > 0 && slot + (RMC_FP_FAST - 1) <= mask) {
     const ulonglong2* E = reinterpret_cast<const ulonglong2*>(T) + slot;
-    const ulonglong2 e0 = E[0], e1 = E[1], e2 = E[2], e3 = E[3];
-    int k = 4;
+    ulonglong2 e[RMC_FP_FAST > 0 ? RMC_FP_FAST : 1];
+#pragma unroll
+    for (int q = 0; q < RMC_FP_FAST; q++) e[q] = E[q];
+    int k = RMC_FP_FAST;
     unsigned long long kv = 0;
     bool found = false;
-    if (e0.x == fp || e0.x == EMPTY) { k = 0; kv = e0.y; found = e0.x == fp; }
-    else if (e1.x == fp || e1.x == EMPTY) { k = 1; kv = e1.y; found = e1.x == fp; }
-    else if (e2.x == fp || e2.x == EMPTY) { k = 2; kv = e2.y; found = e2.x == fp; }
-    else if (e3.x == fp || e3.x == EMPTY) { k = 3; kv = e3.y; found = e3.x == fp; }
-    slot += (unsigned long long)k;
+#pragma unroll
+    for (int q = RMC_FP_FAST - 1; q >= 0; q--)
+      if (e[q].x == fp || e[q].x == EMPTY) { k = q; kv = e[q].y; found = e[q].x == fp; }
+    slot = (slot + (unsigned long long)k) & mask;  // k == RMC_FP_FAST may step past the last slot: wrap
     if (found) {
       if (kv >= floor) atomicMin(T + 2 * slot + 1, val);  // same level (or its claimer's min in flight)
       return slot;

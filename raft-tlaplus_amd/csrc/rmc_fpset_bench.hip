@@ -65,6 +65,30 @@ __global__ __launch_bounds__(256) void k_batch(unsigned long long* T, unsigned l
   }
 }
 
+// Counter calibration (MI355X_MICROARCH.md: FETCH_SIZE / WRITE_SIZE are
+// calibrated only for wide streaming accesses): n random 16 B reads (one
+// entry, one 128 B line each) of a table far larger than the 256 MiB
+// Infinity Cache, then n random returning atomicMin on 8 B words.  Run under
+// rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE: bytes per access = counter * 1024 / n.
+__global__ __launch_bounds__(256) void k_calib_read(const unsigned long long* T, unsigned long long mask,
+                                                    unsigned long long n, unsigned long long* sink) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  unsigned long long acc = 0;
+  for (unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const ulonglong2 e = reinterpret_cast<const ulonglong2*>(T)[sm64(j * 7919) & mask];
+    acc ^= e.x + e.y;
+  }
+  if (acc == 0x1234567ULL) sink[0] = acc;
+}
+__global__ __launch_bounds__(256) void k_calib_atomic(unsigned long long* T, unsigned long long mask,
+                                                      unsigned long long n, unsigned long long* sink) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  unsigned long long acc = 0;
+  for (unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride)
+    acc += atomicMin(T + 2 * (sm64(j * 104729) & mask) + 1, j);
+  if (acc == 0x1234567ULL) sink[0] = acc;
+}
+
 }  // namespace rmc
 
 int main(int argc, char** argv) {
@@ -72,10 +96,12 @@ int main(int argc, char** argv) {
   unsigned long long batch = 64ULL << 20;
   double dup = 1.0 - 1.0 / 3.58;
   std::vector<double> loads = {0.25, 0.5, 0.75};
+  bool calib = false;
   for (int a = 1; a < argc; a++) {
     std::string k = argv[a];
     const char* v = a + 1 < argc ? argv[a + 1] : "";
-    if (k == "-slots_log2") slots_log2 = atoi(v), a++;
+    if (k == "-calib") calib = true;
+    else if (k == "-slots_log2") slots_log2 = atoi(v), a++;
     else if (k == "-batch") batch = strtoull(v, nullptr, 10), a++;
     else if (k == "-dup") dup = atof(v), a++;
     else if (k == "-loads") {
@@ -83,7 +109,7 @@ int main(int argc, char** argv) {
       for (char* t = strtok((char*)v, ","); t; t = strtok(nullptr, ",")) loads.push_back(atof(t));
       a++;
     } else {
-      fprintf(stderr, "usage: fpset_bench [-slots_log2 S] [-batch B] [-dup F] [-loads L1,L2,...]\n");
+      fprintf(stderr, "usage: fpset_bench [-slots_log2 S] [-batch B] [-dup F] [-loads L1,L2,...] [-calib]\n");
       return 2;
     }
   }
@@ -102,6 +128,24 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const unsigned grid = 256 * 64;  // grid-stride: 64 blocks per CU
+  if (calib) {
+    CK(hipMemset(T, 0x11, slots * 16));
+    CK(hipDeviceSynchronize());
+    for (int kind = 0; kind < 2; kind++) {
+      CK(hipEventRecord(e0, 0));
+      if (kind == 0) hipLaunchKernelGGL(rmc::k_calib_read, dim3(grid), dim3(256), 0, 0, T, mask, batch, ctr);
+      else hipLaunchKernelGGL(rmc::k_calib_atomic, dim3(grid), dim3(256), 0, 0, T, mask, batch, ctr);
+      CK(hipGetLastError());
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("{\"calib\": \"%s\", \"accesses\": %llu, \"table_bytes\": %llu, \"ms\": %.3f, \"per_s\": %.4g}\n",
+             kind == 0 ? "random_16B_read" : "random_8B_atomicMin", batch, slots * 16, ms, batch / (ms * 1e-3));
+      fflush(stdout);
+    }
+    return 0;
+  }
   for (double L : loads) {
     const unsigned long long target = (unsigned long long)(L * (double)slots);
     const unsigned long long nb_new = (unsigned long long)((1.0 - dup) * (double)batch);

@@ -77,12 +77,11 @@ struct Tile {
   static constexpr int PB = 64;  // = one 64-bit parent mask per binding in k_expand
 };
 
-// Dynamic LDS layout of k_expand (bytes, host mirrors it in expand_lds_bytes).
+// Dynamic LDS layout of k_expand (bytes; the launch computes the same).
 struct ExpandLds {
-  int Wp, off_Ms, off_Ord, off_EnT, off_BP, off_Base, bytes;
+  int Wp, off_Ms, off_Ord, off_Base, bytes;
 };
-// nbind = max bindings per state (nfixed + kmax).
-__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int nbind, int ordw, int msbytes) {
+__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes) {
   ExpandLds L;
   L.Wp = words | 1;  // odd row stride: lane-per-parent LDS reads are bank-conflict free
   int o = (PB * L.Wp * 4 + 7) & ~7;
@@ -90,11 +89,7 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int nbind, in
   o += PB * msbytes;
   L.off_Ord = o;  // per parent: bitmask over TLC ordinals of its enabled bindings
   o += PB * ordw * 4;
-  L.off_EnT = o;  // per binding: 64-bit mask over the tile's parents where it is enabled
-  o += nbind * 8;
-  L.off_BP = o;  // exclusive prefix over bindings of the masks' popcounts
-  o += (nbind + 1) * 4;
-  L.off_Base = o;
+  L.off_Base = o;  // exclusive prefix over the tile's parents of their successor counts
   o += (PB + 1) * 4;
   L.bytes = o;
   return L;
@@ -148,13 +143,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG, sSeg;
   const int tid = threadIdx.x;
-  const int words = cM.words, ordw = cM.ord_words, nbind = cM.nfixed + cM.kmax;
-  const ExpandLds L = expand_lds(PB, words, nbind, ordw, (int)sizeof(MsgSums<N>));
+  const int words = cM.words, ordw = cM.ord_words;
+  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MsgSums<N>));
   uint32_t* sS = (uint32_t*)lds;
   MsgSums<N>* sMS = (MsgSums<N>*)(lds + L.off_Ms);
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
-  uint32_t* sEnT = (uint32_t*)(lds + L.off_EnT);
-  uint32_t* sBP = (uint32_t*)(lds + L.off_BP);
   uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
@@ -167,7 +160,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     int p = q / words;
     sS[p * L.Wp + (q - p * words)] = src[q];
   }
-  for (int q = tid; q < PB * ordw + 2 * nbind; q += 256) sOrd[q] = 0;  // sOrd and sEnT are adjacent
+  for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
   for (int q = tid; q < PB * (int)(sizeof(MsgSums<N>) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
   __syncthreads();
   STAMP(0);
@@ -200,31 +193,13 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
           for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
           if (nm + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
         }
-        atomicOr(&sEnT[2 * b + (p >> 5)], 1u << (p & 31));
         atomicOr(&sOrd[p * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
       }
     }
   }
   __syncthreads();
   STAMP(2);
-  // ---- per-parent successor counts -> tile prefix (wave 0), one global reservation per tile;
-  //      per-binding counts -> binding prefix (wave 1)
-  if (tid >= 64 && tid < 128) {
-    const int lane = tid - 64;
-    uint32_t carry = 0;
-    if (lane == 0) sBP[0] = 0;
-    for (int b0 = 0; b0 < nbind; b0 += 64) {
-      const int b = b0 + lane;
-      uint32_t incl = b < nbind ? (uint32_t)(__popc(sEnT[2 * b]) + __popc(sEnT[2 * b + 1])) : 0u;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(incl, o, WAVE);
-        if (lane >= o) incl += y;
-      }
-      if (b < nbind) sBP[b + 1] = carry + incl;
-      carry += __shfl(incl, 63, WAVE);
-    }
-  }
+  // ---- per-parent successor counts -> tile prefix (wave 0), one global reservation per tile
   if (tid < 64) {
     int c = 0;
     if (tid < np)
@@ -268,17 +243,17 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     __shared__ unsigned long long sSink;
     unsigned long long acc = 0;
     for (int idx = tid; idx < total; idx += 256) {
-      int lo = 0, hi = nbind - 1;
+      int lo = 0, hi = np - 1;
       while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
-        if ((int)sBP[mid] <= idx) lo = mid; else hi = mid - 1;
+        if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
       }
-      const int b = lo;
-      const int p = select_bit(sEnT + 2 * b, idx - (int)sBP[b]);
+      const int p = lo;
+      const int b = cM.ord2b[select_bit(sOrd + p * ordw, idx - (int)sBase[p])];
       PState<SPEC, N> s{sS + p * L.Wp};
       Delta d;
       eval_binding<SPEC, N>(s, cM, b, d);
-      if (!d.err) acc ^= delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]) + rank_below(sOrd + p * ordw, d.ordinal);
+      if (!d.err) acc ^= delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
     }
     if (acc == 0x123456789ULL) sSink = acc;
     __syncthreads();
@@ -289,22 +264,24 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     }
   }
 #endif
-  // ---- C: fingerprints + inserts, lane per successor.  The tile's enabled
-  //      (parent, binding) pairs are enumerated binding-major, so neighbouring
-  //      lanes run the same binding (the same action, for the fixed ones) of
-  //      different parents instead of diverging over the parent's actions.
+  // ---- C: fingerprints + inserts, lane per successor.  The tile's
+  //      successors are enumerated parent-major in TLC ordinal order, which
+  //      is exactly their order in the candidate buffer: lane idx writes
+  //      candidate gbase + idx, so a wave's candidate stores are contiguous
+  //      (binding-major enumeration scattered them: one 32 B write request per
+  //      8 B store, ~0.7 GB of extra HBM writes per launch on the bench cfg).
   for (int idx = tid; idx < total; idx += 256) {
-    int lo = 0, hi = nbind - 1;  // binding b: sBP[b] <= idx < sBP[b+1]
+    int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
     while (lo < hi) {
       int mid = (lo + hi + 1) >> 1;
-      if ((int)sBP[mid] <= idx) lo = mid; else hi = mid - 1;
+      if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
     }
-    const int b = lo;
-    const int p = select_bit(sEnT + 2 * b, idx - (int)sBP[b]);
+    const int p = lo;
+    const int b = cM.ord2b[select_bit(sOrd + p * ordw, idx - (int)sBase[p])];
     PState<SPEC, N> s{sS + p * L.Wp};
     Delta d;
     eval_binding<SPEC, N>(s, cM, b, d);
-    const unsigned long long t = gbase + sBase[p] + rank_below(sOrd + p * ordw, d.ordinal);
+    const unsigned long long t = gbase + (unsigned long long)idx;
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = CAND_DUP;
     if (!d.err) {
@@ -651,7 +628,7 @@ struct Launch {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
-    ExpandLds L = expand_lds(PB, M.words, M.nfixed + M.kmax, M.ord_words, (int)sizeof(MsgSums<N>));
+    ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(MsgSums<N>));
     hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.floor, a.sharded, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);

@@ -76,6 +76,7 @@ struct Model {
   int msg_act_slot[A_NUM];                   // action slot of each message action
   int ordinal_limit;
   int bind_words, ord_words;  // u32 words of a per-parent bitmask over bindings / over ordinals
+  uint16_t ord2b[1024];       // TLC ordinal -> binding (fixed bindings; message actions: nfixed + DOMAIN index)
 };
 
 // ------------------------------------------------------------- bit helpers

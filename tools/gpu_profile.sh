@@ -5,7 +5,7 @@
 # step has its own time limit; the script stops at the first failing step.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 WL=${WL:-raft_n3v2e2}
 CFG=${CFG:-Raft_n3v2e2}
 O=$R/gpurun_out/prof_$TAG
@@ -19,7 +19,14 @@ CLI="$R/raft-tlaplus_amd/build/raftmc -deadlock -json $R/configs/Raft.tla -confi
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc1 -o run --output-format csv -- $CLI > $O/pmc1.log 2>&1 || { echo "pmc1 failed"; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc2 -o run --output-format csv -- $CLI > $O/pmc2.log 2>&1 || { echo "pmc2 failed"; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $O/pmc3 -o run --output-format csv -- $CLI > $O/pmc3.log 2>&1 || { echo "pmc3 failed"; exit 1; }
+# counter calibration for random (non-streaming) accesses: known access counts
+CAL="$R/raft-tlaplus_amd/build/fpset_bench -calib -slots_log2 30 -batch 67108864"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/cal1 -o run --output-format csv -- $CAL > $O/cal1.log 2>&1 || { echo "cal1 failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/cal2 -o run --output-format csv -- $CAL > $O/cal2.log 2>&1 || { echo "cal2 failed"; exit 1; }
 cd $R
+python3 tools/pmc_summary.py $O/calib.json --pmc $(find $O/cal1 -name '*counter_collection.csv' | head -1) \
+  --pmc $(find $O/cal2 -name '*counter_collection.csv' | head -1) > /dev/null 2>&1
+grep calib $O/cal1.log
 python3 tools/pmc_summary.py $O/summary.json --workload $WL --stats $(ls $O/kt/*kernel_stats.csv | head -1) \
   --pmc $(find $O/pmc1 -name '*counter_collection.csv' | head -1) --pmc $(find $O/pmc2 -name '*counter_collection.csv' | head -1) \
   --pmc $(find $O/pmc3 -name '*counter_collection.csv' | head -1) > $O/summary.txt 2>&1
