@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--logical-shards", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0, help="parents per k_expand launch (0 = librmc's default)")
+    ap.add_argument("--fp-bits", type=int, default=64, choices=(64, 128),
+                    help="fingerprint width (128: confirms the 64-bit counts are collision-free)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -133,7 +135,7 @@ def main():
     elif args.logical_shards:
         run_check = lambda: model.check_logical(args.logical_shards)  # noqa: E731
     else:
-        run_check = lambda: model.check(chunk_parents=args.chunk)  # noqa: E731
+        run_check = lambda: model.check(chunk_parents=args.chunk, fp_bits=args.fp_bits)  # noqa: E731
 
     def barrier():
         if dist is not None:
@@ -202,7 +204,7 @@ def main():
                        "status": res["status"], "time_to_exhaust_s": per_step,
                        "first_check_s": cold[0] if cold else None,
                        "hidden_var_collisions": res["hidden_var_collisions"],
-                       "fpset_slots": res["hash_capacity"], "state_bytes": S},
+                       "fpset_slots": res["hash_capacity"], "state_bytes": S, "fp_bits": args.fp_bits},
             # achieved = B / t_wall with B = 2DS + 8G + 20D per check;
             # the dominant kernels' own shares per launch under "kernels"
             # (HIP-event launch times inside librmc)

@@ -41,7 +41,8 @@ typedef struct {
   int n_gpus;          /* GPUs used by this process (1; multi-GPU = one process per GPU) */
   int cpu_workers;     /* accepted for TLC CLI compatibility (-workers); unused by the GPU path */
   int deadlock_check;  /* 0 = TLC -deadlock (the reference's mode); 1 is rejected */
-  int fp_bits;         /* 64 (default) */
+  int fp_bits;         /* 64 (default, TLC's width) or 128 (rmc_check only): the first 64 bits are the
+                          64-bit fingerprint, the rest an independent hash of the same canonical view */
   int tlc_order;       /* 1 (default): first successor in TLC order wins per fingerprint */
   uint64_t hash_slots; /* initial fingerprint-set capacity, main tier (power of two; grows on demand); 0 = auto */
   uint32_t msg_cap_K;  /* message slots per packed state; 0 = auto */

@@ -65,6 +65,7 @@ int main(int argc, char** argv) {
     else if (k == "-chunk") o.chunk_parents = (uint32_t)atoi(val().c_str());
     else if (k == "-simulate") simulate = true;
     else if (k == "-cpu") cpu = true;
+    else if (k == "-fpwidth") o.fp_bits = atoi(val().c_str());  // 64 (TLC's) or 128
     else if (k == "-depth") sim_depth = (unsigned)atoi(val().c_str());
     else if (k == "-num") sim_num = strtoull(val().c_str(), nullptr, 10);
     else if (k == "-seed") sim_seed = strtoull(val().c_str(), nullptr, 10);
@@ -81,7 +82,7 @@ int main(int argc, char** argv) {
     else tla = k;
   }
   if (tla.empty()) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-fpwidth 64|128] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }

@@ -422,6 +422,7 @@ void finalize_model(rmc_model* m, uint32_t kmax) {
   if (words - 1 - 4 * M.N > 124) words -= 4;
   M.words = words;
   M.kmax = words - 1 - 4 * M.N;
+  M.fpw = 1;
   build_actions(M);
 }
 
@@ -683,10 +684,13 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   auto t0 = std::chrono::steady_clock::now();
   Model& M = m->M;
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
-  if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("only 64-bit fingerprints are supported");
+  if (opt->fp_bits && opt->fp_bits != 64 && opt->fp_bits != 128)
+    throw std::runtime_error("fp_bits must be 64 or 128");
   uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);
+  M.fpw = opt->fp_bits == 128 ? 2 : 1;
+  const int ew = 2 * M.fpw;  // fingerprint-set entry width in 64-bit words
   HIPCHK(upload_model(M));
   hipStream_t stream;
   HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -717,8 +721,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   DevBuf &poff = A.poff, &pn = A.pn, &pwin = A.pwin, &ppos = A.ppos, &counters = A.counters, &stbuf = A.stbuf;
   DevBuf& scantmp = A.scantmp;
   GrowBuf &fa = A.fa, &fb = A.fb, &trp = A.trp, &trb = A.trb;
-  table.ensure(slots * 16);
-  HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * 16, stream));
+  table.ensure(slots * ew * 8);
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * ew * 8, stream));
   fa.ensure(fcap * W * 4);
   fb.ensure(fcap * W * 4);
   cslot.ensure(cand_cap * 8);
@@ -762,14 +766,14 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     HIPCHK(hipStreamSynchronize(stream));
     bool grown = true;
     try {
-      A.table2.ensure(nslots * 16);
+      A.table2.ensure(nslots * ew * 8);
     } catch (OutOfDeviceMemory&) {
       grown = false;
     }
     if (!grown) return false;
-    HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * 16, stream));
+    HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * ew * 8, stream));
     launch_rehash(table.as<unsigned long long>(), slots, A.table2.as<unsigned long long>(), nslots - 1,
-                  stbuf.as<DevStatus>(), stream);
+                  stbuf.as<DevStatus>(), stream, ew);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(stream));
     std::swap(table.p, A.table2.p);
@@ -798,11 +802,18 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   std::vector<uint32_t> init = init_state(M);
   HIPCHK(hipMemcpyAsync(fa.p, init.data(), W * 4, hipMemcpyHostToDevice, stream));
   {
-    unsigned long long fp = host_fingerprint(M, init.data());
-    if (fp == ~0ULL) fp--;
-    const unsigned long long ent[2] = {fp, 0ULL};  // val 0: older than every successor
-    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + 2 * fp_slot(fp, slots - 1), ent, 16, hipMemcpyHostToDevice,
-                          stream));
+    unsigned long long ent[4];
+    if (M.fpw == 2) {
+      host_fingerprint2(M, init.data(), ent);  // (a, b)
+      ent[2] = 0ULL;                           // val 0: older than every successor
+      ent[3] = ~0ULL;
+    } else {
+      ent[0] = host_fingerprint(M, init.data());
+      if (ent[0] == ~0ULL) ent[0]--;
+      ent[1] = 0ULL;
+    }
+    HIPCHK(hipMemcpyAsync(table.as<unsigned long long>() + ew * fp_slot(ent[0], slots - 1), ent, ew * 8,
+                          hipMemcpyHostToDevice, stream));
     unsigned long long root = ~0ULL;
     uint16_t zero = 0;
     HIPCHK(hipMemcpyAsync(trp.p, &root, 8, hipMemcpyHostToDevice, stream));
@@ -829,6 +840,13 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   EventTimer te, tm, tz;
   double expand_ms = 0, mark_ms = 0, mat_ms = 0;
   unsigned long long expand_launches = 0, redos = 0;
+  // hidden-variable collisions counted up to the last chunk that was kept: a
+  // redone chunk's first k_mark has counted its collisions once already
+  unsigned long long coll_kept = 0;
+  auto restore_coll = [&]() {
+    HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, hidden_coll), &coll_kept, 8, hipMemcpyHostToDevice,
+                          stream));
+  };
   uint32_t* cur = fa.as<uint32_t>();
   uint32_t* nxt = fb.as<uint32_t>();
   double rate = 4.0;  // new states per parent of the previous level (pre-sizes the table per chunk)
@@ -926,7 +944,17 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       expand_launches++;
       HIPCHK(hipEventElapsedTime(&ms, te.b, tm.b));
       mark_ms += ms;
-      if (hst.cap_flags == (1u << E_CAP_TABLE) && !full_ok) {
+      if (hst.cap_flags == (1u << E_RETRY)) {
+        // fp_bits 128: a lane met a key whose second word was still in flight;
+        // redo the chunk (idempotent), every key it claimed is complete now
+        const unsigned zero = 0;
+        HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, cap_flags), &zero, 4, hipMemcpyHostToDevice, stream));
+        restore_coll();
+        HIPCHK(hipStreamSynchronize(stream));
+        redos++;
+        continue;
+      }
+      if ((hst.cap_flags & ~(1u << E_RETRY)) == (1u << E_CAP_TABLE) && !full_ok) {
         // the table filled up under this chunk: grow it and redo the chunk
         // (its inserts are idempotent; the next frontier was not touched)
         if (!t_grow(slots * 2)) {
@@ -937,6 +965,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         }
         const unsigned zero = 0;
         HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, cap_flags), &zero, 4, hipMemcpyHostToDevice, stream));
+        restore_coll();
         HIPCHK(hipStreamSynchronize(stream));
         redos++;
         continue;
@@ -953,12 +982,13 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
         static const char* names[] = {"", "", "log longer than the packed layout (5 entries)",
                                       "message capacity msg_cap_K exceeded", "message multiplicity > 7",
                                       "term > 15", "index field > 7", "successor buffer", "fingerprint set full",
-                                      "frontier capacity"};
+                                      "frontier capacity", "fingerprint retry"};
         status = 3;
         message = std::string("capacity overflow: ") + names[e];
         break;
       }
       chunk_log.push_back({c0, gen_lvl, next_n});
+      coll_kept = hst.hidden_coll;
       unsigned long long W_chunk = (unsigned long long)hrb->lastpos + hrb->lastwin;
       for (int sg = 0; sg < 8; sg++) ncand += hrb->segc[16 * sg];
       gen_lvl += ncand;
@@ -1073,6 +1103,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   // parents before it plus the failing parent's up to the failing one; distinct:
   // the winners among those.  An evaluation error in Next drops the failing
   // parent's successors (as the oracle's convention does).
+  DevStatus fin;  // before the recount below (which marks the failing chunk a second time)
+  HIPCHK(hipMemcpy(&fin, stbuf.p, sizeof fin, hipMemcpyDeviceToHost));
   if ((status == 1 || status == 2) && bad_key != ~0ULL && stop_front) {
     const unsigned long long pg = bad_key >> 20, li = pg - stop_level_base;
     const int ordv = (int)((bad_key >> 10) & 0x3FF);
@@ -1142,11 +1174,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     std::reverse(binds.begin(), binds.end());
     replay_trace(m, binds, last_b, status, message, res);
   }
-  {
-    DevStatus fin;
-    HIPCHK(hipMemcpy(&fin, stbuf.p, sizeof fin, hipMemcpyDeviceToHost));
-    res->hidden_var_collisions = fin.hidden_coll;
-  }
+  res->hidden_var_collisions = fin.hidden_coll;
   if (opt->verbose) {
     unsigned long long stp[8];
     read_stamps(stp);

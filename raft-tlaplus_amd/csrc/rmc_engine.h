@@ -50,8 +50,9 @@ struct LevelArgs {
 void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s);
 void launch_mark(const LevelArgs& a, hipStream_t s);
 void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s);
+// ew: entry width in 64-bit words (2: 64-bit fingerprints, 4: 128-bit)
 void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
-                   unsigned long long nmask, DevStatus* st, hipStream_t s);
+                   unsigned long long nmask, DevStatus* st, hipStream_t s, int ew = 2);
 
 size_t scan_temp_bytes(unsigned long long n);
 void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
@@ -84,6 +85,7 @@ void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long w
 int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,
                     int* err);
 unsigned long long host_fingerprint(const Model& M, const uint32_t* S);
+void host_fingerprint2(const Model& M, const uint32_t* S, unsigned long long* ab);  // 128-bit (fp_bits 128)
 int host_check_invariants(const Model& M, const uint32_t* S, int* err);
 int host_fp_check(const Model& M, const uint32_t* parent, int binding, const uint32_t* row);
 

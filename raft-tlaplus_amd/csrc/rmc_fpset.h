@@ -103,6 +103,68 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
   return EMPTY;
 }
 
+// fp_bits = 128: 32 B entries (fp.a, fp.b, val, unused).  The slot is claimed
+// by a CAS of the first word; the claimer then publishes the second.  A lane
+// that finds the first word equal must compare the second; if its claimer (in
+// another wave) has not published it after a bounded wait, the lane cannot
+// decide -- E_RETRY, and the driver redoes the chunk (idempotent; every key of
+// the chunk is complete by then).
+__device__ __forceinline__ unsigned long long fpset_insert128(unsigned long long* T, unsigned long long mask, Fp128 fp,
+                                                              unsigned long long val, unsigned long long floor,
+                                                              DevStatus* st) {
+  unsigned long long slot = fp_slot(fp.a, mask);
+  if (slot + 1 <= mask) {  // fast path: the first two entries of the run, plain loads
+    const ulonglong2* E = reinterpret_cast<const ulonglong2*>(T) + 2 * slot;
+    const ulonglong2 k0 = E[0], v0 = E[1], k1 = E[2], v1 = E[3];
+    int k = 2;
+    unsigned long long kv = 0;
+    bool found = false;
+    if (k1.x == fp.a || k1.x == EMPTY) { k = 1; kv = v1.x; found = k1.x == fp.a && k1.y == fp.b; }
+    if (k0.x == fp.a || k0.x == EMPTY) { k = 0; kv = v0.x; found = k0.x == fp.a && k0.y == fp.b; }
+    slot = (slot + (unsigned long long)k) & mask;
+    if (found) {
+      if (kv >= floor) atomicMin(T + 4 * slot + 2, val);
+      return slot;
+    }
+  }
+  const unsigned long long limit = mask < 4096 ? mask : 4096;
+  for (unsigned long long probe = 0; probe <= limit; probe++) {
+    unsigned long long* e = T + 4 * slot;
+    const unsigned long long prev = atomicCAS(e, EMPTY, fp.a);
+    const bool claimed = prev == EMPTY;
+    // One instruction for the whole wave: the claimer publishes its second
+    // word, every other lane reads it (CAS of EMPTY by EMPTY: no change).
+    // Lanes of one atomic instruction are served in lane order, as in the
+    // claiming CAS, so a same-wave duplicate reads the claimer's word;
+    // correctness does not depend on it (E_RETRY below).
+    unsigned long long lo = atomicCAS(e + 1, EMPTY, claimed ? fp.b : EMPTY);
+    if (claimed) {
+      atomicMin(e + 2, val);
+      return slot;
+    }
+    if (prev == fp.a) {
+      // claimed by another wave whose publish is one instruction behind its
+      // claim: wait a bounded while for it (no wave waits on this one)
+      for (int t = 0; lo == EMPTY && t < 64; t++) {
+        __builtin_amdgcn_s_sleep(2);
+        lo = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lo == EMPTY) {
+        atomicOr(&st->cap_flags, 1u << E_RETRY);
+        return EMPTY;
+      }
+      if (lo == fp.b) {
+        const unsigned long long cur = __hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur >= floor) atomicMin(e + 2, val);
+        return slot;
+      }
+    }
+    slot = (slot + 1) & mask;
+  }
+  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+  return EMPTY;
+}
+
 // The candidate word: CAND_DUP, or hidden << 47 | slot.
 __device__ __forceinline__ unsigned long long cand_word(unsigned long long slot, unsigned long long val) {
   return slot == EMPTY ? CAND_DUP : (((val & 0xFFFFULL) << 47) | slot);

@@ -26,6 +26,14 @@ static unsigned long long fp_t(const Model& M, const uint32_t* S) {
   PState<SPEC, N> s{S};
   return state_fp<SPEC, N>(s, M);
 }
+template <int SPEC, int N>
+static int fp2_t(const Model& M, const uint32_t* S, unsigned long long* ab) {
+  PState<SPEC, N> s{S};
+  const Fp128 f = state_fp2<SPEC, N>(s, M);
+  ab[0] = f.a;
+  ab[1] = f.b;
+  return 0;
+}
 
 // Test hook: the three ways the fingerprint of a successor is computed agree
 // (delta_fp from parent + delta, delta_fp_sums from the parent's message sums
@@ -46,7 +54,11 @@ static int fp_check_t(const Model& M, const uint32_t* parent, int b, const uint3
   const unsigned long long a = delta_fp<SPEC, N>(s, M, d), c = delta_fp_sums<SPEC, N>(s, M, d, ms);
   PState<SPEC, N> t{row};
   const unsigned long long f = state_fp<SPEC, N>(t, M);
-  return (a == f && c == f) ? 0 : 1;
+  // the 128-bit fingerprint: incremental (as k_expand<.., 2> computes it) == full, first word == the 64-bit one
+  MsgSums2<N> ms2{};
+  msg_sums2<SPEC, N>(s, ms2);
+  const Fp128 g = delta_fp_sums2<SPEC, N>(s, M, d, ms2), h = state_fp2<SPEC, N>(t, M);
+  return (a == f && c == f && g.a == h.a && g.b == h.b && g.a == f) ? 0 : 1;
 }
 
 template <int SPEC, int N>
@@ -86,6 +98,9 @@ int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_
 unsigned long long host_fingerprint(const Model& M, const uint32_t* S) {
   RMC_DISPATCH(fp_t, M, S);
   return 0;
+}
+void host_fingerprint2(const Model& M, const uint32_t* S, unsigned long long* ab) {
+  [&]() -> int { RMC_DISPATCH(fp2_t, M, S, ab); return -1; }();
 }
 int host_fp_check(const Model& M, const uint32_t* parent, int binding, const uint32_t* row) {
   RMC_DISPATCH(fp_check_t, M, parent, binding, row);

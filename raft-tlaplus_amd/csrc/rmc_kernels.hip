@@ -130,8 +130,21 @@ __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set 
 #ifndef RMC_EXPAND_WAVES
 #define RMC_EXPAND_WAVES 7
 #endif
-template <int SPEC, int N>
-__global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+// FPW: fingerprint width in 64-bit words (1, or 2 for fp_bits = 128).
+template <int N, int FPW>
+struct SumsOf {
+  using T = MsgSums<N>;
+};
+template <int N>
+struct SumsOf<N, 2> {
+  using T = MsgSums2<N>;
+};
+template <int N>
+__device__ __forceinline__ MsgSums<N>& sums1(MsgSums<N>& m) { return m; }
+template <int N>
+__device__ __forceinline__ MsgSums<N>& sums1(MsgSums2<N>& m) { return m.m; }
+template <int SPEC, int N, int FPW>
+__global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                 unsigned long long pbase, unsigned long long floor, int sharded,
                                                 unsigned long long* __restrict__ table, unsigned long long mask,
                                                 unsigned long long* __restrict__ cand_slot,
@@ -143,10 +156,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG, sSeg;
   const int tid = threadIdx.x;
+  using MS = typename SumsOf<N, FPW>::T;
   const int words = cM.words, ordw = cM.ord_words;
-  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MsgSums<N>));
+  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS));
   uint32_t* sS = (uint32_t*)lds;
-  MsgSums<N>* sMS = (MsgSums<N>*)(lds + L.off_Ms);
+  MS* sMS = (MS*)(lds + L.off_Ms);
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
   uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
@@ -161,7 +175,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     sS[p * L.Wp + (q - p * words)] = src[q];
   }
   for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
-  for (int q = tid; q < PB * (int)(sizeof(MsgSums<N>) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
+  for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
   __syncthreads();
   STAMP(0);
   // ---- B: enabled bindings, lane per parent
@@ -177,9 +191,15 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
       for (int k = tid / PB; k < nm; k += bstride) {
         int src, dst;
         const uint64_t u = msg_u<SPEC>(s.msg(k), src, dst);
-        atomicAdd(&sMS[p].sig[src], (uint32_t)u);
-        atomicAdd(&sMS[p].sig[dst], (uint32_t)(u >> 32));
-        if (src != dst) atomicAdd((unsigned long long*)&sMS[p].S[MsgSums<N>::pair(src, dst)], (unsigned long long)u);
+        MsgSums<N>& m1 = sums1<N>(sMS[p]);
+        atomicAdd(&m1.sig[src], (uint32_t)u);
+        atomicAdd(&m1.sig[dst], (uint32_t)(u >> 32));
+        if (src != dst) atomicAdd((unsigned long long*)&m1.S[MsgSums<N>::pair(src, dst)], (unsigned long long)u);
+        if constexpr (FPW == 2) {
+          if (src != dst)
+            atomicAdd((unsigned long long*)&sMS[p].S2[MsgSums<N>::pair(src, dst)],
+                      (unsigned long long)msg_u2<SPEC>(s.msg(k)));
+        }
       }
       for (int b = tid / PB; b < B; b += bstride) {
         Delta d;
@@ -253,7 +273,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
       PState<SPEC, N> s{sS + p * L.Wp};
       Delta d;
       eval_binding<SPEC, N>(s, cM, b, d);
-      if (!d.err) acc ^= delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
+      if constexpr (FPW == 2) {
+        if (!d.err) acc ^= delta_fp_sums2<SPEC, N>(s, cM, d, sMS[p]).b;
+      } else {
+        if (!d.err) acc ^= delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
+      }
     }
     if (acc == 0x123456789ULL) sSink = acc;
     __syncthreads();
@@ -285,15 +309,20 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = CAND_DUP;
     if (!d.err) {
-      unsigned long long fp = delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
       // TLC-order rank (parent global index, Next ordinal) above the hidden variables
       unsigned long long val = ((((pg + 1) << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
                                (unsigned long long)hidden_of<SPEC>(d.hdr);
-      if (sharded) {  // the fp's owner inserts it (k_insert_recv)
-        slot = fp;
-        cand_val[t] = val;
+      if constexpr (FPW == 2) {
+        const Fp128 fp = delta_fp_sums2<SPEC, N>(s, cM, d, sMS[p]);
+        slot = cand_word(fpset_insert128(table, mask, fp, val, floor, st), val);
       } else {
-        slot = cand_word(fpset_insert(table, mask, fp, val, floor, st), val);
+        unsigned long long fp = delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
+        if (sharded) {  // the fp's owner inserts it (k_insert_recv)
+          slot = fp;
+          cand_val[t] = val;
+        } else {
+          slot = cand_word(fpset_insert(table, mask, fp, val, floor, st), val);
+        }
       }
     }
     cand_slot[t] = slot;
@@ -309,7 +338,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? 4 : RMC_EXPAND_WAVES)) void k_expand
 // a hidden-variable collision (SURVEY.md §7 hard part 1), counted as the
 // oracles count them.
 __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsigned long long pbase,
-                                              unsigned long long floor, const unsigned long long* __restrict__ table,
+                                              unsigned long long floor, int ew,
+                                              const unsigned long long* __restrict__ table,
                                               const unsigned long long* __restrict__ cand_slot,
                                               const uint32_t* __restrict__ cand_ob,
                                               const uint32_t* __restrict__ par_off, const uint32_t* __restrict__ par_n,
@@ -330,7 +360,8 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
       const uint32_t t = t0 + u;
       ob[u] = t < off + n ? cand_ob[t] : OB_ERR;
       sl[u] = (ob[u] & OB_ERR) ? CAND_DUP : cand_slot[t];
-      v[u] = (sl[u] & CAND_DUP) ? ~0ULL : table[2 * (sl[u] & CAND_SLOT_MASK) + 1];
+      // entry = ew words, value in the word after the key (ew 2: fp, val; ew 4: fp.a, fp.b, val, -)
+      v[u] = (sl[u] & CAND_DUP) ? ~0ULL : table[ew * (sl[u] & CAND_SLOT_MASK) + (ew >> 1)];
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -625,11 +656,16 @@ int host_fp_owner(unsigned long long fp, int W) { return fp_owner(fp, W); }
 struct Launch {
   template <int SPEC, int N>
   static void expand(const LevelArgs& a, hipStream_t s) {
+    if (a.model->fpw == 2) return expand_w<SPEC, N, 2>(a, s);
+    return expand_w<SPEC, N, 1>(a, s);
+  }
+  template <int SPEC, int N, int FPW>
+  static void expand_w(const LevelArgs& a, hipStream_t s) {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
-    ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(MsgSums<N>));
-    hipLaunchKernelGGL((k_expand<SPEC, N>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
+    ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T));
+    hipLaunchKernelGGL((k_expand<SPEC, N, FPW>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.floor, a.sharded, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);
   }
@@ -666,25 +702,27 @@ void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatc
 void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, false, a, s); }
 void launch_mark(const LevelArgs& a, hipStream_t s) {
   unsigned long long blocks = (a.nparents + 255) / 256;
-  hipLaunchKernelGGL(k_mark, dim3((unsigned)blocks), dim3(256), 0, s, a.nparents, a.pbase, a.floor, a.table,
+  hipLaunchKernelGGL(k_mark, dim3((unsigned)blocks), dim3(256), 0, s, a.nparents, a.pbase, a.floor,
+                     a.model->fpw == 2 ? 4 : 2, a.table,
                      a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.cand_win, a.par_win, a.st);
 }
 // Move every entry of the fingerprint set into a larger one (values kept).
 // Grid-stride: a table of 2^32 slots or more would need a grid of 2^32
 // threads or more, past HIP's launch limit.
+// ew = entry width in words (2: fp, val; 4: fp.a, fp.b, val, -); every word moves.
 __global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __restrict__ old, unsigned long long nold,
-                                                unsigned long long* __restrict__ nt, unsigned long long mask,
+                                                unsigned long long* __restrict__ nt, unsigned long long mask, int ew,
                                                 DevStatus* st) {
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; e < nold; e += stride) {
-    unsigned long long k = old[2 * e];
+    unsigned long long k = old[ew * e];
     if (k == EMPTY) continue;
     unsigned long long slot = fp_slot(k, mask);
     unsigned long long probe = 0;
     for (; probe <= mask; probe++) {
-      unsigned long long prev = atomicCAS(nt + 2 * slot, EMPTY, k);
+      unsigned long long prev = atomicCAS(nt + ew * slot, EMPTY, k);
       if (prev == EMPTY) {
-        nt[2 * slot + 1] = old[2 * e + 1];
+        for (int w = 1; w < ew; w++) nt[ew * slot + w] = old[ew * e + w];
         break;
       }
       slot = (slot + 1) & mask;
@@ -693,10 +731,10 @@ __global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __rest
   }
 }
 void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
-                   unsigned long long nmask, DevStatus* st, hipStream_t s) {
+                   unsigned long long nmask, DevStatus* st, hipStream_t s, int ew) {
   unsigned long long blocks = (nold + 255) / 256;
   if (blocks > (1ULL << 22)) blocks = 1ULL << 22;  // 2^30 threads, each striding
-  hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, s, old, nold, nt, nmask, st);
+  hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, s, old, nold, nt, nmask, ew, st);
 }
 size_t scan_temp_bytes(unsigned long long n) {
   size_t bytes = 0;

@@ -205,7 +205,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   auto t0 = std::chrono::steady_clock::now();
   Model& M = m->M;
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
-  if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("only 64-bit fingerprints are supported");
+  if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("fp_bits 128 is offered by the single-GPU search (rmc_check) only");
   uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);
@@ -215,7 +215,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   const size_t WD = (size_t)M.words;
   res->state_bytes = (uint32_t)(WD * 4);
   const int maxsucc = M.nfixed + M.kmax;
-  const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 21);
+  const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 22);
   const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
   const int NL = (int)comm.local.size();
   if (W > 64) throw std::runtime_error("at most 64 shards");
@@ -299,8 +299,17 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     if (err) { status = 2; message = "evaluation error in an invariant on the initial state"; bad_state = 0; }
     else if (bad >= 0) { status = 1; snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str()); bad_state = 0; }
   }
-  EventTimer te, tz;
+  // per-shard kernel timers, read after the round's next stream sync (no sync of their own)
+  std::vector<EventTimer> te(NL), tz(NL);
+  std::vector<char> te_on(NL, 0), tz_on(NL, 0);
   double expand_ms = 0, mat_ms = 0;
+  auto read_timers = [&]() {
+    for (int i = 0; i < NL; i++) {
+      float ms = 0;
+      if (te_on[i]) { HIPCHK(hipEventElapsedTime(&ms, te[i].a, te[i].b)); expand_ms += ms; te_on[i] = 0; }
+      if (tz_on[i]) { HIPCHK(hipEventElapsedTime(&ms, tz[i].a, tz[i].b)); mat_ms += ms; tz_on[i] = 0; }
+    }
+  };
   unsigned long long expand_launches = 0;
   std::vector<std::vector<uint64_t>> rows(NL);
   std::vector<uint64_t> all;
@@ -321,7 +330,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     const unsigned long long floor = (lbase + 1) << VAL_FLOOR_SHIFT;  // entries below: earlier levels
     for (unsigned long long c = 0; c < rounds && !stop; c++) {
       // ---- expand: fp + key per candidate
-      for (Shard& s : sh) {
+      for (int si = 0; si < NL; si++) {
+        Shard& s = sh[si];
         s.n = s.ncur > c * CH ? std::min(CH, s.ncur - c * CH) : 0;
         HIPCHK(hipMemsetAsync(s.B->counters.p, 0, 64, stream));
         if (s.n) {
@@ -341,20 +351,18 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           a.counters = s.B->counters.as<unsigned long long>();
           a.cand_cap = cand_cap;
           a.st = s.B->stbuf.as<DevStatus>();
-          HIPCHK(hipEventRecord(te.a, stream));
+          HIPCHK(hipEventRecord(te[si].a, stream));
           launch_expand(M.spec, M.N, a, stream);
           HIPCHK(hipGetLastError());
-          HIPCHK(hipEventRecord(te.b, stream));
-          HIPCHK(hipEventSynchronize(te.b));
-          float ms = 0;
-          HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
-          expand_ms += ms;
+          HIPCHK(hipEventRecord(te[si].b, stream));
+          te_on[si] = 1;
           expand_launches++;
         }
         HIPCHK(hipMemcpyAsync(&s.ncand, s.B->counters.p, 8, hipMemcpyDeviceToHost, stream));
         read_status(s);
       }
       HIPCHK(hipStreamSynchronize(stream));
+      read_timers();
       for (int i = 0; i < NL; i++) rows[i] = {sh[i].ncand, sh[i].hst.cap_flags};
       comm.allgather(rows, all, 2);
       unsigned capf = 0;
@@ -491,7 +499,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       std::vector<unsigned long long> go(W + 1, 0);
       for (int r = 0; r < W; r++) go[r + 1] = go[r] + all[r];
       // ---- materialize winners into staging (TLC order within the generator)
-      for (Shard& s : sh) {
+      for (int si = 0; si < NL; si++) {
+        Shard& s = sh[si];
         if (!s.n || !s.nwin) continue;
         s.B->stage.ensure(s.nwin * WD * 4);
         s.B->stp.ensure(s.nwin * 8);
@@ -513,14 +522,11 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         a.tr_parent = s.B->stp.as<unsigned long long>();
         a.tr_bind = s.B->stb.as<uint16_t>();
         a.st = s.B->stbuf.as<DevStatus>();
-        HIPCHK(hipEventRecord(tz.a, stream));
+        HIPCHK(hipEventRecord(tz[si].a, stream));
         launch_materialize(M.spec, M.N, a, stream);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(tz.b, stream));
-        HIPCHK(hipEventSynchronize(tz.b));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, tz.a, tz.b));
-        mat_ms += ms;
+        HIPCHK(hipEventRecord(tz[si].b, stream));
+        tz_on[si] = 1;
       }
       // ---- rows + trace records to their next-level owners (block-cyclic by global position)
       {
@@ -584,6 +590,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       // ---- first problem in TLC order stops the search (as TLC does)
       for (Shard& s : sh) read_status(s);
       HIPCHK(hipStreamSynchronize(stream));
+      read_timers();
       for (int i = 0; i < NL; i++)
         rows[i] = {sh[i].hst.err_key, sh[i].hst.inv_err_key, sh[i].hst.viol_key,
                    sh[i].hst.cap_flags | ((unsigned long long)sh[i].hst.max_msgs << 32)};

@@ -59,7 +59,7 @@ enum ErrCode {
   E_CAP_SUCC = 7,   // more successors for one state than the candidate buffer holds
   E_CAP_TABLE = 8,  // fingerprint set full
   E_CAP_FRONTIER = 9,
-  E_CAP_LEVEL = 10   // fingerprint set: level tier full (the driver grows it and redoes the chunk)
+  E_RETRY = 10  // fp_bits 128: a key's second word was read before its claimer stored it (the chunk is redone)
 };
 constexpr int NILS = 7;
 constexpr int MAXN = 7, MAXV = 4, MAXLOG = 5, MAXOPS = 7, MAXPERM = 120, MAXACT = 16, MAXFIXED = 192;
@@ -75,6 +75,7 @@ struct Model {
   uint8_t fb_act[MAXFIXED], fb_x[MAXFIXED];  // fixed binding -> (action slot, binding index)
   int msg_act_slot[A_NUM];                   // action slot of each message action
   int ordinal_limit;
+  int fpw;                    // fingerprint width in 64-bit words (1: 64-bit, 2: 128-bit)
   int bind_words, ord_words;  // u32 words of a per-parent bitmask over bindings / over ordinals
   uint16_t ord2b[1024];       // TLC ordinal -> binding (fixed bindings; message actions: nfixed + DOMAIN index)
 };
@@ -1258,6 +1259,164 @@ RMC_HD uint64_t delta_fp_sums(const PState<SPEC, N>& s, const Model& M, const De
     msg_contrib<SPEC, N>(d.opc[q], false, sig, S);
   }
   return canon_from_sums<SPEC, N>(M, V, sig, S);
+}
+
+// ------------------------------------------------ 128-bit fingerprints
+// fp_bits = 128 (SURVEY.md §7 hard part 2: min-of-hashes over permutations
+// raises the collision rate, so a wider mode is offered).  The first word is
+// the 64-bit fingerprint above, unchanged; the second is an independent
+// 64-bit hash of the same relabelled view (other finalizer, other constants,
+// its own message multiset sums S2), taken at the same permutation -- the
+// one minimising (first word, second word).  Orbit invariance holds for the
+// pair exactly as for the first word.
+struct Fp128 {
+  uint64_t a, b;
+};
+RMC_HD bool fp128_less(const Fp128& x, const Fp128& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }
+RMC_HD uint64_t mix64b(uint64_t z) {  // MurmurHash3 fmix64
+  z ^= z >> 33;
+  z *= 0xff51afd7ed558ccdULL;
+  z ^= z >> 33;
+  z *= 0xc4ceb9fe1a85ec53ULL;
+  return z ^ (z >> 33);
+}
+template <int SPEC>
+RMC_HD uint64_t msg_u2(uint32_t w) {  // the second word's hash of a message body (servers masked)
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  return mix64b((uint64_t)(w & ~((7u << sp) | (7u << dp))) * 0x9FB21C651E98DF25ULL + 0x2545F4914F6CDD1DULL);
+}
+template <int SPEC, int N>
+RMC_HD uint64_t h_server2(uint32_t P, int i, uint32_t a, uint32_t b, uint32_t c, uint32_t dd) {
+  int v = a_voted(a);
+  uint32_t a2 = setb(a, 6, 3, v == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v));
+  a2 = setb(a2, 18, 7, relabel_set<N>(a_votes(a), P));
+  a2 = setb(a2, 25, 7, relabel_set<N>(a_pending(a), P));
+  uint64_t lo = (uint64_t)a2 | ((uint64_t)b << 32);
+  uint64_t hi = (uint64_t)relabel_row<N>(c, P) | ((uint64_t)relabel_row<N>(dd, P) << 32);
+  int pos = perm_of(P, i);
+  return mix64b(mix64b(lo ^ (0xD1B54A32D192ED03ULL * (uint64_t)(pos + 1))) + hi);
+}
+// The parent's message sums for both words.
+template <int N>
+struct MsgSums2 {
+  MsgSums<N> m;              // first word's sums and the signatures (as MsgSums)
+  uint64_t S2[N * (N - 1)];  // second word's pair sums
+};
+template <int SPEC, int N>
+RMC_HD void msg_contrib2(uint32_t w, bool neg, uint64_t (&S2)[N][N]) {
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  const int src = (int)((w >> sp) & 7u), dst = (int)((w >> dp) & 7u);
+  uint64_t u = msg_u2<SPEC>(w);
+  if (neg) u = 0ULL - u;
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++)
+      if (i != j) S2[i][j] += (i == src && j == dst) ? u : 0ULL;
+}
+template <int SPEC, int N>
+RMC_HD Fp128 canon_from_sums2(const Model& M, const DeltaView<SPEC, N>& V, const uint32_t (&sig)[N],
+                              const uint64_t (&S)[N][N], const uint64_t (&S2)[N][N]) {
+  bool ties;
+  const uint32_t P0 = sig_perm<N>(sig, ties);
+  const uint64_t aux = SPEC == PULL ? h_acked_view(V.d.hdr) : 0ULL;
+  const uint64_t aux2 = SPEC == PULL ? mix64b(((uint64_t)(V.d.hdr >> 16) & 0xFFu) + 0x8CB92BA72F3D8DD7ULL) : 0ULL;
+  Fp128 best{~0ULL, ~0ULL};
+  const int np = ties ? M.nperm : 1;
+#pragma unroll 1
+  for (int p = 0; p < np; p++) {
+    uint32_t P = P0;
+    if (ties) {
+      P = M.perm[p];
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < N; j++)
+#pragma unroll
+        for (int k = 0; k < N; k++)
+          if (sig[j] < sig[k] && perm_of(P, j) > perm_of(P, k)) ok = false;
+      if (!ok) continue;
+    }
+    uint64_t h = aux, h2 = aux2;
+#pragma unroll 1
+    for (int i = 0; i < N; i++) {
+      h += h_server<SPEC, N>(P, i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
+      h2 += h_server2<SPEC, N>(P, i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3));
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++)
+#pragma unroll
+      for (int j = 0; j < N; j++)
+        if (i != j) {
+          const uint64_t key = (uint64_t)(8 * perm_of(P, i) + perm_of(P, j) + 1);
+          h += mix64(S[i][j] + 0x9E3779B97F4A7C15ULL * key);
+          h2 += mix64b(S2[i][j] + 0xC2B2AE3D27D4EB4FULL * key);
+        }
+    const Fp128 f{mix64(h), mix64b(h2)};
+    if (fp128_less(f, best)) best = f;
+  }
+  if (best.a == ~0ULL) best.a--;  // ~0 marks an empty slot (first word) / a claim in flight (second word)
+  if (best.b == ~0ULL) best.b--;
+  return best;
+}
+// delta_fp_sums for both words (the first equals delta_fp_sums bit for bit).
+template <int SPEC, int N>
+RMC_HD Fp128 delta_fp_sums2(const PState<SPEC, N>& s, const Model& M, const Delta& d, const MsgSums2<N>& ms) {
+  const DeltaView<SPEC, N> V{s, d};
+  uint32_t sig[N];
+  uint64_t S[N][N], S2[N][N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    sig[i] = server_sig_own<SPEC, N>(i, V.sw(i, 0), V.sw(i, 1), V.sw(i, 2), V.sw(i, 3)) + ms.m.sig[i];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      S[i][j] = i == j ? 0ULL : ms.m.S[MsgSums<N>::pair(i, j)];
+      S2[i][j] = i == j ? 0ULL : ms.S2[MsgSums<N>::pair(i, j)];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXOPS; q++) {
+    if (q >= d.nops) continue;
+    const int k = d.opk[q];
+    if (k >= 0) {
+      bool last = true;
+#pragma unroll
+      for (int r = q + 1; r < MAXOPS; r++)
+        if (r < d.nops && d.opk[r] == k) last = false;
+      if (!last) continue;
+      msg_contrib<SPEC, N>(s.msg(k), true, sig, S);
+      msg_contrib2<SPEC, N>(s.msg(k), true, S2);
+    }
+    msg_contrib<SPEC, N>(d.opc[q], false, sig, S);
+    msg_contrib2<SPEC, N>(d.opc[q], false, S2);
+  }
+  return canon_from_sums2<SPEC, N>(M, V, sig, S, S2);
+}
+// The parent's message sums for both words (k_expand builds the same in LDS).
+template <int SPEC, int N>
+RMC_HD void msg_sums2(const PState<SPEC, N>& s, MsgSums2<N>& ms) {
+  for (int k = 0; k < s.nmsg(); k++) {
+    int src, dst;
+    const uint64_t u = msg_u<SPEC>(s.msg(k), src, dst);
+    ms.m.sig[src] += (uint32_t)u;
+    ms.m.sig[dst] += (uint32_t)(u >> 32);
+    if (src != dst) {
+      ms.m.S[MsgSums<N>::pair(src, dst)] += u;
+      ms.S2[MsgSums<N>::pair(src, dst)] += msg_u2<SPEC>(s.msg(k));
+    }
+  }
+}
+// 128-bit canonical fp of a full packed state.
+template <int SPEC, int N>
+RMC_HD Fp128 state_fp2(const PState<SPEC, N>& s, const Model& M) {
+  Delta d;
+  d.srv = -1;
+  d.nops = 0;
+  d.hdr = s.hdr();
+  MsgSums2<N> ms{};
+  msg_sums2<SPEC, N>(s, ms);
+  return delta_fp_sums2<SPEC, N>(s, M, d, ms);
 }
 
 // Canonical fp of the successor parent + delta.

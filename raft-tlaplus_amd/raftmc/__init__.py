@@ -117,7 +117,7 @@ class Model:
 
     def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
                  chunk_parents=0, verbose=False, max_depth=0, workers=0, grow_on_overflow=False,
-                 time_limit=0.0):
+                 time_limit=0.0, fp_bits=64):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
@@ -126,6 +126,7 @@ class Model:
         o.chunk_parents, o.verbose, o.max_depth, o.cpu_workers = chunk_parents, int(verbose), max_depth, workers
         o.grow_on_overflow = int(grow_on_overflow)
         o.time_limit = float(time_limit)
+        o.fp_bits = int(fp_bits)
         return o
 
     def _result(self, rc, r):

@@ -93,3 +93,14 @@ def test_message_capacity_rerun(name):
     assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
         (g["generated"], g["distinct"], g["depth"], g["levels"])
     assert r["max_msgs"] == g["max_msgs"]
+
+
+@pytest.mark.parametrize("name", ["fsync_n2v2e2r1_hidden", "raft_n2v2e2r2_order"])
+@pytest.mark.parametrize("fp_bits", [64, 128])
+def test_first_wins_through_redos(name, fp_bits):
+    """Chunks redone after the fingerprint set overflows: the TLC-order winners
+    and the hidden-variable collision count (a redone chunk's collisions
+    counted once) are unchanged."""
+    g = ORDER[name]
+    same(raftmc.check_text(g["module"], g["cfg"], hash_slots=256, grow_on_overflow=True, chunk_parents=300,
+                           fp_bits=fp_bits), g)
