@@ -45,6 +45,7 @@ int main(int argc, char** argv) {
   o.deadlock_check = 1;  // TLC default; the reference always passes -deadlock
   std::string tla, cfg;
   bool json = false, simulate = false, cpu = false;
+  int shards = 0;  // > 0: the fingerprint-sharded protocol with this many logical shards on one GPU
   std::string dump_fmt, dump_file;
   unsigned long long sim_walkers = 1ULL << 20, sim_num = 0, sim_seed = 0;
   unsigned sim_depth = 100;
@@ -65,6 +66,7 @@ int main(int argc, char** argv) {
     else if (k == "-chunk") o.chunk_parents = (uint32_t)atoi(val().c_str());
     else if (k == "-simulate") simulate = true;
     else if (k == "-cpu") cpu = true;
+    else if (k == "-shards") shards = atoi(val().c_str());
     else if (k == "-fpwidth") o.fp_bits = atoi(val().c_str());  // 64 (TLC's) or 128
     else if (k == "-depth") sim_depth = (unsigned)atoi(val().c_str());
     else if (k == "-num") sim_num = strtoull(val().c_str(), nullptr, 10);
@@ -82,7 +84,7 @@ int main(int argc, char** argv) {
     else tla = k;
   }
   if (tla.empty()) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-fpwidth 64|128] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }
@@ -121,7 +123,7 @@ int main(int argc, char** argv) {
     return r.status == 0 ? 0 : (r.status == 1 ? 12 : 13);
   }
   printf("raftmc %s: model checking %s\n", rmc_version(), tla.c_str());
-  int rc = cpu ? rmc_check_cpu(m, &o, &r) : rmc_check(m, &o, &r);
+  int rc = cpu ? rmc_check_cpu(m, &o, &r) : shards > 0 ? rmc_check_logical(m, &o, shards, &r) : rmc_check(m, &o, &r);
   if (rc != 0) {
     fprintf(stderr, "raftmc: %s\n", rmc_last_error());
     rmc_model_free(m);

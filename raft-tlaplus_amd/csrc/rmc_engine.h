@@ -30,11 +30,12 @@ struct LevelArgs {
   unsigned long long nparents, pbase;
   unsigned level;  // level of the successors (parents are level-1)
   unsigned long long floor;  // (first global index of the parents' level) << 26: entries below are older
-  int sharded;               // 1: k_expand leaves the fingerprint-set insert to the fp's owner
+  int sharded;               // W > 0 shards: k_expand inserts only the fps this shard owns, the owners the rest
+  int shard_self;            // this shard's id (sharded search)
   unsigned long long* table;  // fingerprint set: (fp, val) entries
   unsigned long long mask;
-  unsigned long long* cand_slot;  // single shard: CAND_DUP or hidden << 47 | slot; sharded: the candidate's fp
-  unsigned long long* cand_val;   // sharded: the candidate's TLC-order rank << 16 | hidden variables (rmc_fpset.h)
+  unsigned long long* cand_slot;  // CAND_DUP or hidden << 47 | slot; sharded, remote owner: the candidate's fp
+  unsigned long long* cand_val;   // sharded: remote owner: rank << 16 | hidden (rmc_fpset.h); local: the fp
   uint32_t* cand_ob;
   uint16_t* cand_win;
   uint32_t *par_off, *par_n, *par_win, *par_pos;
@@ -73,8 +74,11 @@ void launch_insert_recv(const unsigned long long* recv, unsigned long long n, un
 void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
                       const unsigned long long* table, unsigned long long floor, uint8_t* flag,
                       unsigned long long* newcount, DevStatus* st, hipStream_t s);
-void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
-                     const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s);
+// k_mark for the sharded search: a (cand_ob, cand_slot, cand_val,
+// par_off/par_n -> cand_win/par_win, table/mask/floor, pbase, st); moved = the
+// table grew since k_expand (local-owner candidates are found by fp)
+void launch_mark_gen(const LevelArgs& a, int moved, const uint32_t* perm, const uint8_t* flag_back,
+                     unsigned long long* newcount, hipStream_t s);
 int host_fp_owner(unsigned long long fp, int W);
 void read_stamps(unsigned long long* out);  // -DRMC_STAMPS diagnostic builds
 void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long walkers, unsigned depth,

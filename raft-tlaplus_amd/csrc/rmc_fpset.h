@@ -46,6 +46,12 @@ __host__ __device__ __forceinline__ unsigned long long fp_slot(unsigned long lon
   return ((fp * 0x9E3779B97F4A7C15ULL) >> sh) & mask;
 }
 
+// Owner of a fingerprint among W shards (sharded search): multiply-shift range
+// reduction of the high word (independent of the slot, which is a hash of all of fp).
+__host__ __device__ __forceinline__ int fp_owner(unsigned long long fp, int W) {
+  return (int)(((fp >> 32) * (unsigned long long)W) >> 32);
+}
+
 // Insert fp with value val; returns the slot, or EMPTY when the probe run is
 // too long (the table is too full: the driver grows it and redoes the chunk,
 // whose inserts are idempotent).
@@ -100,6 +106,19 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
     slot = (slot + 1) & mask;
   }
   atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+  return EMPTY;
+}
+
+// The value of fp's entry (~0 if absent): read-only probe.
+__device__ __forceinline__ unsigned long long fpset_value(const unsigned long long* T, unsigned long long mask,
+                                                          unsigned long long fp) {
+  unsigned long long slot = fp_slot(fp, mask);
+  for (unsigned long long probe = 0; probe <= mask; probe++) {
+    const ulonglong2 e = reinterpret_cast<const ulonglong2*>(T)[slot];
+    if (e.x == fp) return e.y;
+    if (e.x == EMPTY) break;
+    slot = (slot + 1) & mask;
+  }
   return EMPTY;
 }
 

@@ -31,7 +31,8 @@ __constant__ Model cM;
 constexpr int WAVE = 64;
 constexpr int EXPAND_SEGS = 8;  // candidate-buffer segments of the single-shard k_expand (one per XCD)
 // cand_ob = ordinal << 16 | flags | binding (10 bits)
-constexpr uint32_t OB_ERR = 0x8000u;  // evaluation error: no successor
+constexpr uint32_t OB_ERR = 0x8000u;    // evaluation error: no successor
+constexpr uint32_t OB_LOCAL = 0x4000u;  // sharded search: this shard owns the fp and k_expand inserted it
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -146,6 +147,7 @@ __device__ __forceinline__ MsgSums<N>& sums1(MsgSums2<N>& m) { return m.m; }
 template <int SPEC, int N, int FPW>
 __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                 unsigned long long pbase, unsigned long long floor, int sharded,
+                                                int shard_self,
                                                 unsigned long long* __restrict__ table, unsigned long long mask,
                                                 unsigned long long* __restrict__ cand_slot,
                                                 uint32_t* __restrict__ cand_ob, uint32_t* __restrict__ par_off,
@@ -308,6 +310,7 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
     const unsigned long long t = gbase + (unsigned long long)idx;
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = CAND_DUP;
+    uint32_t local = 0;
     if (!d.err) {
       // TLC-order rank (parent global index, Next ordinal) above the hidden variables
       unsigned long long val = ((((pg + 1) << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
@@ -317,16 +320,24 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
         slot = cand_word(fpset_insert128(table, mask, fp, val, floor, st), val);
       } else {
         unsigned long long fp = delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
-        if (sharded) {  // the fp's owner inserts it (k_insert_recv)
-          slot = fp;
-          cand_val[t] = val;
+        if (sharded) {  // the fp's owner inserts it: here when that is this shard, else k_insert_recv
+          if (fp_owner(fp, sharded) == shard_self) {
+            // as the single-shard search (a full table flags E_CAP_TABLE: the
+            // round is redone), plus the fp: the table may grow before k_mark_gen
+            slot = cand_word(fpset_insert(table, mask, fp, val, floor, st), val);
+            cand_val[t] = fp;
+            local = OB_LOCAL;
+          } else {
+            slot = fp;
+            cand_val[t] = val;
+          }
         } else {
           slot = cand_word(fpset_insert(table, mask, fp, val, floor, st), val);
         }
       }
     }
     cand_slot[t] = slot;
-    cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : 0u);
+    cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : local);
   }
   STAMP(3);
 }
@@ -501,13 +512,8 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
 }
 
 // ------------------------------------------------- sharded search
-// Owner of a fingerprint among W shards: multiply-shift range reduction of the
-// high word (the table slot uses the low bits, so the two are independent).
-__host__ __device__ __forceinline__ int fp_owner(unsigned long long fp, int W) {
-  return (int)(((fp >> 32) * (unsigned long long)W) >> 32);
-}
-
-// Bucketing by owner without global atomics: per-block LDS histograms land in
+// Bucketing by owner (the remote candidates only: k_expand inserted the
+// local-owner ones) without global atomics: per-block LDS histograms land in
 // an owner-major [W][nblocks] array; its exclusive scan gives every (owner,
 // block) pair its offset in the send buffer (= owner segment + earlier blocks).
 constexpr int BUCKET_MAXW = 64;
@@ -519,7 +525,7 @@ __global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* _
   if (threadIdx.x < W) h[threadIdx.x] = 0;
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n && !(cand_ob[t] & OB_ERR)) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
+  if (t < n && !(cand_ob[t] & (OB_ERR | OB_LOCAL))) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
   __syncthreads();
   if (threadIdx.x < W) blk_counts[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
@@ -537,7 +543,7 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  if (cand_ob[t] & OB_ERR) {
+  if (cand_ob[t] & (OB_ERR | OB_LOCAL)) {
     perm[t] = 0xFFFFFFFFu;
     return;
   }
@@ -588,33 +594,76 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
   if (threadIdx.x == 0 && c) atomicAdd(newcount, (unsigned long long)c);
 }
 
-// Generator side: per parent, winners (flags returned in send order) ranked
-// in TLC ordinal order, as k_mark does for the single-shard search.
-__global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, const uint32_t* __restrict__ par_off,
+// Generator side: per parent, winners ranked in TLC ordinal order, as k_mark
+// does for the single-shard search.  A remote-owner candidate's outcome is the
+// owner's flag (returned in send order); a local-owner one is read from this
+// shard's table at the slot k_expand recorded -- or, when the table grew since
+// (`moved`), found again by its fp -- with the same-level hidden-variable
+// collisions counted as k_mark counts them.  newcount += local winners (=
+// entries they added).
+__global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, unsigned long long pbase,
+                                                  const uint32_t* __restrict__ par_off,
                                                   const uint32_t* __restrict__ par_n,
+                                                  const uint32_t* __restrict__ cand_ob,
+                                                  const unsigned long long* __restrict__ cand_fp,
+                                                  const unsigned long long* __restrict__ cand_val,
                                                   const uint32_t* __restrict__ perm,
                                                   const uint8_t* __restrict__ flag_back,
-                                                  uint16_t* __restrict__ cand_win, uint32_t* __restrict__ par_win) {
-  unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= nparents) return;
-  uint32_t off = par_off[p], n = par_n[p], cnt = 0;
-  constexpr int U = 8;  // independent flag reads issued together, as in k_mark
-  for (uint32_t t0 = off; t0 < off + n; t0 += U) {
-    bool w[U];
+                                                  const unsigned long long* __restrict__ table, unsigned long long mask,
+                                                  unsigned long long floor, int moved, uint16_t* __restrict__ cand_win,
+                                                  uint32_t* __restrict__ par_win, unsigned long long* __restrict__ newcount,
+                                                  DevStatus* st) {
+  const unsigned long long p = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t nloc = 0, coll = 0;
+  if (p < nparents) {
+    const uint32_t off = par_off[p], n = par_n[p];
+    uint32_t cnt = 0;
+    const unsigned long long base = (pbase + p + 1) << 10;
+    constexpr int U = 8;  // independent reads issued together, as in k_mark
+    for (uint32_t t0 = off; t0 < off + n; t0 += U) {
+      uint32_t ob[U];
+      bool w[U];
+      unsigned long long v[U], mine[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t t = t0 + u;
-      const uint32_t q = t < off + n ? perm[t] : 0xFFFFFFFFu;
-      w[u] = q != 0xFFFFFFFFu && flag_back[q];
-    }
+      for (int u = 0; u < U; u++) {
+        const uint32_t t = t0 + u;
+        ob[u] = t < off + n ? cand_ob[t] : OB_ERR;
+        w[u] = false;
+        v[u] = mine[u] = 0;
+        if (ob[u] & OB_ERR) continue;
+        if (ob[u] & OB_LOCAL) {
+          mine[u] = cand_fp[t];  // hidden << 47 | slot, or CAND_DUP (the insert failed: the round was redone)
+          if (mine[u] & CAND_DUP) { ob[u] |= OB_ERR; continue; }
+          v[u] = moved ? fpset_value(table, mask, cand_val[t]) : table[2 * (mine[u] & CAND_SLOT_MASK) + 1];
+          mine[u] >>= 47;
+        } else {
+          const uint32_t q = perm[t];
+          w[u] = flag_back[q] != 0;
+        }
+      }
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t t = t0 + u;
-      if (t >= off + n) break;
-      cand_win[t] = w[u] ? (uint16_t)(++cnt) : (uint16_t)0;
+      for (int u = 0; u < U; u++) {
+        const uint32_t t = t0 + u;
+        if (t >= off + n) break;
+        if ((ob[u] & (OB_ERR | OB_LOCAL)) == OB_LOCAL) {
+          bool c = false;
+          w[u] = fpset_won(v[u], base | (ob[u] >> 16), floor, mine[u], c);
+          coll += c ? 1u : 0u;
+          nloc += w[u] ? 1u : 0u;
+        }
+        cand_win[t] = w[u] ? (uint16_t)(++cnt) : (uint16_t)0;
+      }
     }
+    par_win[p] = cnt;
   }
-  par_win[p] = cnt;
+  __shared__ unsigned int sn, sc;
+  if (threadIdx.x == 0) sn = sc = 0;
+  __syncthreads();
+  if (nloc) atomicAdd(&sn, nloc);
+  if (coll) atomicAdd(&sc, coll);
+  __syncthreads();
+  if (threadIdx.x == 0 && sn) atomicAdd(newcount, (unsigned long long)sn);
+  if (threadIdx.x == 0 && sc) atomicAdd(&st->hidden_coll, (unsigned long long)sc);
 }
 
 unsigned long long bucket_blocks(unsigned long long n) { return n ? (n + 255) / 256 : 1; }
@@ -644,11 +693,12 @@ void launch_mark_recv(const unsigned long long* recv, const unsigned long long* 
   hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, recv_slot, n, table, floor,
                      flag, newcount, st);
 }
-void launch_mark_gen(unsigned long long nparents, const uint32_t* par_off, const uint32_t* par_n, const uint32_t* perm,
-                     const uint8_t* flag_back, uint16_t* cand_win, uint32_t* par_win, hipStream_t s) {
-  if (!nparents) return;
-  hipLaunchKernelGGL(k_mark_gen, dim3((unsigned)((nparents + 255) / 256)), dim3(256), 0, s, nparents, par_off, par_n,
-                     perm, flag_back, cand_win, par_win);
+void launch_mark_gen(const LevelArgs& a, int moved, const uint32_t* perm, const uint8_t* flag_back,
+                     unsigned long long* newcount, hipStream_t s) {
+  if (!a.nparents) return;
+  hipLaunchKernelGGL(k_mark_gen, dim3((unsigned)((a.nparents + 255) / 256)), dim3(256), 0, s, a.nparents, a.pbase,
+                     a.par_off, a.par_n, a.cand_ob, a.cand_slot, a.cand_val, perm, flag_back, a.table, a.mask, a.floor,
+                     moved, a.cand_win, a.par_win, newcount, a.st);
 }
 int host_fp_owner(unsigned long long fp, int W) { return fp_owner(fp, W); }
 
@@ -666,7 +716,7 @@ struct Launch {
     const Model& M = *a.model;
     ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T));
     hipLaunchKernelGGL((k_expand<SPEC, N, FPW>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
-                       a.floor, a.sharded, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
+                       a.floor, a.sharded, a.shard_self, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);
   }
   template <int SPEC, int N>

@@ -16,10 +16,14 @@
 // order; they are written to their global positions (next level's block-
 // cyclic layout) by an all-to-all of state rows.
 //
-// Per round: expand (fp + key per candidate, no insert) -> bucket by owner ->
-// all-to-all (fp, key) 16 B -> owner inserts, then marks -> reverse all-to-all
-// of 1-byte win flags -> per-parent winner ranks, scan -> materialize into a
-// staging array -> all-to-all of rows + trace records to their owners.
+// Per round: expand (fp + key per candidate; the candidates whose fp this
+// shard owns are inserted right there, as the single-GPU search does) ->
+// bucket the others by owner -> all-to-all (fp, key) 16 B -> owners insert,
+// then mark -> reverse all-to-all of 1-byte win flags -> per-parent winner
+// ranks (local-owner outcomes read from the shard's own table), scan ->
+// materialize (straight into the next frontier when every winner stays with
+// its generator, else into staging) -> all-to-all of rows + trace records.
+// At W = 1 that is the single-GPU search plus the protocol's host round trips.
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -157,6 +161,7 @@ struct Shard {
   int id = 0;
   ShardBufs* B = nullptr;
   unsigned long long slots = 0, entries = 0;  // fingerprint set of this owner: slots, entries
+  unsigned long long expand_slots = 0;        // its size when this round's k_expand inserted
   uint32_t *cur = nullptr, *nxt = nullptr;
   unsigned long long fcap = 0;       // states per frontier buffer
   unsigned long long ncur = 0;       // local states of the current level
@@ -318,39 +323,63 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   };
   bool stop = false;
   unsigned gmax_msgs = 0;  // largest |DOMAIN messages| materialized on any shard
+  double rate = 4.0;       // new states per parent of the previous level (pre-sizes the tables per round)
+  unsigned long long lbase = 0, floor = 0;
+  // the round's arguments for shard s's c-th local block of parents
+  auto round_args = [&](LevelArgs& a, Shard& s, unsigned long long c) {
+    memset(&a, 0, sizeof a);
+    a.model = &M;
+    a.frontier = s.cur + c * CH * WD;
+    a.nparents = s.n;
+    a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
+    a.level = depth + 1;
+    a.floor = floor;
+    a.sharded = W;
+    a.shard_self = s.id;
+    a.table = s.B->table.as<unsigned long long>();
+    a.mask = s.slots - 1;
+    a.cand_slot = s.B->cfp.as<unsigned long long>();
+    a.cand_val = s.B->cval.as<unsigned long long>();
+    a.cand_ob = s.B->cob.as<uint32_t>();
+    a.cand_win = s.B->cwin.as<uint16_t>();
+    a.par_off = s.B->poff.as<uint32_t>();
+    a.par_n = s.B->pn.as<uint32_t>();
+    a.par_win = s.B->pwin.as<uint32_t>();
+    a.par_pos = s.B->ppos.as<uint32_t>();
+    a.counters = s.B->counters.as<unsigned long long>();
+    a.cand_cap = cand_cap;
+    a.st = s.B->stbuf.as<DevStatus>();
+  };
   while (status == 0 && P > 0 && !stop) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     const unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     const unsigned long long rounds = (P + W * CH - 1) / (W * CH);
-    const unsigned long long lbase = level_base[depth];
+    lbase = level_base[depth];
     unsigned long long GW = 0, gen_lvl = 0;
     if (lbase + P + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
     for (Shard& s : sh) s.next_fill = 0;
-    const unsigned long long floor = (lbase + 1) << VAL_FLOOR_SHIFT;  // entries below: earlier levels
-    for (unsigned long long c = 0; c < rounds && !stop; c++) {
-      // ---- expand: fp + key per candidate
+    floor = (lbase + 1) << VAL_FLOOR_SHIFT;  // entries below: earlier levels
+    for (unsigned long long c = 0; c < rounds && !stop;) {
+      // ---- room in each owner's table for the local inserts of k_expand (at
+      //      the highest rate of new states per parent seen; a full table is
+      //      grown and the round redone below)
+      {
+        const unsigned long long done = std::min(P, c * W * CH);
+        const double r = std::max(rate, done ? (double)GW / (double)done : 0.0);
+        for (Shard& s : sh) {
+          s.n = s.ncur > c * CH ? std::min(CH, s.ncur - c * CH) : 0;
+          if (!opt->grow_on_overflow) table_grow(s, s.entries + (unsigned long long)((double)s.n * r * 1.25) + 1024, stream);
+        }
+      }
+      // ---- expand: fp + key per candidate; the fps this shard owns are inserted here
       for (int si = 0; si < NL; si++) {
         Shard& s = sh[si];
-        s.n = s.ncur > c * CH ? std::min(CH, s.ncur - c * CH) : 0;
         HIPCHK(hipMemsetAsync(s.B->counters.p, 0, 64, stream));
         if (s.n) {
           LevelArgs a;
-          memset(&a, 0, sizeof a);
-          a.model = &M;
-          a.frontier = s.cur + c * CH * WD;
-          a.nparents = s.n;
-          a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
-          a.level = level;
-          a.sharded = 1;
-          a.cand_slot = s.B->cfp.as<unsigned long long>();
-          a.cand_val = s.B->cval.as<unsigned long long>();
-          a.cand_ob = s.B->cob.as<uint32_t>();
-          a.par_off = s.B->poff.as<uint32_t>();
-          a.par_n = s.B->pn.as<uint32_t>();
-          a.counters = s.B->counters.as<unsigned long long>();
-          a.cand_cap = cand_cap;
-          a.st = s.B->stbuf.as<DevStatus>();
+          round_args(a, s, c);
+          s.expand_slots = s.slots;
           HIPCHK(hipEventRecord(te[si].a, stream));
           launch_expand(M.spec, M.N, a, stream);
           HIPCHK(hipGetLastError());
@@ -366,7 +395,21 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       for (int i = 0; i < NL; i++) rows[i] = {sh[i].ncand, sh[i].hst.cap_flags};
       comm.allgather(rows, all, 2);
       unsigned capf = 0;
-      for (int r = 0; r < W; r++) { gen_lvl += all[2 * r]; capf |= (unsigned)all[2 * r + 1]; }
+      for (int r = 0; r < W; r++) capf |= (unsigned)all[2 * r + 1];
+      if (capf == (1u << E_CAP_TABLE)) {
+        // a local insert found its owner's table full: grow the full tables and
+        // redo the round on every shard (inserts are idempotent; nothing else
+        // of the round has happened yet)
+        for (Shard& s : sh) {
+          if (s.hst.cap_flags) table_grow(s, s.slots, stream);  // doubles
+          s.hst.cap_flags = 0;
+          HIPCHK(hipMemcpyAsync((char*)s.B->stbuf.p + offsetof(DevStatus, cap_flags), &s.hst.cap_flags, 4,
+                                hipMemcpyHostToDevice, stream));
+        }
+        HIPCHK(hipStreamSynchronize(stream));
+        continue;
+      }
+      for (int r = 0; r < W; r++) gen_lvl += all[2 * r];
       if (capf) {
         int e = 0;
         while (!((capf >> e) & 1)) e++;
@@ -378,103 +421,112 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         message = "capacity overflow (sharded search, code " + std::to_string(e) + ")";
         break;
       }
-      // ---- bucket by owner (per-block histograms, owner-major scan), exchange counts
-      std::vector<std::vector<unsigned int>> cnts(NL, std::vector<unsigned int>(W + 1));
-      for (int i = 0; i < NL; i++) {
-        Shard& s = sh[i];
-        const unsigned long long nb = bucket_blocks(s.ncand), nbw = nb * (unsigned long long)W;
-        s.B->bcnt.ensure((nbw + 1) * 4);
-        s.B->boff.ensure((nbw + 1) * 4);
-        size_t tb = scan_temp_bytes(nbw + 1);
-        s.B->btmp.ensure(tb ? tb : 16);
-        unsigned int* bc = s.B->bcnt.as<unsigned int>();
-        HIPCHK(hipMemsetAsync(bc + nbw, 0, 4, stream));
-        launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, bc, stream);
-        HIPCHK(hipGetLastError());
-        launch_scan(s.B->btmp.p, s.B->btmp.bytes, bc, s.B->boff.as<unsigned int>(), nbw + 1, stream);
-        HIPCHK(hipGetLastError());
-        // owner segment starts (boff[o*nb]) and the total (boff[nbw])
-        HIPCHK(hipMemcpy2DAsync(cnts[i].data(), 4, s.B->boff.as<unsigned int>(), nb * 4, 4, W, hipMemcpyDeviceToHost,
-                                stream));
-        HIPCHK(hipMemcpyAsync(&cnts[i][W], s.B->boff.as<unsigned int>() + nbw, 4, hipMemcpyDeviceToHost, stream));
-      }
-      HIPCHK(hipStreamSynchronize(stream));
-      for (int i = 0; i < NL; i++) {
-        rows[i].assign(W, 0);
-        for (int d = 0; d < W; d++) rows[i][d] = cnts[i][d + 1] - cnts[i][d];
-      }
-      comm.allgather(rows, all, W);  // all[src*W + dst] = records src sends to dst
-      for (int i = 0; i < NL; i++) {
-        Shard& s = sh[i];
-        s.seg_off.assign(W + 1, 0);
-        for (int d = 0; d < W; d++) s.seg_off[d + 1] = s.seg_off[d] + all[(size_t)s.id * W + d];
-        s.rseg_off.assign(W + 1, 0);
-        for (int q = 0; q < W; q++) s.rseg_off[q + 1] = s.rseg_off[q] + all[(size_t)q * W + s.id];
-        s.nrecv = s.rseg_off[W];
-        s.B->send.ensure(std::max<size_t>(16, s.seg_off[W] * 16));
-        s.B->sflag.ensure(std::max<size_t>(1, s.seg_off[W]));
-        s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
-        s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
-        s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
-        launch_bucket(s.B->cfp.as<unsigned long long>(), s.B->cval.as<unsigned long long>(), s.B->cob.as<uint32_t>(),
-                      s.ncand, W, s.B->boff.as<unsigned int>(), s.B->send.as<unsigned long long>(),
-                      s.B->perm.as<uint32_t>(), stream);
-        HIPCHK(hipGetLastError());
-      }
-      // ---- (fp, key) records to their owners
-      {
-        std::vector<Xfer> x;
-        for (int q = 0; q < W; q++)
-          for (int d = 0; d < W; d++) {
-            size_t cntqd = all[(size_t)q * W + d];
-            if (!cntqd) continue;
-            Xfer t{q, d, nullptr, nullptr, cntqd * 16};
-            for (Shard& s : sh) {
-              if (s.id == q) t.sbuf = s.B->send.as<unsigned long long>() + 2 * s.seg_off[d];
-              if (s.id == d) t.rbuf = s.B->recv.as<unsigned long long>() + 2 * s.rseg_off[q];
+      if (W > 1) {
+        // ---- remote-owner candidates: bucket by owner (per-block histograms,
+        //      owner-major scan), exchange counts
+        std::vector<std::vector<unsigned int>> cnts(NL, std::vector<unsigned int>(W + 1));
+        for (int i = 0; i < NL; i++) {
+          Shard& s = sh[i];
+          const unsigned long long nb = bucket_blocks(s.ncand), nbw = nb * (unsigned long long)W;
+          s.B->bcnt.ensure((nbw + 1) * 4);
+          s.B->boff.ensure((nbw + 1) * 4);
+          size_t tb = scan_temp_bytes(nbw + 1);
+          s.B->btmp.ensure(tb ? tb : 16);
+          unsigned int* bc = s.B->bcnt.as<unsigned int>();
+          HIPCHK(hipMemsetAsync(bc + nbw, 0, 4, stream));
+          launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, bc, stream);
+          HIPCHK(hipGetLastError());
+          launch_scan(s.B->btmp.p, s.B->btmp.bytes, bc, s.B->boff.as<unsigned int>(), nbw + 1, stream);
+          HIPCHK(hipGetLastError());
+          // owner segment starts (boff[o*nb]) and the total (boff[nbw])
+          HIPCHK(hipMemcpy2DAsync(cnts[i].data(), 4, s.B->boff.as<unsigned int>(), nb * 4, 4, W, hipMemcpyDeviceToHost,
+                                  stream));
+          HIPCHK(hipMemcpyAsync(&cnts[i][W], s.B->boff.as<unsigned int>() + nbw, 4, hipMemcpyDeviceToHost, stream));
+        }
+        HIPCHK(hipStreamSynchronize(stream));
+        for (int i = 0; i < NL; i++) {
+          rows[i].assign(W, 0);
+          for (int d = 0; d < W; d++) rows[i][d] = cnts[i][d + 1] - cnts[i][d];
+        }
+        comm.allgather(rows, all, W);  // all[src*W + dst] = records src sends to dst
+        for (int i = 0; i < NL; i++) {
+          Shard& s = sh[i];
+          s.seg_off.assign(W + 1, 0);
+          for (int d = 0; d < W; d++) s.seg_off[d + 1] = s.seg_off[d] + all[(size_t)s.id * W + d];
+          s.rseg_off.assign(W + 1, 0);
+          for (int q = 0; q < W; q++) s.rseg_off[q + 1] = s.rseg_off[q] + all[(size_t)q * W + s.id];
+          s.nrecv = s.rseg_off[W];
+          s.B->send.ensure(std::max<size_t>(16, s.seg_off[W] * 16));
+          s.B->sflag.ensure(std::max<size_t>(1, s.seg_off[W]));
+          s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
+          s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
+          s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
+          launch_bucket(s.B->cfp.as<unsigned long long>(), s.B->cval.as<unsigned long long>(), s.B->cob.as<uint32_t>(),
+                        s.ncand, W, s.B->boff.as<unsigned int>(), s.B->send.as<unsigned long long>(),
+                        s.B->perm.as<uint32_t>(), stream);
+          HIPCHK(hipGetLastError());
+        }
+        // ---- (fp, key) records to their owners
+        {
+          std::vector<Xfer> x;
+          for (int q = 0; q < W; q++)
+            for (int d = 0; d < W; d++) {
+              size_t cntqd = all[(size_t)q * W + d];
+              if (!cntqd) continue;
+              Xfer t{q, d, nullptr, nullptr, cntqd * 16};
+              for (Shard& s : sh) {
+                if (s.id == q) t.sbuf = s.B->send.as<unsigned long long>() + 2 * s.seg_off[d];
+                if (s.id == d) t.rbuf = s.B->recv.as<unsigned long long>() + 2 * s.rseg_off[q];
+              }
+              x.push_back(t);
             }
-            x.push_back(t);
-          }
-        comm.alltoallv(x);
-      }
-      // ---- owners insert, then mark
-      for (Shard& s : sh) {
-        table_grow(s, s.entries + s.nrecv, stream);  // exact bound: every received record new
-        launch_insert_recv(s.B->recv.as<unsigned long long>(), s.nrecv, s.B->table.as<unsigned long long>(),
-                           s.slots - 1, floor, s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
-        HIPCHK(hipGetLastError());
-      }
-      for (Shard& s : sh) {
-        unsigned long long* nc = s.B->counters.as<unsigned long long>() + 1;
-        launch_mark_recv(s.B->recv.as<unsigned long long>(), s.B->rslot.as<unsigned long long>(), s.nrecv,
-                         s.B->table.as<unsigned long long>(), floor, s.B->rflag.as<uint8_t>(), nc,
-                         s.B->stbuf.as<DevStatus>(), stream);
-        HIPCHK(hipGetLastError());
-      }
-      // ---- win flags back to the generators (reverse of the record exchange)
-      {
-        std::vector<Xfer> x;
-        for (int q = 0; q < W; q++)
-          for (int d = 0; d < W; d++) {
-            size_t cntqd = all[(size_t)q * W + d];
-            if (!cntqd) continue;
-            Xfer t{d, q, nullptr, nullptr, cntqd};
-            for (Shard& s : sh) {
-              if (s.id == d) t.sbuf = s.B->rflag.as<uint8_t>() + s.rseg_off[q];
-              if (s.id == q) t.rbuf = s.B->sflag.as<uint8_t>() + s.seg_off[d];
+          comm.alltoallv(x);
+        }
+        // ---- owners insert, then mark
+        for (Shard& s : sh) {
+          // exact bound: the local candidates (inserted) and every received record new
+          table_grow(s, s.entries + s.ncand + s.nrecv, stream);
+          launch_insert_recv(s.B->recv.as<unsigned long long>(), s.nrecv, s.B->table.as<unsigned long long>(),
+                             s.slots - 1, floor, s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
+          HIPCHK(hipGetLastError());
+        }
+        for (Shard& s : sh) {
+          unsigned long long* nc = s.B->counters.as<unsigned long long>() + 1;
+          launch_mark_recv(s.B->recv.as<unsigned long long>(), s.B->rslot.as<unsigned long long>(), s.nrecv,
+                           s.B->table.as<unsigned long long>(), floor, s.B->rflag.as<uint8_t>(), nc,
+                           s.B->stbuf.as<DevStatus>(), stream);
+          HIPCHK(hipGetLastError());
+        }
+        // ---- win flags back to the generators (reverse of the record exchange)
+        {
+          std::vector<Xfer> x;
+          for (int q = 0; q < W; q++)
+            for (int d = 0; d < W; d++) {
+              size_t cntqd = all[(size_t)q * W + d];
+              if (!cntqd) continue;
+              Xfer t{d, q, nullptr, nullptr, cntqd};
+              for (Shard& s : sh) {
+                if (s.id == d) t.sbuf = s.B->rflag.as<uint8_t>() + s.rseg_off[q];
+                if (s.id == q) t.rbuf = s.B->sflag.as<uint8_t>() + s.seg_off[d];
+              }
+              x.push_back(t);
             }
-            x.push_back(t);
-          }
-        comm.alltoallv(x);
+          comm.alltoallv(x);
+        }
       }
-      // ---- generators: winner ranks per parent, positions
+      // ---- generators: winner ranks per parent (local-owner outcomes from
+      //      their own table, remote ones from the flags), positions
       std::vector<unsigned long long> newc(NL, 0);
       for (int i = 0; i < NL; i++) {
         Shard& s = sh[i];
         s.nwin = 0;
         if (s.n) {
-          launch_mark_gen(s.n, s.B->poff.as<uint32_t>(), s.B->pn.as<uint32_t>(), s.B->perm.as<uint32_t>(),
-                          s.B->sflag.as<uint8_t>(), s.B->cwin.as<uint16_t>(), s.B->pwin.as<uint32_t>(), stream);
+          LevelArgs a;
+          round_args(a, s, c);
+          s.B->sflag.ensure(1);
+          s.B->perm.ensure(4);
+          launch_mark_gen(a, s.slots != s.expand_slots, s.B->perm.as<uint32_t>(), s.B->sflag.as<uint8_t>(),
+                          s.B->counters.as<unsigned long long>() + 1, stream);
           HIPCHK(hipGetLastError());
           launch_scan(s.B->scantmp.p, s.B->scantmp.bytes, s.B->pwin.as<uint32_t>(), s.B->ppos.as<uint32_t>(), s.n,
                       stream);
@@ -492,77 +544,93 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       for (int i = 0; i < NL; i++) {
         sh[i].nwin = (unsigned long long)lastpos[i] + lastwin[i];
         sh[i].entries += newc[i];
-        HIPCHK(hipMemsetAsync(sh[i].B->counters.as<unsigned long long>() + 1, 0, 8, stream));
         rows[i] = {sh[i].nwin};
       }
       comm.allgather(rows, all, 1);  // all[r] = winners generated by shard r this round
       std::vector<unsigned long long> go(W + 1, 0);
       for (int r = 0; r < W; r++) go[r + 1] = go[r] + all[r];
-      // ---- materialize winners into staging (TLC order within the generator)
+      // ---- where the winners go: generator q's winners take the global
+      //      positions [GW + go[q], GW + go[q+1]), cut into pieces by
+      //      next-level owner (block-cyclic)
+      struct Piece { int q, d; unsigned long long a, b, dl; };
+      std::vector<Piece> pcs;
+      for (int q = 0; q < W; q++) {
+        unsigned long long a = GW + go[q], end = GW + go[q + 1];
+        while (a < end) {
+          unsigned long long blk = a / CH, b = std::min(end, (blk + 1) * CH);
+          pcs.push_back({q, (int)(blk % W), a, b, (blk / W) * CH + a % CH});
+          a = b;
+        }
+      }
+      for (Shard& s : sh) {  // capacity of the receiving side
+        unsigned long long need = s.next_fill;
+        for (auto& pc : pcs)
+          if (pc.d == s.id) need = std::max(need, pc.dl + (pc.b - pc.a));
+        {  // the next-level buffer grows in place to exactly what it receives
+          bool cur_is_a = s.cur == s.B->fa.as<uint32_t>();
+          GrowBuf& nb = cur_is_a ? s.B->fb : s.B->fa;
+          grow_keep(nb, need * WD * 4, s.next_fill * WD * 4, stream);
+          s.cur = (cur_is_a ? s.B->fa : s.B->fb).as<uint32_t>();
+          s.nxt = nb.as<uint32_t>();
+          s.fcap = std::max(s.fcap, need);
+        }
+        unsigned long long trneed = s.tr_base[depth + 1] + need;
+        if (trneed > s.trcap) {
+          unsigned long long nt = trneed + trneed / 4;
+          grow_keep(s.B->trp, nt * 8, s.tr_base[depth + 1] * 8 + s.next_fill * 8, stream);
+          grow_keep(s.B->trb, nt * 2, s.tr_base[depth + 1] * 2 + s.next_fill * 2, stream);
+          s.trcap = nt;
+        }
+        s.next_fill = need;
+      }
+      // A generator whose winners all stay with it, in one local run (always
+      // at W = 1), writes them straight into its next frontier; the others
+      // materialize into staging and send.
+      std::vector<char> direct(W, 0);
+      std::vector<unsigned long long> direct_dl(W, 0);
+      for (int q = 0; q < W; q++) {
+        bool ok = true, first = true;
+        unsigned long long expect = 0;
+        for (auto& pc : pcs) {
+          if (pc.q != q) continue;
+          if (pc.d != q || (!first && pc.dl != expect)) ok = false;
+          if (first) direct_dl[q] = pc.dl;
+          first = false;
+          expect = pc.dl + (pc.b - pc.a);
+        }
+        direct[q] = ok && !first;
+      }
+      // ---- materialize winners (TLC order within the generator)
       for (int si = 0; si < NL; si++) {
         Shard& s = sh[si];
         if (!s.n || !s.nwin) continue;
-        s.B->stage.ensure(s.nwin * WD * 4);
-        s.B->stp.ensure(s.nwin * 8);
-        s.B->stb.ensure(s.nwin * 2);
         LevelArgs a;
-        memset(&a, 0, sizeof a);
-        a.model = &M;
-        a.frontier = s.cur + c * CH * WD;
-        a.nparents = s.n;
-        a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
-        a.level = level;
-        a.cand_ob = s.B->cob.as<uint32_t>();
-        a.cand_win = s.B->cwin.as<uint16_t>();
-        a.par_off = s.B->poff.as<uint32_t>();
-        a.par_n = s.B->pn.as<uint32_t>();
-        a.par_pos = s.B->ppos.as<uint32_t>();
-        a.out = s.B->stage.as<uint32_t>();
-        a.out_base_global = 0;
-        a.tr_parent = s.B->stp.as<unsigned long long>();
-        a.tr_bind = s.B->stb.as<uint16_t>();
-        a.st = s.B->stbuf.as<DevStatus>();
+        round_args(a, s, c);
+        if (direct[s.id]) {
+          a.out = s.nxt + direct_dl[s.id] * WD;
+          a.out_base_global = s.tr_base[depth + 1] + direct_dl[s.id];
+          a.tr_parent = s.B->trp.as<unsigned long long>();
+          a.tr_bind = s.B->trb.as<uint16_t>();
+        } else {
+          s.B->stage.ensure(s.nwin * WD * 4);
+          s.B->stp.ensure(s.nwin * 8);
+          s.B->stb.ensure(s.nwin * 2);
+          a.out = s.B->stage.as<uint32_t>();
+          a.out_base_global = 0;
+          a.tr_parent = s.B->stp.as<unsigned long long>();
+          a.tr_bind = s.B->stb.as<uint16_t>();
+        }
         HIPCHK(hipEventRecord(tz[si].a, stream));
         launch_materialize(M.spec, M.N, a, stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(tz[si].b, stream));
         tz_on[si] = 1;
       }
-      // ---- rows + trace records to their next-level owners (block-cyclic by global position)
+      // ---- rows + trace records of the staged generators to their next-level owners
       {
-        struct Piece { int q, d; unsigned long long a, b, dl; };
-        std::vector<Piece> pcs;
-        for (int q = 0; q < W; q++) {
-          unsigned long long a = GW + go[q], end = GW + go[q + 1];
-          while (a < end) {
-            unsigned long long blk = a / CH, b = std::min(end, (blk + 1) * CH);
-            pcs.push_back({q, (int)(blk % W), a, b, (blk / W) * CH + a % CH});
-            a = b;
-          }
-        }
-        for (Shard& s : sh) {  // capacity of the receiving side
-          unsigned long long need = s.next_fill;
-          for (auto& pc : pcs)
-            if (pc.d == s.id) need = std::max(need, pc.dl + (pc.b - pc.a));
-          {  // the next-level buffer grows in place to exactly what it receives
-            bool cur_is_a = s.cur == s.B->fa.as<uint32_t>();
-            GrowBuf& nb = cur_is_a ? s.B->fb : s.B->fa;
-            grow_keep(nb, need * WD * 4, s.next_fill * WD * 4, stream);
-            s.cur = (cur_is_a ? s.B->fa : s.B->fb).as<uint32_t>();
-            s.nxt = nb.as<uint32_t>();
-            s.fcap = std::max(s.fcap, need);
-          }
-          unsigned long long trneed = s.tr_base[depth + 1] + need;
-          if (trneed > s.trcap) {
-            unsigned long long nt = trneed + trneed / 4;
-            grow_keep(s.B->trp, nt * 8, s.tr_base[depth + 1] * 8 + s.next_fill * 8, stream);
-            grow_keep(s.B->trb, nt * 2, s.tr_base[depth + 1] * 2 + s.next_fill * 2, stream);
-            s.trcap = nt;
-          }
-          s.next_fill = need;
-        }
         std::vector<Xfer> x;
         for (auto& pc : pcs) {
+          if (direct[pc.q]) continue;
           unsigned long long cnt = pc.b - pc.a, so = pc.a - (GW + go[pc.q]);
           Xfer rowsx{pc.q, pc.d, nullptr, nullptr, cnt * WD * 4};
           Xfer parx{pc.q, pc.d, nullptr, nullptr, cnt * 8};
@@ -621,6 +689,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         }
         stop = true;
       }
+      c++;
     }
     generated += gen_lvl;
     distinct += GW;
@@ -634,6 +703,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       s.ncur = local_count(GW, W, CH, s.id);
       std::swap(s.cur, s.nxt);
     }
+    if (P) rate = (double)GW / (double)P;
     P = GW;
     if (opt->verbose && comm.local[0] == 0)
       fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated (%d shards)\n", depth,

@@ -74,6 +74,21 @@ def test_logical_growth_paths():
     same(m.check_logical(3, chunk_parents=33, frontier_cap=16), g)
 
 
+@pytest.mark.parametrize("name", ["pull_n3v1e2r1", "raft_n4v1e1"])
+@pytest.mark.parametrize("shards,chunk", [(1, 0), (3, 333)])
+def test_logical_table_overflow_redo(name, shards, chunk):
+    """64-slot tables and no growth ahead of rounds: k_expand's local-owner
+    inserts overflow a shard's table, every shard redoes the round after it
+    grows; the owners' remote inserts grow the table mid-round (local-owner
+    outcomes are then found by fingerprint).  Counts unchanged."""
+    g = MEDIUM[name]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    r = m.check_logical(shards, chunk_parents=chunk, hash_slots=64, grow_on_overflow=True)
+    assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
+        (g["generated"], g["distinct"], g["depth"], g["levels"])
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
 UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
 
 
