@@ -166,7 +166,7 @@ def main():
     G, D, S = res["generated"] - 1, res["distinct"], res["state_bytes"]
     pmc, pmc_src = pmc_summary(args.workload)
     kpmc = {}
-    if pmc:
+    if pmc and world == 1 and not args.logical_shards:  # the summary profiles the single-shard kernels
         for k, v in pmc.get("kernels", {}).items():
             for short in ("k_expand", "k_mark", "k_materialize"):
                 if k.startswith("rmc::" + short) and "traffic_bytes_per_dispatch" in v:
@@ -212,7 +212,7 @@ def main():
                          "frac": B / per_step / HBM_PEAK,
                          "traffic": sum(kpmc.values()) * launches if len(kpmc) == 3 else None,
                          "traffic_unit": "HBM bytes per check (PMC: k_expand + k_mark + k_materialize)",
-                         "traffic_source": pmc_src,
+                         "traffic_source": pmc_src if kpmc else None,
                          "formula": "B = 2*D*S + 8*G + 20*D per check (SURVEY.md 8d) over the check's wall time",
                          "bytes_per_check": B, "kernel": "k_expand", "launches": launches, "kernels": kern,
                          "candidate_bytes_per_check": G * (8 + 4 + 2)},

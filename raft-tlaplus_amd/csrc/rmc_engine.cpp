@@ -1176,7 +1176,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   }
   res->hidden_var_collisions = fin.hidden_coll;
   if (opt->verbose) {
-    unsigned long long stp[8];
+    unsigned long long stp[16];
     read_stamps(stp);
     double tot = (double)(stp[0] + stp[2] + stp[3]);
     if (tot > 0)
@@ -1184,6 +1184,10 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
               "(the same without inserts: %.1f%%); "
               "fingerprints %llu, with signature ties %llu, permutations hashed under ties %llu\n",
               100 * stp[0] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot, 100 * stp[7] / tot, stp[4], stp[5], stp[6]);
+    if (stp[8])
+      fprintf(stderr, "[rmc] phase B: %llu parents, %.2f message bindings and %.2f live ones per parent (%d fixed); "
+              "wave steps %llu, with live messages only %llu\n", stp[8], (double)stp[9] / stp[8],
+              (double)stp[10] / stp[8], M.nfixed, stp[11], stp[12]);
     fprintf(stderr, "[rmc] fingerprint set: 2^%d slots, load %.3f, %llu growths, %llu chunk redos\n",
             __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);
   }

@@ -83,7 +83,9 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
       if (e[q].x == fp || e[q].x == EMPTY) { k = q; kv = e[q].y; found = e[q].x == fp; }
     slot = (slot + (unsigned long long)k) & mask;  // k == RMC_FP_FAST may step past the last slot: wrap
     if (found) {
-      if (kv >= floor) atomicMin(T + 2 * slot + 1, val);  // same level (or its claimer's min in flight)
+      // same level (or its claimer's min in flight): values only decrease, so
+      // a snapshot already below val means this successor lost -- no atomic
+      if (kv >= floor && val < kv) atomicMin(T + 2 * slot + 1, val);
       return slot;
     }
   }
@@ -100,7 +102,7 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
       // ~0 is an entry being claimed this level, whose claimer's atomicMin is
       // still in flight: >= floor, so this one takes part.)
       const unsigned long long cur = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur >= floor) atomicMin(e + 1, val);
+      if (cur >= floor && val < cur) atomicMin(e + 1, val);
       return slot;
     }
     slot = (slot + 1) & mask;
@@ -142,7 +144,7 @@ __device__ __forceinline__ unsigned long long fpset_insert128(unsigned long long
     if (k0.x == fp.a || k0.x == EMPTY) { k = 0; kv = v0.x; found = k0.x == fp.a && k0.y == fp.b; }
     slot = (slot + (unsigned long long)k) & mask;
     if (found) {
-      if (kv >= floor) atomicMin(T + 4 * slot + 2, val);
+      if (kv >= floor && val < kv) atomicMin(T + 4 * slot + 2, val);
       return slot;
     }
   }
@@ -174,7 +176,7 @@ __device__ __forceinline__ unsigned long long fpset_insert128(unsigned long long
       }
       if (lo == fp.b) {
         const unsigned long long cur = __hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur >= floor) atomicMin(e + 2, val);
+        if (cur >= floor && val < cur) atomicMin(e + 2, val);
         return slot;
       }
     }

@@ -49,7 +49,7 @@ __device__ __forceinline__ unsigned long long order_key(unsigned long long pg, i
 // summed over blocks (thread 0's shader-clock deltas, with an extra barrier
 // between phases A and B).  Read the shares, not the absolute time.
 #ifdef RMC_STAMPS
-__device__ unsigned long long g_stamps[8];
+__device__ unsigned long long g_stamps[16];
 #define STAMP(i)                                                   \
   do {                                                             \
     __syncthreads();                                               \
@@ -66,9 +66,9 @@ __device__ unsigned long long g_stamps[8];
 #endif
 void read_stamps(unsigned long long* out) {
 #ifdef RMC_STAMPS
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 8 * sizeof(unsigned long long));
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 16 * sizeof(unsigned long long));
 #else
-  for (int i = 0; i < 8; i++) out[i] = 0;
+  for (int i = 0; i < 16; i++) out[i] = 0;
 #endif
 }
 
@@ -79,8 +79,9 @@ struct Tile {
 };
 
 // Dynamic LDS layout of k_expand (bytes; the launch computes the same).
+constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
 struct ExpandLds {
-  int Wp, off_Ms, off_Ord, off_Base, bytes;
+  int Wp, off_Ms, off_Ord, off_Base, off_Live, bytes;
 };
 __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes) {
   ExpandLds L;
@@ -92,6 +93,8 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
   o += PB * ordw * 4;
   L.off_Base = o;  // exclusive prefix over the tile's parents of their successor counts
   o += (PB + 1) * 4;
+  L.off_Live = o;  // per parent: bitmask over DOMAIN messages that can enable an action (msg_live)
+  o += PB * LIVE_WORDS * 4;
   L.bytes = o;
   return L;
 }
@@ -145,7 +148,9 @@ __device__ __forceinline__ MsgSums<N>& sums1(MsgSums<N>& m) { return m; }
 template <int N>
 __device__ __forceinline__ MsgSums<N>& sums1(MsgSums2<N>& m) { return m.m; }
 template <int SPEC, int N, int FPW>
-__global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+// waves per SIMD: as many as fit without scratch spills (N >= 4 and 128-bit
+// fingerprints need more registers; a spill costs a scratch store per binding)
+__global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW == 2 ? 3 : 4) : FPW == 2 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                 unsigned long long pbase, unsigned long long floor, int sharded,
                                                 int shard_self,
                                                 unsigned long long* __restrict__ table, unsigned long long mask,
@@ -165,6 +170,7 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
   MS* sMS = (MS*)(lds + L.off_Ms);
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
   uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
+  uint32_t* sLive = (uint32_t*)(lds + L.off_Live);
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
 #ifdef RMC_STAMPS
@@ -177,6 +183,7 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
     sS[p * L.Wp + (q - p * words)] = src[q];
   }
   for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
+  for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
   for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
   __syncthreads();
   STAMP(0);
@@ -186,13 +193,15 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
     if (p < np) {
       PState<SPEC, N> s{sS + p * L.Wp};
       const int nm = s.nmsg();
-      const int B = cM.nfixed + nm;
-      const unsigned long long pg = pbase + p0 + p;
       // the parent's message sums (MsgSums): each of its messages hashed once
-      // here instead of once per successor in phase C
+      // here instead of once per successor in phase C; and which messages can
+      // enable an action at all (84% of DOMAIN messages cannot on the bench
+      // workload: delivered, and not newer than their receiver)
       for (int k = tid / PB; k < nm; k += bstride) {
         int src, dst;
-        const uint64_t u = msg_u<SPEC>(s.msg(k), src, dst);
+        const uint32_t w = s.msg(k);
+        if (msg_live<SPEC, N>(s, w)) atomicOr(&sLive[p * LIVE_WORDS + (k >> 5)], 1u << (k & 31));
+        const uint64_t u = msg_u<SPEC>(w, src, dst);
         MsgSums<N>& m1 = sums1<N>(sMS[p]);
         atomicAdd(&m1.sig[src], (uint32_t)u);
         atomicAdd(&m1.sig[dst], (uint32_t)(u >> 32));
@@ -200,12 +209,45 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
         if constexpr (FPW == 2) {
           if (src != dst)
             atomicAdd((unsigned long long*)&sMS[p].S2[MsgSums<N>::pair(src, dst)],
-                      (unsigned long long)msg_u2<SPEC>(s.msg(k)));
+                      (unsigned long long)msg_u2<SPEC>(w));
         }
       }
-      for (int b = tid / PB; b < B; b += bstride) {
+    }
+    __syncthreads();
+    if (p < np) {
+      PState<SPEC, N> s{sS + p * L.Wp};
+      const int nm = s.nmsg();
+      const int B = cM.nfixed + nm;
+      const unsigned long long pg = pbase + p0 + p;
+#ifdef RMC_STAMPS
+      {  // binding statistics: message bindings, live ones (act_message's fast reject passes), wave steps
+        int live = 0;
+        for (int k = 0; k < nm; k++) {
+          const uint32_t w = s.msg(k);
+          live += !(msg_count(w) == 0 && msg_term<SPEC>(w) <= a_term(s.A(msg_dst<SPEC>(w))));
+        }
+        const int w0 = tid / PB;
+        int steps = (B - w0 + bstride - 1) / bstride, lsteps = (cM.nfixed + live - w0 + bstride - 1) / bstride;
+        for (int o = 32; o > 0; o >>= 1) {
+          steps = max(steps, __shfl_xor(steps, o, WAVE));
+          lsteps = max(lsteps, __shfl_xor(lsteps, o, WAVE));
+        }
+        if (w0 == 0) {
+          atomicAdd(&g_stamps[8], 1ULL);
+          atomicAdd(&g_stamps[9], (unsigned long long)nm);
+          atomicAdd(&g_stamps[10], (unsigned long long)live);
+        }
+        if ((tid & (WAVE - 1)) == 0) {
+          atomicAdd(&g_stamps[11], (unsigned long long)steps);
+          atomicAdd(&g_stamps[12], (unsigned long long)lsteps);
+        }
+      }
+#endif
+      // fixed bindings (wave-uniform: every lane on the same binding), then
+      // the parent's live messages, every 4th one per wave
+      auto eval_one = [&](int b) {
         Delta d;
-        if (!eval_binding<SPEC, N>(s, cM, b, d)) continue;
+        if (!eval_binding<SPEC, N>(s, cM, b, d)) return;
         if (d.err) {
           if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pg, d.ordinal, b));
           else atomicOr(&st->cap_flags, 1u << d.err);
@@ -216,7 +258,19 @@ __global__ __launch_bounds__(256, (N >= 5 || FPW == 2 ? 4 : RMC_EXPAND_WAVES)) v
           if (nm + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
         }
         atomicOr(&sOrd[p * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
+      };
+      const int w0 = tid / PB;
+      for (int b = w0; b < cM.nfixed; b += bstride) eval_one(b);
+      int t = 0;
+      for (int q = 0; q < LIVE_WORDS; q++) {
+        uint32_t x = sLive[p * LIVE_WORDS + q];
+        while (x) {
+          const int k = 32 * q + __ffs(x) - 1;
+          x &= x - 1u;
+          if ((t++ & (bstride - 1)) == w0) eval_one(cM.nfixed + k);
+        }
       }
+      (void)B;
     }
   }
   __syncthreads();

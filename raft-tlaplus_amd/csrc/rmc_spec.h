@@ -617,13 +617,19 @@ RMC_HD bool act_sendpull(const PState<SPEC, N>& s, const Model& M, int i, int j,
   return op_send_once(s, d, msg_encode<SPEC>(m));
 }
 
+// Can DOMAIN element w enable any action?  A delivered message (count 0)
+// enables nothing unless its term is newer than its receiver's (UpdateTerm
+// ranges over all of DOMAIN messages, Raft.tla:349-350).
+template <int SPEC, int N>
+RMC_HD bool msg_live(const PState<SPEC, N>& s, uint32_t w) {
+  return !(msg_count(w) == 0 && msg_term<SPEC>(w) <= a_term(s.A(msg_dst<SPEC>(w))));
+}
+
 // ---- message-bound actions: exactly one can be enabled per DOMAIN element
 template <int SPEC, int N>
 RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
   uint32_t w = s.msg(k);
-  // Fast reject before the full decode: a delivered message (count 0) enables
-  // nothing unless its term is newer than its receiver's (UpdateTerm).
-  if (msg_count(w) == 0 && msg_term<SPEC>(w) <= a_term(s.A(msg_dst<SPEC>(w)))) return false;
+  if (!msg_live<SPEC, N>(s, w)) return false;  // fast reject before the full decode
   MsgF m = msg_decode<SPEC>(w);
   int i = m.dst, j = m.src;
   uint32_t a = s.A(i), b = s.B(i);
@@ -1177,7 +1183,7 @@ RMC_HD uint64_t canon_from_sums(const Model& M, const DeltaView<SPEC, N>& V, con
   uint64_t best = ~0ULL;
   const int np = ties ? M.nperm : 1;
 #if defined(RMC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-  extern __device__ unsigned long long g_stamps[8];
+  extern __device__ unsigned long long g_stamps[16];
   atomicAdd(&g_stamps[4], 1ULL);
   if (ties) atomicAdd(&g_stamps[5], 1ULL);
 #endif
