@@ -8,6 +8,7 @@
 //   flexible-raft/FlexibleRaft.tla (Next :488-500)
 //   raft-and-fsync/RaftFsync.tla  (Next :522-536)
 //   pull-raft/PullRaft.tla        (Next :542-558)
+//   pull-raft/PullRaftVariant2.tla (Next :560-576)
 // TLC semantics: actions split per constant binding
 // (first bound variable fastest), DOMAIN messages enumerated in TLC value
 // order, FIFO BFS, first successor per fingerprint wins, invariants checked on
@@ -36,7 +37,7 @@
 
 namespace {
 
-enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3 };
+enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3, PULL2 = 4 };
 enum MType : int8_t { RVREQ = 0, RVRESP, AEREQ, AERESP, LNREQ, PEREQ, PERESP };
 enum SState : int8_t { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 constexpr int NIL = -1;
@@ -57,6 +58,7 @@ struct Msg {
   int8_t commit;                     // mcommitIndex
   int8_t success, matchIndex;        // AppendEntriesResponse, PullEntriesResponse
   int8_t lciIndex, lciTerm;          // mlastCommonEntry
+  int8_t lceNil;                     // Variant2 LeaderNotifyRequest: mlastCommonEntry = Nil
   uint8_t count;
 };
 constexpr size_t REC_BYTES = offsetof(Msg, count);
@@ -68,7 +70,9 @@ struct State {
   int16_t nmsg;
   int8_t electionCtr, restartCtr;
   int8_t acked[MAXV];  // -1 Nil, 0 FALSE, 1 TRUE
-  int8_t term[MAXN], st[MAXN], voted[MAXN];  // voted = votedFor (Pull: leader)
+  int8_t term[MAXN], st[MAXN], voted[MAXN];  // voted = votedFor (Pull, Variant2: leader)
+  int8_t voted2[MAXN];                        // Variant2: votedFor
+  int8_t vleI[MAXN][MAXN], vleT[MAXN][MAXN];  // Variant2: votesLastEntry (index -1 = Nil)
   int8_t loglen[MAXN], commit[MAXN], fsync[MAXN];
   uint8_t votes[MAXN], pending[MAXN];  // bitsets over servers
   Entry log[MAXN][MAXL];
@@ -79,6 +83,7 @@ constexpr size_t FIXED_BYTES = offsetof(State, msgs);
 
 struct Config {
   SpecKind spec = RAFT;
+  bool pull() const { return spec == PULL || spec == PULL2; }
   int N = 3, V = 1, E = 2, R = 0;
   int EQ = 0, RQ = 0;                       // FlexibleRaft quorum sizes
   bool lfae = false, lfiq = true, ffbr = true;  // RaftFsync policy flags
@@ -104,7 +109,9 @@ struct Key {
   void str(const char* s) { while (*s) b[n++] = (uint8_t)*s++; b[n++] = 0; }
 };
 struct Field { const char* name; int kind; int v0, v1, v2; };
-// kinds: 0 int/bool/server, 1 type name, 2 mentries seq, 3 lastCommonEntry record
+// kinds: 0 int/bool/server, 1 type name, 2 mentries seq, 3 lastCommonEntry record,
+// 4 lastCommonEntry Nil-or-record (Variant2: the untyped model value Nil
+// compares below any record)
 void msg_key(const Msg& m, Key& k) {
   Field f[8];
   int nf = 0;
@@ -116,12 +123,17 @@ void msg_key(const Msg& m, Key& k) {
   switch (m.type) {
     case RVREQ: case PEREQ:
       add("mlastLogTerm", 0, m.lastLogTerm); add("mlastLogIndex", 0, m.lastLogIndex); break;
-    case RVRESP: add("mvoteGranted", 0, m.voteGranted); break;
+    case RVRESP:
+      add("mvoteGranted", 0, m.voteGranted);
+      if (C.spec == PULL2) { add("mlastLogIndex", 0, m.lastLogIndex); add("mlastLogTerm", 0, m.lastLogTerm); }
+      break;
     case AEREQ:
       add("mprevLogIndex", 0, m.prevLogIndex); add("mprevLogTerm", 0, m.prevLogTerm);
       add("mentries", 2, m.nent, m.eterm, m.evalue); add("mcommitIndex", 0, m.commit); break;
     case AERESP: add("msuccess", 0, m.success); add("mmatchIndex", 0, m.matchIndex); break;
-    case LNREQ: break;
+    case LNREQ:
+      if (C.spec == PULL2) add("mlastCommonEntry", 4, m.lceNil, m.lciIndex, m.lciTerm);
+      break;
     case PERESP:
       add("msuccess", 0, m.success);
       if (m.success) { add("mentries", 2, m.nent, m.eterm, m.evalue); add("mcommitIndex", 0, m.commit); }
@@ -141,6 +153,10 @@ void msg_key(const Msg& m, Key& k) {
         if (f[i].v0) { k.byte(2); k.str("term"); k.byte(f[i].v1); k.str("value"); k.byte(f[i].v2); }
         break;
       case 3: k.byte(2); k.str("index"); k.byte(f[i].v0); k.str("term"); k.byte(f[i].v1); break;
+      case 4:
+        if (f[i].v0) k.byte(0);
+        else { k.byte(1); k.byte(2); k.str("index"); k.byte(f[i].v1); k.str("term"); k.byte(f[i].v2); }
+        break;
     }
   }
 }
@@ -258,6 +274,10 @@ void Restart(const State& s, int i, Emitter& E) {
   t.pending[i] = 0;
   t.commit[i] = 0;
   t.restartCtr++;
+  if (C.spec == PULL2) {  // PullRaftVariant2.tla:251-260: leader and votesLastEntry reset too
+    t.voted[i] = NIL;
+    for (int j = 0; j < C.N; j++) { t.vleI[i][j] = -1; t.vleT[i][j] = 0; }
+  }
   if (C.spec == FSYNC) {
     int f = s.fsync[i], L = s.loglen[i];
     if (f == 0) t.loglen[i] = 0;
@@ -282,6 +302,10 @@ void RequestVote(const State& s, int i, Emitter& E) {
   t.st[i] = CANDIDATE;
   t.term[i] = (int8_t)(s.term[i] + 1);
   t.voted[i] = (int8_t)i;
+  if (C.spec == PULL2) {  // PullRaftVariant2.tla:284-286: votedFor = i, leader = Nil
+    t.voted2[i] = (int8_t)i;
+    t.voted[i] = NIL;
+  }
   t.votes[i] = (uint8_t)(1u << i);
   t.electionCtr++;
   E.emit(t, A_REQUESTVOTE);
@@ -339,6 +363,7 @@ void AppendEntries(const State& s, int i, int j, Emitter& E) {
   E.emit(t, A_APPENDENTRIES);
 }
 
+void LastCommonEntry(const State& s, int i, int lastIndex, int lastTerm, int& idx, int& term);
 void BecomeLeader(const State& s, int i, Emitter& E) {
   // Raft.tla:289-300; FlexibleRaft.tla:260-269; RaftFsync.tla:276-285; PullRaft.tla:354-366
   if (s.st[i] != CANDIDATE) return;
@@ -353,9 +378,25 @@ void BecomeLeader(const State& s, int i, Emitter& E) {
       insert_msg(t, m, 1);
     }
   }
+  if (C.spec == PULL2) {  // PullRaftVariant2.tla:361-379: every other server, with the last common entry
+    for (int j = 0; j < C.N; j++) {
+      if (j == i) continue;
+      Msg m = mk(LNREQ, s.term[i], i, j);
+      if (s.vleI[i][j] < 0) m.lceNil = 1;
+      else {
+        int a, b;
+        LastCommonEntry(s, i, s.vleI[i][j], s.vleT[i][j], a, b);
+        m.lciIndex = (int8_t)a;
+        m.lciTerm = (int8_t)b;
+      }
+      if (find_msg(s, m) >= 0) return;
+      insert_msg(t, m, 1);
+    }
+    t.voted[i] = (int8_t)i;  // leader' = i
+  }
   t.st[i] = LEADER;
   for (int j = 0; j < C.N; j++) {
-    if (C.spec != PULL) t.next[i][j] = (int8_t)(Len(s, i) + 1);
+    if (!C.pull()) t.next[i][j] = (int8_t)(Len(s, i) + 1);
     t.match[i][j] = 0;
   }
   if (C.spec == RAFT) t.pending[i] = 0;
@@ -423,6 +464,7 @@ void UpdateTerm(const State& s, Emitter& E) {  // Raft.tla:348-355; PullRaft.tla
     t.term[m.dst] = m.term;
     t.st[m.dst] = FOLLOWER;
     t.voted[m.dst] = NIL;
+    if (C.spec == PULL2) t.voted2[m.dst] = NIL;  // PullRaftVariant2.tla:269-270
     E.emit(t, A_UPDATETERM);
   }
 }
@@ -434,12 +476,15 @@ void HandleRequestVoteRequest(const State& s, Emitter& E) {  // Raft.tla:360-381
     int i = m.dst, j = m.src;
     int lt = LastTerm(s, i);
     bool logOk = m.lastLogTerm > lt || (m.lastLogTerm == lt && m.lastLogIndex >= Len(s, i));
-    bool grant = m.term == s.term[i] && logOk && (s.voted[i] == NIL || s.voted[i] == j);
+    // PullRaftVariant2.tla:303-326: the vote is votedFor's; the response carries the last entry
+    const int8_t* vf = C.spec == PULL2 ? s.voted2 : s.voted;
+    bool grant = m.term == s.term[i] && logOk && (vf[i] == NIL || vf[i] == j);
     Msg r = mk(RVRESP, s.term[i], i, j);
     r.voteGranted = grant;
+    if (C.spec == PULL2) { r.lastLogIndex = (int8_t)Len(s, i); r.lastLogTerm = (int8_t)lt; }
     State t = s;
     if (!reply(t, r, k)) continue;
-    if (grant) t.voted[i] = (int8_t)j;
+    if (grant) (C.spec == PULL2 ? t.voted2 : t.voted)[i] = (int8_t)j;
     E.emit(t, A_HRVREQ);
   }
 }
@@ -450,6 +495,10 @@ void HandleRequestVoteResponse(const State& s, Emitter& E) {  // Raft.tla:386-40
     const Msg& m = s.msgs[k];
     State t = s;
     if (m.voteGranted) t.votes[m.dst] |= (uint8_t)(1u << m.src);
+    if (m.voteGranted && C.spec == PULL2) {  // PullRaftVariant2.tla:342-344
+      t.vleI[m.dst][m.src] = m.lastLogIndex;
+      t.vleT[m.dst][m.src] = m.lastLogTerm;
+    }
     t.msgs[k].count--;  // Discard
     E.emit(t, A_HRVRESP);
   }
@@ -554,6 +603,9 @@ void LearnOfLeader(const State& s, Emitter& E) {  // PullRaft.tla:383-391
   for (int k = 0; k < s.nmsg; k++) {
     if (!receivable(s, k, LNREQ, true)) continue;
     State t = s;
+    const Msg& m = s.msgs[k];
+    // PullRaftVariant2.tla:404-406: NeedsTruncation / TruncateLog (:171-179)
+    if (C.spec == PULL2 && !m.lceNil && Len(s, m.dst) >= m.lciIndex) t.loglen[m.dst] = m.lciIndex;
     t.voted[s.msgs[k].dst] = s.msgs[k].src;
     t.msgs[k].count--;
     E.emit(t, A_LEARNOFLEADER);
@@ -689,7 +741,7 @@ void Next(const State& s, Emitter& E) {
       AcceptAppendEntriesRequest(s, E);
       HandleAppendEntriesResponse(s, E);
       break;
-    case PULL:  // PullRaft.tla:542-558
+    case PULL: case PULL2:  // PullRaft.tla:542-558; PullRaftVariant2.tla:560-576 (same disjuncts)
       for (int i = 0; i < N; i++) Restart(s, i, E);
       UpdateTerm(s, E);
       for (int i = 0; i < N; i++) RequestVote(s, i, E);
@@ -715,7 +767,8 @@ State Init() {  // Raft.tla:197-218 (and the variants' Init)
     s.term[i] = 1;
     s.st[i] = FOLLOWER;
     s.voted[i] = NIL;
-    for (int j = 0; j < C.N; j++) { s.next[i][j] = 1; s.match[i][j] = 0; }
+    s.voted2[i] = NIL;
+    for (int j = 0; j < C.N; j++) { s.next[i][j] = 1; s.match[i][j] = 0; s.vleI[i][j] = -1; }
   }
   return s;
 }
@@ -827,6 +880,7 @@ void canonical(const State& s, Ser& best) {
     for (int pos = 0; pos < N; pos++) {
       int i = cur[pos];
       o.put(s.voted[i] == NIL ? 255 : p[s.voted[i]]);
+      if (C.spec == PULL2) o.put(s.voted2[i] == NIL ? 255 : p[s.voted2[i]]);
       unsigned vg = 0, pd = 0;
       for (int j = 0; j < N; j++) {
         if (s.votes[i] >> j & 1) vg |= 1u << p[j];
@@ -836,8 +890,9 @@ void canonical(const State& s, Ser& best) {
       if (C.spec == RAFT) o.put(pd);
       for (int q = 0; q < N; q++) {
         int j = cur[q];
-        if (C.spec != PULL) o.put(s.next[i][j]);
+        if (!C.pull()) o.put(s.next[i][j]);
         o.put(s.match[i][j]);
+        if (C.spec == PULL2) { o.put(s.vleI[i][j] + 1); o.put(s.vleT[i][j]); }
       }
     }
     if (C.spec == PULL) for (int v = 0; v < C.V; v++) o.put(s.acked[v] + 1);
@@ -1155,7 +1210,8 @@ std::string state_json(const State& s) {
   };
   arr("currentTerm", s.term, C.N);
   arr("state", s.st, C.N);
-  arr(C.spec == PULL ? "leader" : "votedFor", s.voted, C.N);
+  arr(C.pull() ? "leader" : "votedFor", s.voted, C.N);
+  if (C.spec == PULL2) arr("votedFor", s.voted2, C.N);
   arr("commitIndex", s.commit, C.N);
   if (C.spec == FSYNC) arr("fsyncIndex", s.fsync, C.N);
   arr("acked", s.acked, C.V);
@@ -1237,6 +1293,7 @@ int main(int argc, char** argv) {
       std::string v = val();
       if (v == "Raft") C.spec = RAFT; else if (v == "FlexibleRaft") C.spec = FLEX;
       else if (v == "RaftFsync") C.spec = FSYNC; else if (v == "PullRaft") C.spec = PULL;
+      else if (v == "PullRaftVariant2") C.spec = PULL2;
       else { fprintf(stderr, "unknown spec %s\n", v.c_str()); return 2; }
     } else if (k == "--servers") C.N = std::stoi(val());
     else if (k == "--values") C.V = std::stoi(val());

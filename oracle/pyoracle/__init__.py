@@ -15,9 +15,10 @@ from .tlc import bfs, EvalError
 
 def make_spec(module, cfg):
     from .raft import RaftSpec
-    from .variants import FlexibleRaftSpec, RaftFsyncSpec, PullRaftSpec
+    from .variants import FlexibleRaftSpec, RaftFsyncSpec, PullRaftSpec, PullRaftVariant2Spec
     table = {"Raft": RaftSpec, "FlexibleRaft": FlexibleRaftSpec,
-             "RaftFsync": RaftFsyncSpec, "PullRaft": PullRaftSpec}
+             "RaftFsync": RaftFsyncSpec, "PullRaft": PullRaftSpec,
+             "PullRaftVariant2": PullRaftVariant2Spec}
     if module not in table:
         raise ValueError("oracle: unsupported module %r" % module)
     return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]))

@@ -46,6 +46,16 @@ class Rec(tuple):
                 return v
         raise AttributeError("record has no field %s" % name)
 
+    # record fields named like tuple methods (mlastCommonEntry.index,
+    # PullRaft.tla:187) must read the field, not tuple.index / tuple.count
+    @property
+    def index(self):
+        return self.__getattr__("index")
+
+    @property
+    def count(self):
+        return self.__getattr__("count")
+
     def replace(self, **kw):
         d = dict(tuple.__iter__(self))
         d.update(kw)
@@ -62,10 +72,23 @@ def _rec_from_items(items):
 def tlc_key(v):
     """Sort key reproducing TLC's compareTo for the value kinds the specs use."""
     if isinstance(v, Rec):
-        return (len(v), tuple((k, tlc_key(x)) for k, x in v))
+        return (len(v), tuple((k, _field_key(x)) for k, x in v))
     if isinstance(v, tuple):  # sequence: length first, then elements
         return (len(v), tuple(tlc_key(x) for x in v))
     return v  # ints, bools (False < True), model-value names / indices
+
+
+def _field_key(x):
+    """A record field's key.  A field that holds either the model value Nil or a
+    record (PullRaftVariant2.tla:369-375, mlastCommonEntry) compares Nil below
+    every record: TLC's untyped model value is less than any non-model value and
+    a record greater than a model value.  Record-valued fields of the other
+    specs keep their relative order (both sides wrapped the same way)."""
+    if isinstance(x, Rec):
+        return (1, tlc_key(x))
+    if type(x) is int and x == NIL:
+        return (0,)
+    return tlc_key(x)
 
 
 def seq_get(s, i):

@@ -1,10 +1,11 @@
-"""Literal restatements of FlexibleRaft.tla, RaftFsync.tla and PullRaft.tla.
+"""Literal restatements of FlexibleRaft.tla, RaftFsync.tla, PullRaft.tla and
+PullRaftVariant2.tla.
 
 TEST INFRASTRUCTURE ONLY.  The Raft-derived variants subclass RaftSpec and
 override exactly the operators whose TLA+ text differs (cited per method);
-PullRaft is restated in full.
+PullRaft is restated in full, PullRaftVariant2 as its differences from it.
 """
-from .tlc import NIL, Rec, seq_get, fset, fset2, freeze_msgs, msg_in
+from .tlc import NIL, Rec, seq_get, fset, fset2, freeze_msgs, msg_in, tlc_key
 from .raft import (RaftSpec, FOLLOWER, CANDIDATE, LEADER, RVREQ, RVRESP, AEREQ,
                    AERESP, EQUAL, LEQ)
 
@@ -590,4 +591,181 @@ class PullRaftSpec(RaftSpec):
             return tuple(out)
         if var == "acked":
             return val
+        return RaftSpec.permute_value(self, var, val, p)
+
+
+# -------------------------------------------------------- PullRaftVariant2
+class PullRaftVariant2Spec(PullRaftSpec):
+    """MODULE PullRaftVariant2 (pull-raft/PullRaftVariant2.tla): PullRaft, but a
+    follower pulls only after a LeaderNotifyRequest names the leader; votedFor
+    is a variable again, candidates record each voter's last log entry
+    (votesLastEntry) and the leader's notification carries the last common
+    entry, which the follower truncates to (:12-26 of the notes)."""
+    module = "PullRaftVariant2"
+    # declaration order of VARIABLES (PullRaftVariant2.tla:56-106)
+    variables = ("messages", "acked", "electionCtr", "restartCtr", "currentTerm",
+                 "state", "leader", "votedFor", "log", "commitIndex", "votesGranted",
+                 "votesLastEntry", "matchIndex")
+    # view == <<messages, serverVars, candidateVars, leaderVars, logVars>> (:114): acked is hidden
+    hidden_vars = ("acked", "electionCtr", "restartCtr")
+
+    def init_states(self):
+        # PullRaftVariant2.tla:222-243
+        N = self.N
+        for s in PullRaftSpec.init_states(self):
+            s["votedFor"] = tuple(NIL for _ in range(N))
+            s["votesLastEntry"] = tuple(tuple(NIL for _ in range(N)) for _ in range(N))
+            yield s
+
+    def Restart(self, s, i):
+        # PullRaftVariant2.tla:251-260
+        if not s["restartCtr"] < self.MaxRestarts:
+            return
+        t = dict(s)
+        t["state"] = fset(s["state"], i, FOLLOWER)
+        t["leader"] = fset(s["leader"], i, NIL)
+        t["votesGranted"] = fset(s["votesGranted"], i, frozenset())
+        t["votesLastEntry"] = fset(s["votesLastEntry"], i, tuple(NIL for _ in range(self.N)))
+        t["matchIndex"] = fset(s["matchIndex"], i, tuple(0 for _ in range(self.N)))
+        t["commitIndex"] = fset(s["commitIndex"], i, 0)
+        t["restartCtr"] = s["restartCtr"] + 1
+        yield t
+
+    def UpdateTerm(self, s):
+        # PullRaftVariant2.tla:264-272
+        for m, _ in s["messages"]:
+            d = m.mdest
+            if m.mterm > s["currentTerm"][d]:
+                t = dict(s)
+                t["currentTerm"] = fset(s["currentTerm"], d, m.mterm)
+                t["state"] = fset(s["state"], d, FOLLOWER)
+                t["votedFor"] = fset(s["votedFor"], d, NIL)
+                t["leader"] = fset(s["leader"], d, NIL)
+                yield t
+
+    def RequestVote(self, s, i):
+        # PullRaftVariant2.tla:279-295
+        if not s["electionCtr"] < self.MaxElections:
+            return
+        if s["state"][i] not in (FOLLOWER, CANDIDATE):
+            return
+        term = s["currentTerm"][i] + 1
+        ms = [Rec(mtype=RVREQ, mterm=term, mlastLogTerm=self.LastTerm(s["log"][i]),
+                  mlastLogIndex=len(s["log"][i]), msource=i, mdest=j)
+              for j in self.Server if j != i]
+        msgs = RaftSpec.SendMultipleOnce(s["messages"], ms)
+        if msgs is None:
+            return
+        t = dict(s)
+        t["state"] = fset(s["state"], i, CANDIDATE)
+        t["currentTerm"] = fset(s["currentTerm"], i, term)
+        t["votedFor"] = fset(s["votedFor"], i, i)
+        t["votesGranted"] = fset(s["votesGranted"], i, frozenset([i]))
+        t["leader"] = fset(s["leader"], i, NIL)
+        t["electionCtr"] = s["electionCtr"] + 1
+        t["messages"] = msgs
+        yield t
+
+    def HandleRequestVoteRequest(self, s):
+        # PullRaftVariant2.tla:303-326: grant on votedFor; the response carries the voter's last entry
+        for m, c in s["messages"]:
+            if not self.ReceivableMessage(s, m, c, RVREQ, LEQ):
+                continue
+            i, j = m.mdest, m.msource
+            lt = self.LastTerm(s["log"][i])
+            logOk = (m.mlastLogTerm > lt or
+                     (m.mlastLogTerm == lt and m.mlastLogIndex >= len(s["log"][i])))
+            grant = (m.mterm == s["currentTerm"][i] and logOk and s["votedFor"][i] in (NIL, j))
+            if not m.mterm <= s["currentTerm"][i]:
+                continue
+            resp = Rec(mtype=RVRESP, mterm=s["currentTerm"][i], mvoteGranted=grant,
+                       mlastLogIndex=len(s["log"][i]), mlastLogTerm=lt, msource=i, mdest=j)
+            msgs = self.Reply(s["messages"], resp, m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            if grant:
+                t["votedFor"] = fset(s["votedFor"], i, j)
+            t["messages"] = msgs
+            yield t
+
+    def HandleRequestVoteResponse(self, s):
+        # PullRaftVariant2.tla:331-349
+        for m, c in s["messages"]:
+            if not self.ReceivableMessage(s, m, c, RVRESP, EQUAL):
+                continue
+            i, j = m.mdest, m.msource
+            msgs = self.Discard(s["messages"], m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            if m.mvoteGranted:
+                t["votesGranted"] = fset(s["votesGranted"], i, s["votesGranted"][i] | {j})
+                t["votesLastEntry"] = fset2(s["votesLastEntry"], i, j,
+                                            Rec(index=m.mlastLogIndex, term=m.mlastLogTerm))
+            t["messages"] = msgs
+            yield t
+
+    def BecomeLeader(self, s, i):
+        # PullRaftVariant2.tla:361-379: notify every other server, with the last
+        # common entry for the voters whose last entry is known
+        if s["state"][i] != CANDIDATE or not self.IsQuorum(s["votesGranted"][i]):
+            return
+        ms = []
+        for j in self.Server:
+            if j == i:
+                continue
+            vle = s["votesLastEntry"][i][j]
+            lce = NIL if vle == NIL else self.LastCommonEntry(s, i, vle.index, vle.term)
+            ms.append(Rec(mtype=LNREQ, mterm=s["currentTerm"][i], mlastCommonEntry=lce,
+                          msource=i, mdest=j))
+        msgs = RaftSpec.SendMultipleOnce(s["messages"], ms)
+        if msgs is None:
+            return
+        t = dict(s)
+        t["state"] = fset(s["state"], i, LEADER)
+        t["leader"] = fset(s["leader"], i, i)
+        t["matchIndex"] = fset(s["matchIndex"], i, tuple(0 for _ in range(self.N)))
+        t["messages"] = msgs
+        yield t
+
+    def NeedsTruncation(self, s, i, m):
+        # PullRaftVariant2.tla:171-173
+        return m.mlastCommonEntry != NIL and len(s["log"][i]) >= m.mlastCommonEntry.index
+
+    def LearnOfLeader(self, s):
+        # PullRaftVariant2.tla:398-410 (the LET's `index == m.mlastLogIndex` is never used)
+        for m, c in s["messages"]:
+            if not self.ReceivableMessage(s, m, c, LNREQ, EQUAL):
+                continue
+            i, j = m.mdest, m.msource
+            msgs = self.Discard(s["messages"], m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            if self.NeedsTruncation(s, i, m):
+                t["log"] = fset(s["log"], i, self.PTruncateLog(s, i, m))
+            t["leader"] = fset(s["leader"], i, j)
+            t["messages"] = msgs
+            yield t
+
+    def actions(self):
+        """Next (PullRaftVariant2.tla:560-576): PullRaft's disjuncts in the same order."""
+        return PullRaftSpec.actions(self)
+
+    def permute_value(self, var, val, p):
+        # canonical forms only need an injective, totally ordered encoding:
+        # Nil and records are mapped to comparable keys
+        N = self.N
+        inv = [0] * N
+        for a, b in enumerate(p):
+            inv[b] = a
+        if var == "messages":
+            out = [(tlc_key(m.replace(msource=p[m.msource], mdest=p[m.mdest])), c) for m, c in val]
+            out.sort()
+            return tuple(out)
+        if var == "votesLastEntry":
+            def k(x):
+                return (0,) if x == NIL else (1, x.index, x.term)
+            return tuple(tuple(k(val[inv[a]][inv[b]]) for b in range(N)) for a in range(N))
         return RaftSpec.permute_value(self, var, val, p)

@@ -179,6 +179,7 @@ int spec_of_module(const std::string& m) {
   if (m == "FlexibleRaft") return FLEX;
   if (m == "RaftFsync") return FSYNC;
   if (m == "PullRaft") return PULL;
+  if (m == "PullRaftVariant2") return PULL2;
   return -1;
 }
 
@@ -206,7 +207,7 @@ void build_actions(Model& M) {
            {A_ADVCOMMIT, K_I}, {A_APPENDENTRIES, K_IJ}, {A_ADVFSYNC, K_I}, {A_UPDATETERM, K_MSG},
            {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG}, {A_REJAE, K_MSG}, {A_ACCAE, K_MSG}, {A_HAERESP, K_MSG}};
       break;
-    case PULL:  // PullRaft.tla:542-558
+    case PULL: case PULL2:  // PullRaft.tla:542-558; PullRaftVariant2.tla:560-576 (same disjuncts)
       t = {{A_RESTART, K_I}, {A_UPDATETERM, K_MSG}, {A_REQUESTVOTE, K_I}, {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG},
            {A_BECOMELEADER, K_I}, {A_CLIENT, K_IV}, {A_REJPULL, K_MSG}, {A_ACCPULL, K_MSG}, {A_LEARN, K_MSG},
            {A_SENDPULL, K_IJ}, {A_HSUCC, K_MSG}, {A_HFAIL, K_MSG}};
@@ -285,6 +286,7 @@ unsigned long long known_spec_hash(const std::string& module) {
       {"FlexibleRaft", 0xc4f3c1e150bbc233ULL},  // specifications/flexible-raft/FlexibleRaft.tla
       {"PullRaft", 0x158f1b6f8dd861a3ULL},      // specifications/pull-raft/PullRaft.tla
       {"RaftFsync", 0x8135c01b3aedbce3ULL},     // specifications/raft-and-fsync/RaftFsync.tla
+      {"PullRaftVariant2", 0xa830c4c4ebcf30b0ULL},  // specifications/pull-raft/PullRaftVariant2.tla
   };
   auto it = k.find(module);
   return it == k.end() ? 0 : it->second;
@@ -298,7 +300,7 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     int spec = spec_of_module(module);
     if (spec < 0)
       throw std::runtime_error("unsupported module '" + module +
-                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft)");
+                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft, PullRaftVariant2)");
     if (!tla_text.empty() && tla_text.find("MODULE " + module) == std::string::npos)
       throw std::runtime_error("the .tla file does not declare MODULE " + module);
     if (!tla_text.empty()) {
@@ -404,6 +406,10 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
         m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "leader", "log",
                         "commitIndex", "votesGranted", "matchIndex"};
         break;
+      case PULL2:  // declaration order, PullRaftVariant2.tla:56-106
+        m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "leader",
+                        "votedFor", "log", "commitIndex", "votesGranted", "votesLastEntry", "matchIndex"};
+        break;
     }
   } catch (std::exception& e) {
     delete m;
@@ -442,9 +448,10 @@ std::vector<uint32_t> init_state(const Model& M) {
   S[0] = 0;  // nmsg 0, counters 0, acked all Nil (Raft.tla:209-213)
   for (int i = 0; i < M.N; i++) {
     uint32_t a = 1u | (FOLLOWER << 4) | ((uint32_t)NILS << 6);  // currentTerm 1, Follower, votedFor Nil
+    if (M.spec == PULL2) a |= (uint32_t)NILS << 15;          // leader and votedFor Nil (PullRaftVariant2.tla:224-225)
     S[1 + 4 * i] = a;
     S[2 + 4 * i] = 0;
-    S[3 + 4 * i] = M.spec == PULL ? 0u : all_rows(M.N, 1);  // nextIndex = 1
+    S[3 + 4 * i] = pullish(M.spec) ? 0u : all_rows(M.N, 1);  // nextIndex = 1; Variant2: votesLastEntry Nil
     S[4 + 4 * i] = 0;                                        // matchIndex = 0
   }
   return S;
@@ -471,7 +478,8 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
       else {
         val = "(";
         for (int k = 0; k < nm; k++) {
-          MsgF f = M.spec == PULL ? msg_decode<PULL>(S[1 + 4 * M.N + k]) : msg_decode<RAFT>(S[1 + 4 * M.N + k]);
+          const uint32_t mw = S[1 + 4 * M.N + k];
+          MsgF f = M.spec == PULL2 ? msg_decode<PULL2>(mw) : M.spec == PULL ? msg_decode<PULL>(mw) : msg_decode<RAFT>(mw);
           std::string r;
           auto B = [](int x) { return std::string(x ? "TRUE" : "FALSE"); };
           auto ents = [&](int n, int t, int v) { return n ? "<<" + entry(t, v) + ">>" : std::string("<<>>"); };
@@ -487,8 +495,13 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
                   ", mtype |-> PullEntriesRequest]";
               break;
             case RVRESP:
-              r = "[mdest |-> " + sv(f.dst) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
-                  ", mtype |-> RequestVoteResponse, mvoteGranted |-> " + B(f.granted) + "]";
+              if (M.spec == PULL2)
+                r = "[mdest |-> " + sv(f.dst) + ", mlastLogIndex |-> " + std::to_string(f.lli) +
+                    ", mlastLogTerm |-> " + std::to_string(f.llt) + ", msource |-> " + sv(f.src) + ", mterm |-> " +
+                    std::to_string(f.term) + ", mtype |-> RequestVoteResponse, mvoteGranted |-> " + B(f.granted) + "]";
+              else
+                r = "[mdest |-> " + sv(f.dst) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                    ", mtype |-> RequestVoteResponse, mvoteGranted |-> " + B(f.granted) + "]";
               break;
             case AEREQ:
               r = "[mcommitIndex |-> " + std::to_string(f.commit) + ", mdest |-> " + sv(f.dst) + ", mentries |-> " +
@@ -502,8 +515,15 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
                   ", mtype |-> AppendEntriesResponse]";
               break;
             case LNREQ:
-              r = "[mdest |-> " + sv(f.dst) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
-                  ", mtype |-> LeaderNotifyRequest]";
+              if (M.spec == PULL2)
+                r = "[mdest |-> " + sv(f.dst) + ", mlastCommonEntry |-> " +
+                    (f.lcenil ? std::string("Nil")
+                              : "[index |-> " + std::to_string(f.lci) + ", term |-> " + std::to_string(f.lct) + "]") +
+                    ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                    ", mtype |-> LeaderNotifyRequest]";
+              else
+                r = "[mdest |-> " + sv(f.dst) + ", msource |-> " + sv(f.src) + ", mterm |-> " + std::to_string(f.term) +
+                    ", mtype |-> LeaderNotifyRequest]";
               break;
             case PERESP:
               if (f.success)
@@ -535,7 +555,19 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
         int st = a_st(S[1 + 4 * i]);
         return std::string(st == FOLLOWER ? "Follower" : st == CANDIDATE ? "Candidate" : "Leader");
       });
+    else if (var == "votedFor" && M.spec == PULL2) val = fn([&](int i) { return sv(a_votedfor2(S[1 + 4 * i])); });
     else if (var == "votedFor" || var == "leader") val = fn([&](int i) { return sv(a_voted(S[1 + 4 * i])); });
+    else if (var == "votesLastEntry")
+      val = fn([&](int i) {
+        std::string o2 = "(";
+        for (int j = 0; j < M.N; j++) {
+          const uint32_t v = j == i ? 0u : vle_get(S[3 + 4 * i], i, j);
+          o2 += (j ? " @@ " : "") + m->server_names[j] + " :> " +
+                (v ? "[index |-> " + std::to_string((int)(v & 7u) - 1) + ", term |-> " + std::to_string((int)(v >> 3)) + "]"
+                   : std::string("Nil"));
+        }
+        return o2 + ")";
+      });
     else if (var == "log")
       val = fn([&](int i) {
         uint32_t a = S[1 + 4 * i], b = S[2 + 4 * i];

@@ -88,6 +88,10 @@ static int inv_t(const Model& M, const uint32_t* S, int* err) {
     case PULL * 8 + 3: return FN<PULL, 3>(__VA_ARGS__);          \
     case PULL * 8 + 4: return FN<PULL, 4>(__VA_ARGS__);          \
     case PULL * 8 + 5: return FN<PULL, 5>(__VA_ARGS__);          \
+    case PULL2 * 8 + 2: return FN<PULL2, 2>(__VA_ARGS__);        \
+    case PULL2 * 8 + 3: return FN<PULL2, 3>(__VA_ARGS__);        \
+    case PULL2 * 8 + 4: return FN<PULL2, 4>(__VA_ARGS__);        \
+    case PULL2 * 8 + 5: return FN<PULL2, 5>(__VA_ARGS__);        \
   }
 
 int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,
@@ -128,8 +132,8 @@ namespace rmc {
 std::vector<uint32_t> selftest_init_state(const Model& M) {
   std::vector<uint32_t> S(M.words, 0u);
   for (int i = 0; i < M.N; i++) {
-    S[1 + 4 * i] = 1u | ((uint32_t)NILS << 6);
-    S[3 + 4 * i] = M.spec == PULL ? 0u : all_rows(M.N, 1);
+    S[1 + 4 * i] = 1u | ((uint32_t)NILS << 6) | (M.spec == PULL2 ? (uint32_t)NILS << 15 : 0u);
+    S[3 + 4 * i] = pullish(M.spec) ? 0u : all_rows(M.N, 1);
   }
   return S;
 }
@@ -141,16 +145,23 @@ extern "C" int rmc_selftest_encode_msg(int spec, const int* f, uint32_t* out) {
   m.type = f[0]; m.term = f[1]; m.src = f[2]; m.dst = f[3]; m.lli = f[4]; m.llt = f[5]; m.granted = f[6];
   m.pli = f[7]; m.plt = f[8]; m.nent = f[9]; m.eterm = f[10]; m.evalue = f[11]; m.commit = f[12];
   m.success = f[13]; m.midx = f[14]; m.lci = f[15]; m.lct = f[16]; m.count = f[17];
-  *out = spec == PULL ? msg_encode<PULL>(m) : msg_encode<RAFT>(m);
-  MsgF d = spec == PULL ? msg_decode<PULL>(*out) : msg_decode<RAFT>(*out);
-  int sp, dp;
-  if (spec == PULL) msg_srcdst_pos<PULL>(*out, sp, dp); else msg_srcdst_pos<RAFT>(*out, sp, dp);
-  int term = spec == PULL ? msg_term<PULL>(*out) : msg_term<RAFT>(*out);
-  int type = spec == PULL ? msg_type<PULL>(*out) : msg_type<RAFT>(*out);
+  if (spec == PULL2) m.lcenil = f[18];  // the PullRaftVariant2 probe passes 19 fields
+  MsgF d;
+  int sp, dp, term, type;
+  if (spec == PULL2) {
+    *out = msg_encode<PULL2>(m); d = msg_decode<PULL2>(*out); msg_srcdst_pos<PULL2>(*out, sp, dp);
+    term = msg_term<PULL2>(*out); type = msg_type<PULL2>(*out);
+  } else if (spec == PULL) {
+    *out = msg_encode<PULL>(m); d = msg_decode<PULL>(*out); msg_srcdst_pos<PULL>(*out, sp, dp);
+    term = msg_term<PULL>(*out); type = msg_type<PULL>(*out);
+  } else {
+    *out = msg_encode<RAFT>(m); d = msg_decode<RAFT>(*out); msg_srcdst_pos<RAFT>(*out, sp, dp);
+    term = msg_term<RAFT>(*out); type = msg_type<RAFT>(*out);
+  }
   int ok = d.type == m.type && d.term == m.term && d.src == m.src && d.dst == m.dst && d.lli == m.lli &&
            d.llt == m.llt && d.granted == m.granted && d.pli == m.pli && d.plt == m.plt && d.nent == m.nent &&
            d.eterm == m.eterm && d.evalue == m.evalue && d.commit == m.commit && d.success == m.success &&
-           d.midx == m.midx && d.lci == m.lci && d.lct == m.lct && d.count == m.count &&
+           d.midx == m.midx && d.lci == m.lci && d.lct == m.lct && d.lcenil == m.lcenil && d.count == m.count &&
            (int)((*out >> sp) & 7u) == m.src && (int)((*out >> dp) & 7u) == m.dst && term == m.term &&
            type == m.type;
   return ok ? 0 : 1;

@@ -799,6 +799,7 @@ static void dispatch(int spec, int N, bool expand, const LevelArgs& a, hipStream
     case FLEX: dispatch_n<FLEX>(N, expand, a, s); break;
     case FSYNC: dispatch_n<FSYNC>(N, expand, a, s); break;
     case PULL: dispatch_n<PULL>(N, expand, a, s); break;
+    case PULL2: dispatch_n<PULL2>(N, expand, a, s); break;
   }
 }
 
@@ -932,6 +933,7 @@ void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long w
   RMC_SIM(FLEX, 2) RMC_SIM(FLEX, 3) RMC_SIM(FLEX, 4) RMC_SIM(FLEX, 5)
   RMC_SIM(FSYNC, 2) RMC_SIM(FSYNC, 3) RMC_SIM(FSYNC, 4) RMC_SIM(FSYNC, 5)
   RMC_SIM(PULL, 2) RMC_SIM(PULL, 3) RMC_SIM(PULL, 4) RMC_SIM(PULL, 5)
+  RMC_SIM(PULL2, 2) RMC_SIM(PULL2, 3) RMC_SIM(PULL2, 4) RMC_SIM(PULL2, 5)
 #undef RMC_SIM
 }
 

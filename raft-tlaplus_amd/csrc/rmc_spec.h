@@ -10,8 +10,12 @@
 //                   (7 = Nil) | Len(log) 9-11 | commitIndex 12-14 |
 //                   fsyncIndex 15-17 | votesGranted 18-24 | pendingResponse 25-31
 //   S[1+4i+1] (B)   log: entry x (0-based) at 6x: term 0-3 | value 4-5
-//   S[1+4i+2] (C)   nextIndex[i][j] at 3j
+//   S[1+4i+2] (C)   nextIndex[i][j] at 3j (PullRaft: unused; PullRaftVariant2:
+//                   votesLastEntry[i][j] for j != i at 7*slot(i, j), slot =
+//                   j - (j > i): index+1 0-2 (0 = Nil) | term 3-6)
 //   S[1+4i+3] (D)   matchIndex[i][j] at 3j
+//   PullRaft: bits 6-8 of A hold leader[i]; PullRaftVariant2: leader[i] in
+//   6-8 and votedFor[i] in 15-17 (the fsyncIndex bits of RaftFsync).
 //   S[1+4N+k]       DOMAIN messages, ascending = TLC's value order; record in
 //                   bits 3-31 (layouts below), count (messages[m]) in bits 0-2.
 //
@@ -28,6 +32,9 @@
 //   PullRaft.tla:405-410 PullReq {same names as RVReq}
 //   PullRaft.tla:426-433 PullResp fail {mdest, mlastCommonEntry, msource, msuccess, mterm, mtype}
 //   PullRaft.tla:480-486 PullResp ok   {mcommitIndex, mdest, mentries, msource, msuccess, mterm, mtype}
+//   PullRaftVariant2.tla:317-323 RVResp {mdest, mlastLogIndex, mlastLogTerm, msource, mterm, mtype, mvoteGranted}
+//   PullRaftVariant2.tla:369-377 LeaderNotify {mdest, mlastCommonEntry, msource, mterm, mtype}, where
+//                       mlastCommonEntry is Nil (below every record) or [index, term]
 #pragma once
 #include <stdint.h>
 #if defined(__HIPCC__)
@@ -39,7 +46,9 @@
 
 namespace rmc {
 
-enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3 };
+enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3, PULL2 = 4 };
+// the pull family (PullRaft, PullRaftVariant2): no nextIndex, LeaderNotify, pull replication
+constexpr bool pullish(int spec) { return spec == PULL || spec == PULL2; }
 enum SrvState { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 enum MType { RVREQ = 0, RVRESP = 1, AEREQ = 2, AERESP = 3, LNREQ = 4, PEREQ = 5, PERESP = 6 };
 enum ActId {
@@ -101,10 +110,18 @@ RMC_HD int a_fsync(uint32_t a) { return (int)getb(a, 15, 3); }
 RMC_HD int a_votes(uint32_t a) { return (int)getb(a, 18, 7); }
 RMC_HD int a_pending(uint32_t a) { return (int)getb(a, 25, 7); }
 // The variables VIEW drops, from a header word (16 bits): electionCtr,
-// restartCtr and acked (Raft.tla:115, FlexibleRaft.tla:117, RaftFsync.tla:117);
-// PullRaft's view keeps acked, so only the counters (PullRaft.tla:123).
+// restartCtr and acked (Raft.tla:115, FlexibleRaft.tla:117, RaftFsync.tla:117,
+// PullRaftVariant2.tla:114); PullRaft's view keeps acked, so only the counters
+// (PullRaft.tla:123).
 template <int SPEC>
 RMC_HD uint32_t hidden_of(uint32_t h) { return SPEC == 3 /* PULL */ ? (h >> 8) & 0xFFu : (h >> 8) & 0xFFFFu; }
+// PullRaftVariant2: votedFor[i] (bits 15-17 of A) and votesLastEntry row (C)
+RMC_HD int a_votedfor2(uint32_t a) { return (int)getb(a, 15, 3); }
+RMC_HD int vle_slot(int i, int j) { return j - (j > i ? 1 : 0); }
+RMC_HD uint32_t vle_get(uint32_t c, int i, int j) { return (c >> (7 * vle_slot(i, j))) & 0x7Fu; }  // 0 = Nil
+RMC_HD uint32_t vle_set(uint32_t c, int i, int j, int index, int term) {
+  return setb(c, 7 * vle_slot(i, j), 7, (uint32_t)((index + 1) | (term << 3)));
+}
 // log word B
 RMC_HD int e_term(uint32_t b, int x) { return (int)getb(b, 6 * x, 4); }
 RMC_HD int e_value(uint32_t b, int x) { return (int)getb(b, 6 * x + 4, 2); }
@@ -123,12 +140,13 @@ struct MsgF {
   int commit;                 // mcommitIndex
   int success, midx;          // msuccess, mmatchIndex
   int lci, lct;               // mlastCommonEntry.index/.term
+  int lcenil;                 // PullRaftVariant2 LeaderNotify: mlastCommonEntry = Nil
   int count;
 };
 RMC_HD MsgF msg_zero() {
   MsgF f;
   f.type = f.term = f.src = f.dst = f.lli = f.llt = f.granted = f.pli = f.plt = 0;
-  f.nent = f.eterm = f.evalue = f.commit = f.success = f.midx = f.lci = f.lct = f.count = 0;
+  f.nent = f.eterm = f.evalue = f.commit = f.success = f.midx = f.lci = f.lct = f.lcenil = f.count = 0;
   return f;
 }
 struct Bits {
@@ -141,10 +159,35 @@ struct Rd {
   int pos;
   RMC_HD int get(int w) { pos -= w; return (int)((v >> pos) & ((1u << w) - 1u)); }
 };
+// PullRaftVariant2's record classes, in TLC order (field count, then names):
+//   cls0 LeaderNotify (5 fields): dst | lce Nil 0 / record 1 | lce.index 3 | lce.term 4 | src | term
+//   cls1 6 fields, mdest first: dst | 0 = PullResp fail (mlastCommonEntry < mlastLogIndex) | 1 = request
+//   cls2 PullResp ok (7 fields, mcommitIndex first), as PullRaft's cls3
+//   cls3 RVResp (7 fields, mdest first): dst | lli | llt | src | term | granted
 template <int SPEC>
 RMC_HD uint32_t msg_encode(const MsgF& f) {
   Bits b{0u, 32};
-  if (SPEC != PULL) {
+  if (SPEC == PULL2) {
+    switch (f.type) {
+      case LNREQ:
+        b.put(0, 2); b.put(f.dst, 3); b.put(f.lcenil ? 0 : 1, 1); b.put(f.lcenil ? 0 : f.lci, 3);
+        b.put(f.lcenil ? 0 : f.lct, 4); b.put(f.src, 3); b.put(f.term, 4); break;
+      case RVRESP:
+        b.put(3, 2); b.put(f.dst, 3); b.put(f.lli, 3); b.put(f.llt, 4); b.put(f.src, 3); b.put(f.term, 4);
+        b.put(f.granted, 1); break;
+      case RVREQ: case PEREQ:
+        b.put(1, 2); b.put(f.dst, 3); b.put(1, 1); b.put(f.lli, 3); b.put(f.llt, 4); b.put(f.src, 3); b.put(f.term, 4);
+        b.put(f.type == RVREQ ? 1 : 0, 1); break;
+      default: /* PERESP */
+        if (!f.success) {
+          b.put(1, 2); b.put(f.dst, 3); b.put(0, 1); b.put(f.lci, 3); b.put(f.lct, 4); b.put(f.src, 3); b.put(0, 1); b.put(f.term, 4);
+        } else {
+          b.put(2, 2); b.put(f.commit, 3); b.put(f.dst, 3); b.put(f.nent, 1); b.put(f.eterm, 4); b.put(f.evalue, 2);
+          b.put(f.src, 3); b.put(1, 1); b.put(f.term, 4);
+        }
+        break;
+    }
+  } else if (SPEC != PULL) {
     switch (f.type) {
       case RVRESP: b.put(0, 2); b.put(f.dst, 3); b.put(f.src, 3); b.put(f.term, 4); b.put(f.granted, 1); break;
       case RVREQ: b.put(1, 2); b.put(f.dst, 3); b.put(0, 1); b.put(f.lli, 3); b.put(f.llt, 4); b.put(f.src, 3); b.put(f.term, 4); break;
@@ -178,7 +221,22 @@ RMC_HD MsgF msg_decode(uint32_t w) {
   Rd r{w, 32};
   f.count = (int)(w & 7u);
   int cls = r.get(2);
-  if (SPEC != PULL) {
+  if (SPEC == PULL2) {
+    if (cls == 0) {
+      f.type = LNREQ; f.dst = r.get(3); f.lcenil = r.get(1) ? 0 : 1; f.lci = r.get(3); f.lct = r.get(4);
+      f.src = r.get(3); f.term = r.get(4);
+    } else if (cls == 1) {
+      f.dst = r.get(3);
+      if (r.get(1) == 0) { f.type = PERESP; f.success = 0; f.lci = r.get(3); f.lct = r.get(4); f.src = r.get(3); r.get(1); f.term = r.get(4); }
+      else { f.lli = r.get(3); f.llt = r.get(4); f.src = r.get(3); f.term = r.get(4); f.type = r.get(1) ? RVREQ : PEREQ; }
+    } else if (cls == 2) {
+      f.type = PERESP; f.success = 1; f.commit = r.get(3); f.dst = r.get(3); f.nent = r.get(1); f.eterm = r.get(4);
+      f.evalue = r.get(2); f.src = r.get(3); r.get(1); f.term = r.get(4);
+    } else {
+      f.type = RVRESP; f.dst = r.get(3); f.lli = r.get(3); f.llt = r.get(4); f.src = r.get(3); f.term = r.get(4);
+      f.granted = r.get(1);
+    }
+  } else if (SPEC != PULL) {
     if (cls == 0) { f.type = RVRESP; f.dst = r.get(3); f.src = r.get(3); f.term = r.get(4); f.granted = r.get(1); }
     else if (cls == 1) {
       f.dst = r.get(3);
@@ -210,10 +268,17 @@ RMC_HD MsgF msg_decode(uint32_t w) {
 //   Pull  cls0 LN      dst27 src24 term20 | cls1 RVResp dst27 src24 term20 |
 //         cls2 fail    dst27 src16 term11 | cls2 req   dst27 src16 term12 (isRV at 11) |
 //         cls3 ok      dst24 src14 term9
+//   Pull2 cls0 LN      dst27 src16 term12 | cls1 fail   dst27 src16 term11 |
+//         cls1 req     dst27 src16 term12 (isRV at 11) | cls2 ok dst24 src14 term9 |
+//         cls3 RVResp  dst27 src17 term13
 template <int SPEC>
 RMC_HD void msg_srcdst_pos(uint32_t w, int& sp, int& dp) {
   int cls = (int)(w >> 30);
-  if (SPEC != PULL) {
+  if (SPEC == PULL2) {
+    if (cls == 0 || cls == 1) { dp = 27; sp = 16; }
+    else if (cls == 2) { dp = 24; sp = 14; }
+    else { dp = 27; sp = 17; }
+  } else if (SPEC != PULL) {
     if (cls == 0) { dp = 27; sp = 24; }
     else if (cls == 1) { dp = 27; sp = ((w >> 26) & 1u) ? 20 : 16; }
     else { dp = 24; sp = 7; }
@@ -226,6 +291,12 @@ RMC_HD void msg_srcdst_pos(uint32_t w, int& sp, int& dp) {
 template <int SPEC>
 RMC_HD int msg_type(uint32_t w) {
   int cls = (int)(w >> 30);
+  if (SPEC == PULL2) {
+    if (cls == 0) return LNREQ;
+    if (cls == 1) return ((w >> 26) & 1u) ? (((w >> 11) & 1u) ? RVREQ : PEREQ) : PERESP;
+    if (cls == 2) return PERESP;
+    return RVRESP;
+  }
   if (SPEC != PULL) {
     if (cls == 0) return RVRESP;
     if (cls == 1) return ((w >> 26) & 1u) ? AERESP : RVREQ;
@@ -240,7 +311,12 @@ template <int SPEC>
 RMC_HD int msg_term(uint32_t w) {
   int cls = (int)(w >> 30);
   int pos;
-  if (SPEC != PULL) {
+  if (SPEC == PULL2) {
+    if (cls == 0) pos = 12;
+    else if (cls == 1) pos = ((w >> 26) & 1u) ? 12 : 11;
+    else if (cls == 2) pos = 9;
+    else pos = 13;
+  } else if (SPEC != PULL) {
     if (cls == 0) pos = 20;
     else if (cls == 1) pos = ((w >> 26) & 1u) ? 15 : 12;
     else pos = 3;
@@ -397,6 +473,20 @@ RMC_HD uint32_t all_rows(int N, int v) {
   return w;
 }
 
+// LastCommonEntry(i, lastIndex, lastTerm) (PullRaft.tla:211-226,
+// PullRaftVariant2.tla:202-217): the highest index of log[i] whose entry
+// compares <= (lastIndex, lastTerm) (term first), with its term; [0, 0] if none.
+RMC_HD int last_common_entry(uint32_t a, uint32_t b, int lastIndex, int lastTerm, int& term) {
+  int idx = 0;
+  for (int x = 1; x <= a_len(a); x++) {
+    int t = e_term(b, x - 1);
+    int cmp = t > lastTerm ? 1 : (t == lastTerm && x > lastIndex) ? 1 : (t == lastTerm && x == lastIndex) ? 0 : -1;
+    if (cmp <= 0) idx = x;
+  }
+  term = idx ? e_term(b, idx - 1) : 0;
+  return idx;
+}
+
 // ---------------------------------------------------------------- actions
 // Each returns true iff the action is enabled for the binding; d receives the
 // successor.  Citations are to /root/reference/specifications/.
@@ -411,7 +501,11 @@ RMC_HD bool act_restart(const PState<SPEC, N>& s, const Model& M, int i, Delta& 
   a = setb(a, 18, 7, 0);   // votesGranted[i] = {}
   a = setb(a, 25, 7, 0);   // pendingResponse[i] = [j |-> FALSE]
   a = setb(a, 12, 3, 0);   // commitIndex[i] = 0
-  if (SPEC != PULL) d.w[2] = all_rows(N, 1);
+  if (!pullish(SPEC)) d.w[2] = all_rows(N, 1);
+  if (SPEC == PULL2) {  // PullRaftVariant2.tla:254-256: leader Nil, votesLastEntry[i] Nil (votedFor kept)
+    a = setb(a, 6, 3, NILS);
+    d.w[2] = 0;
+  }
   d.w[3] = 0;
   if (SPEC == FSYNC) {
     int f = a_fsync(a), L = a_len(a);
@@ -445,7 +539,12 @@ RMC_HD bool act_requestvote(const PState<SPEC, N>& s, const Model& M, int i, Del
   begin_srv(s, d, i);
   a = setb(a, 4, 2, CANDIDATE);
   a = setb(a, 0, 4, (uint32_t)t1);
-  a = setb(a, 6, 3, (uint32_t)i);
+  if (SPEC == PULL2) {  // PullRaftVariant2.tla:284-286: votedFor = i, leader = Nil
+    a = setb(a, 15, 3, (uint32_t)i);
+    a = setb(a, 6, 3, NILS);
+  } else {
+    a = setb(a, 6, 3, (uint32_t)i);
+  }
   a = setb(a, 18, 7, 1u << i);
   d.w[0] = a;
   d.hdr = setb(s.hdr(), 8, 4, (uint32_t)(ec + 1));
@@ -531,10 +630,27 @@ RMC_HD bool act_becomeleader(const PState<SPEC, N>& s, const Model& M, int i, De
       if (!op_send_once(s, d, msg_encode<SPEC>(m))) return false;
     }
   }
+  if (SPEC == PULL2) {
+    // PullRaftVariant2.tla:368-377: every other server; the last common entry
+    // for those whose last entry the votes reported, else Nil
+    MsgF m = msg_zero();
+    m.type = LNREQ; m.term = a_term(a); m.src = i; m.count = 1;
+    const uint32_t b = s.B(i), c = s.Cw(i);
+    for (int j = 0; j < N; j++) {
+      if (j == i) continue;
+      m.dst = j;
+      const uint32_t v = vle_get(c, i, j);
+      m.lcenil = v == 0;
+      m.lci = m.lct = 0;
+      if (v) m.lci = last_common_entry(a, b, (int)(v & 7u) - 1, (int)(v >> 3), m.lct);
+      if (!op_send_once(s, d, msg_encode<SPEC>(m))) return false;
+    }
+  }
   begin_srv(s, d, i);
   d.w[0] = setb(d.w[0], 4, 2, LEADER);
+  if (SPEC == PULL2) d.w[0] = setb(d.w[0], 6, 3, (uint32_t)i);  // leader' = i
   if (SPEC == RAFT) d.w[0] = setb(d.w[0], 25, 7, 0);
-  if (SPEC != PULL) {
+  if (!pullish(SPEC)) {
     int nx = a_len(a) + 1;
     if (nx > 7) { d.err = E_CAP_FIELD; return true; }
     d.w[2] = all_rows(N, nx);
@@ -641,6 +757,7 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
     uint32_t x = setb(a, 0, 4, (uint32_t)m.term);
     x = setb(x, 4, 2, FOLLOWER);
     x = setb(x, 6, 3, NILS);
+    if (SPEC == PULL2) x = setb(x, 15, 3, NILS);  // PullRaftVariant2.tla:269-270: votedFor and leader
     d.w[0] = x;
     return true;
   }
@@ -652,19 +769,25 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
       d.act = A_HRVREQ;
       int lt = last_term(a, b);
       bool logOk = m.llt > lt || (m.llt == lt && m.lli >= a_len(a));
-      int vf = a_voted(a);
+      // PullRaftVariant2.tla:303-326: votedFor decides, the response carries the last entry
+      int vf = SPEC == PULL2 ? a_votedfor2(a) : a_voted(a);
       bool grant = m.term == cur && logOk && (vf == NILS || vf == j);
       MsgF r = msg_zero();
       r.type = RVRESP; r.term = cur; r.granted = grant; r.src = i; r.dst = j; r.count = 1;
+      if (SPEC == PULL2) { r.lli = a_len(a); r.llt = lt; }
       if (!op_reply(s, d, msg_encode<SPEC>(r), k)) return false;
-      if (grant) { begin_srv(s, d, i); d.w[0] = setb(a, 6, 3, (uint32_t)j); }
+      if (grant) { begin_srv(s, d, i); d.w[0] = setb(a, SPEC == PULL2 ? 15 : 6, 3, (uint32_t)j); }
       return true;
     }
     case RVRESP: {
       // HandleRequestVoteResponse: Raft.tla:386-401 (EqualTerm)
       if (m.term != cur) return false;
       d.act = A_HRVRESP;
-      if (m.granted) { begin_srv(s, d, i); d.w[0] = setb(a, 18 + j, 1, 1); }
+      if (m.granted) {
+        begin_srv(s, d, i);
+        d.w[0] = setb(a, 18 + j, 1, 1);
+        if (SPEC == PULL2) d.w[2] = vle_set(d.w[2], i, j, m.lli, m.llt);  // PullRaftVariant2.tla:342-344
+      }
       op_discard(s, d, k);
       return true;
     }
@@ -730,6 +853,8 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
       d.act = A_LEARN;
       begin_srv(s, d, i);
       d.w[0] = setb(a, 6, 3, (uint32_t)j);
+      // PullRaftVariant2.tla:404-406: NeedsTruncation (:171-173) -> TruncateLog (:176-179)
+      if (SPEC == PULL2 && !m.lcenil && a_len(a) >= m.lci) log_truncate(d.w[0], d.w[1], m.lci);
       op_discard(s, d, k);
       return true;
     }
@@ -742,14 +867,8 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
       if (!valid) {
         // RejectPullEntriesRequest: PullRaft.tla:418-436, LastCommonEntry :211-226
         d.act = A_REJPULL;
-        int idx = 0;
-        for (int x = 1; x <= a_len(a); x++) {
-          int t = e_term(b, x - 1);
-          int cmp = t > m.llt ? 1 : (t == m.llt && x > m.lli) ? 1 : (t == m.llt && x == m.lli) ? 0 : -1;
-          if (cmp <= 0) idx = x;
-        }
         MsgF r = msg_zero();
-        r.type = PERESP; r.term = cur; r.success = 0; r.lci = idx; r.lct = idx ? e_term(b, idx - 1) : 0;
+        r.type = PERESP; r.term = cur; r.success = 0; r.lci = last_common_entry(a, b, m.lli, m.llt, r.lct);
         r.src = i; r.dst = j; r.count = 1;
         return op_reply(s, d, msg_encode<SPEC>(r), k);
       }
@@ -999,14 +1118,37 @@ RMC_HD uint32_t relabel_row(uint32_t row, uint32_t P) {
   for (int j = 0; j < N; j++) o |= ((row >> (3 * j)) & 7u) << (3 * perm_of(P, j));
   return o;
 }
+// PullRaftVariant2's votesLastEntry row of server i, relabelled by P
+template <int N>
+RMC_HD uint32_t relabel_vle(uint32_t c, int i, uint32_t P) {
+  uint32_t o = 0;
+  const int pi = perm_of(P, i);
+#pragma unroll
+  for (int j = 0; j < N; j++)
+    if (j != i) o |= vle_get(c, i, j) << (7 * vle_slot(pi, perm_of(P, j)));
+  return o;
+}
+// server i's words with every server-valued field relabelled by P
 template <int SPEC, int N>
-RMC_HD uint64_t h_server(uint32_t P, int i, uint32_t a, uint32_t b, uint32_t c, uint32_t dd) {
+RMC_HD void relabel_server(uint32_t P, int i, uint32_t a, uint32_t c, uint32_t dd, uint32_t& a2, uint32_t& c2,
+                           uint32_t& d2) {
   int v = a_voted(a);
-  uint32_t a2 = setb(a, 6, 3, v == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v));
+  a2 = setb(a, 6, 3, v == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v));
+  if (SPEC == PULL2) {
+    int v2 = a_votedfor2(a);
+    a2 = setb(a2, 15, 3, v2 == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v2));
+  }
   a2 = setb(a2, 18, 7, relabel_set<N>(a_votes(a), P));
   a2 = setb(a2, 25, 7, relabel_set<N>(a_pending(a), P));
+  c2 = SPEC == PULL2 ? relabel_vle<N>(c, i, P) : relabel_row<N>(c, P);
+  d2 = relabel_row<N>(dd, P);
+}
+template <int SPEC, int N>
+RMC_HD uint64_t h_server(uint32_t P, int i, uint32_t a, uint32_t b, uint32_t c, uint32_t dd) {
+  uint32_t a2, c2, d2;
+  relabel_server<SPEC, N>(P, i, a, c, dd, a2, c2, d2);
   uint64_t lo = (uint64_t)a2 | ((uint64_t)b << 32);
-  uint64_t hi = (uint64_t)relabel_row<N>(c, P) | ((uint64_t)relabel_row<N>(dd, P) << 32);
+  uint64_t hi = (uint64_t)c2 | ((uint64_t)d2 << 32);
   int pos = perm_of(P, i);
   return mix64(mix64(lo + 0x9E3779B97F4A7C15ULL * (uint64_t)(pos + 1)) ^ hi);
 }
@@ -1063,11 +1205,21 @@ RMC_HD uint32_t server_sig_own(int i, uint32_t a, uint32_t b, uint32_t c, uint32
   uint32_t votes = (uint32_t)a_votes(a), pend = (uint32_t)a_pending(a);
   uint32_t x = (a & 0x0003FE3Fu);  // term | state | Len | commitIndex | fsyncIndex
   x ^= vcls << 6;
+  if (SPEC == PULL2) {  // bits 15-17 are votedFor: its class, not its value
+    const int v2 = a_votedfor2(a);
+    x = (x & ~(7u << 15)) | ((v2 == NILS ? 0u : (v2 == i ? 1u : 2u)) << 15);
+    // votesLastEntry row: the multiset of its entries (j != i)
+    uint32_t ms = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++)
+      if (j != i) ms += mix32(vle_get(c, i, j) + 0x3C6EF372u);
+    c = ms;
+  }
   x ^= ((uint32_t)popc7(votes) << 18) | (((votes >> i) & 1u) << 21) | ((uint32_t)popc7(pend) << 22) |
        (((pend >> i) & 1u) << 25);
   uint32_t h = mix32(x + 0x9E3779B9u);
   h = mix32(h ^ b);
-  h = mix32(h ^ (row_multiset(c, N, i) + 0x85EBCA6Bu * (((c >> (3 * i)) & 7u) + 1u)));
+  h = mix32(h ^ (SPEC == PULL2 ? c : row_multiset(c, N, i) + 0x85EBCA6Bu * (((c >> (3 * i)) & 7u) + 1u)));
   h = mix32(h ^ (row_multiset(d, N, i) + 0xC2B2AE35u * (((d >> (3 * i)) & 7u) + 1u)));
   return h;
 }
@@ -1294,12 +1446,10 @@ RMC_HD uint64_t msg_u2(uint32_t w) {  // the second word's hash of a message bod
 }
 template <int SPEC, int N>
 RMC_HD uint64_t h_server2(uint32_t P, int i, uint32_t a, uint32_t b, uint32_t c, uint32_t dd) {
-  int v = a_voted(a);
-  uint32_t a2 = setb(a, 6, 3, v == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v));
-  a2 = setb(a2, 18, 7, relabel_set<N>(a_votes(a), P));
-  a2 = setb(a2, 25, 7, relabel_set<N>(a_pending(a), P));
+  uint32_t a2, c2, d2;
+  relabel_server<SPEC, N>(P, i, a, c, dd, a2, c2, d2);
   uint64_t lo = (uint64_t)a2 | ((uint64_t)b << 32);
-  uint64_t hi = (uint64_t)relabel_row<N>(c, P) | ((uint64_t)relabel_row<N>(dd, P) << 32);
+  uint64_t hi = (uint64_t)c2 | ((uint64_t)d2 << 32);
   int pos = perm_of(P, i);
   return mix64b(mix64b(lo ^ (0xD1B54A32D192ED03ULL * (uint64_t)(pos + 1))) + hi);
 }

@@ -268,8 +268,8 @@ def check_text(module, cfg_text, **kw):
 def encode_msg(spec, **f):
     """TEST HOOK: the packed word for a message record + codec self-consistency flag."""
     names = ["type", "term", "src", "dst", "lli", "llt", "granted", "pli", "plt", "nent", "eterm",
-             "evalue", "commit", "success", "midx", "lci", "lct", "count"]
-    arr = (ctypes.c_int * 18)(*[int(f.get(n, 0)) for n in names])
+             "evalue", "commit", "success", "midx", "lci", "lct", "count", "lcenil"]
+    arr = (ctypes.c_int * 19)(*[int(f.get(n, 0)) for n in names])
     out = ctypes.c_uint32()
     ok = lib().rmc_selftest_encode_msg(spec, arr, ctypes.byref(out))
     return out.value, ok == 0

@@ -95,3 +95,22 @@ ORDER = [
     ("fsync_n2v2e1r1_hidden", "RaftFsync", dict(n=2, v=2, E=1, R=1)),
     ("fsync_n2v2e2r1_hidden", "RaftFsync", dict(n=2, v=2, E=2, R=1)),
 ]
+
+# PullRaftVariant2 (pull-raft/PullRaftVariant2.tla): followers
+# pull only after LeaderNotify, which carries the last common entry.
+# (name, kwargs): both oracles (small) / C oracle (medium) / 5-server prefix
+VARIANT2_SMALL = [
+    ("pull2_n2v1e1", dict(n=2, v=1, E=1)),
+    ("pull2_n3v1e1", dict(n=3, v=1, E=1)),
+    ("pull2_n2v1e2r1", dict(n=2, v=1, E=2, R=1)),
+    ("pull2_n3v2e1", dict(n=3, v=2, E=1)),
+    ("pull2_n4v1e1", dict(n=4, v=1, E=1)),
+    # two elections: truncation on LeaderNotify and HandleFailPullEntriesResponse
+    ("pull2_n3v1e2", dict(n=3, v=1, E=2)),
+]
+VARIANT2_MEDIUM = [
+    ("pull2_n3v1e2r1", dict(n=3, v=1, E=2, R=1)),
+]
+VARIANT2_N5 = [
+    ("pull2_n5v1e1", dict(n=5, v=1, E=1), 400000, 3000),
+]

@@ -23,12 +23,14 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, cfg_text  # noqa: E402
+from cfgs import (MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM, VARIANT2_N5,  # noqa: E402
+                  VARIANT2_SMALL, cfg_text)
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
     ("Raft_cfg", "Raft", "configs/Raft.cfg"),
     ("PullRaft_cfg", "PullRaft", "configs/PullRaft.cfg"),
     ("RaftFsync_cfg", "RaftFsync", "configs/RaftFsync.cfg"),
+    ("PullRaftVariant2_cfg", "PullRaftVariant2", "configs/PullRaftVariant2.cfg"),
 ]
 
 
@@ -107,7 +109,61 @@ def order():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def variant2():
+    """--variant2: PullRaftVariant2 fixtures (tests/golden/variant2.json): small
+    cases by both oracles (every level, hidden collisions), medium by the C
+    oracle, the 5-server case level-truncated (both oracles on the prefix the
+    Python one completes), each with the C oracle's --reverse-order counts."""
+    M = "PullRaftVariant2"
+    out = {}
+    for name, kw in VARIANT2_SMALL:
+        txt = cfg_text(M, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(M, cfg["constants"], cfg["invariants"], threads=4)
+        p = bfs(make_spec(M, cfg))
+        pr = (p.generated, p.distinct, p.depth, p.status, [list(x) for x in p.levels], p.hidden_same_level)
+        cr = (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"], c["hidden_same_level"])
+        if pr != cr:
+            raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pr[:4], cr[:4]))
+        out[name] = dict(module=M, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], levels=c["levels"], action_counts=c["action_counts"],
+                         max_msgs=c["max_msgs"], hidden_same_level=c["hidden_same_level"],
+                         pinned_by="pyoracle==coracle")
+        print(name, c["generated"], c["distinct"], c["depth"], flush=True)
+    for name, kw in VARIANT2_MEDIUM:
+        txt = cfg_text(M, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(M, cfg["constants"], cfg["invariants"], threads=8)
+        out[name] = dict(module=M, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], levels=c["levels"], action_counts=c["action_counts"],
+                         max_msgs=c["max_msgs"], hidden_same_level=c["hidden_same_level"], pinned_by="coracle")
+        print(name, c["generated"], c["distinct"], c["depth"], flush=True)
+    for name, kw, c_max, py_max in VARIANT2_N5:
+        txt = cfg_text(M, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(M, cfg["constants"], cfg["invariants"], threads=8, extra=["--max-distinct", str(c_max)])
+        p = bfs(make_spec(M, cfg), max_states=py_max)
+        pl = [list(x) for x in p.levels]
+        if pl != c["levels"][:len(pl)]:
+            raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pl, c["levels"][:len(pl)]))
+        out[name] = dict(module=M, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], levels=c["levels"], max_distinct=c_max, max_msgs=c["max_msgs"],
+                         hidden_same_level=c["hidden_same_level"], pyoracle_levels=len(pl),
+                         pinned_by="coracle; first %d levels pyoracle==coracle" % len(pl))
+        print(name, c["generated"], c["distinct"], c["depth"], "py levels", len(pl), flush=True)
+    for name, g in out.items():
+        if g["status"] != "ok":
+            continue
+        cfg = parse_cfg(g["cfg"])
+        rv = run_c.run(M, cfg["constants"], cfg["invariants"], threads=1, extra=["--reverse-order"])
+        g["reverse_order"] = dict(generated=rv["generated"], distinct=rv["distinct"])
+    with open(os.path.join(HERE, "variant2.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--variant2" in sys.argv:
+        return variant2()
     if "--order" in sys.argv:
         return order()
     if "--shipped-one" in sys.argv:

@@ -68,7 +68,7 @@ def test_tight_rows_from_the_previous_check(name):
     assert r2["max_msgs"] == g["max_msgs"]
 
 
-N_SERVERS = {"Raft": 3, "PullRaft": 3, "RaftFsync": 3, "FlexibleRaft": 5}
+N_SERVERS = {"Raft": 3, "PullRaft": 3, "RaftFsync": 3, "FlexibleRaft": 5, "PullRaftVariant2": 3}
 
 
 def test_report_is_tlc_format():

@@ -9,7 +9,8 @@ import os
 import sys
 
 SPECS = {"Raft": "standard-raft/Raft.tla", "FlexibleRaft": "flexible-raft/FlexibleRaft.tla",
-         "PullRaft": "pull-raft/PullRaft.tla", "RaftFsync": "raft-and-fsync/RaftFsync.tla"}
+         "PullRaft": "pull-raft/PullRaft.tla", "RaftFsync": "raft-and-fsync/RaftFsync.tla",
+         "PullRaftVariant2": "pull-raft/PullRaftVariant2.tla"}
 
 
 def normalise(t):
