@@ -119,7 +119,9 @@ int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result
  * or a violation / evaluation error is found (its behaviour is then available
  * through rmc_trace_*).  Results: generated = states generated, distinct =
  * behaviours generated, depth = longest behaviour in states, status as for
- * rmc_check.  The same seed gives the same run. */
+ * rmc_check.  The same seed gives the same run (a time limit aside): every
+ * behaviour of a round runs to its end and a failure reports the round's
+ * lowest-index failing behaviour. */
 int rmc_simulate(rmc_model* m, const rmc_options* o, uint64_t walkers, uint32_t depth, uint64_t seed,
                  uint64_t behaviors, double seconds, rmc_result* out);
 /* The CPU engine: TLC's -workers N on host threads (o->cpu_workers; 0 = every hardware thread), over the

@@ -19,8 +19,13 @@ struct DevStatus {
 
 // simulation mode: the first behaviour to stop the run (violation / error)
 struct SimStatus {
-  unsigned stop;  // 0 running, 1 invariant violated, 2 evaluation error in Next, 3 evaluation error in an invariant
-  unsigned steps;  // steps of the stopping behaviour (its last binding is the failing one)
+  // the failing behaviour with the lowest walker index (atomicMin, so the
+  // report does not depend on wave scheduling): walker << 20 | steps << 2 |
+  // kind (1 invariant violated, 2 evaluation error in Next, 3 in an
+  // invariant); ~0 = none.  Decoded by the host into the fields below.
+  unsigned long long key;
+  unsigned stop;   // kind, 0 = none
+  unsigned steps;  // steps of the failing behaviour (its last binding is the failing one)
   unsigned long long walker;
 };
 

@@ -880,8 +880,9 @@ __global__ __launch_bounds__(SIM_BLOCK) void k_simulate(const uint32_t* __restri
   for (int q = 0; q < words; q++) cur[q] = init[q];
   unsigned long long rng = seed ^ (w * 0xD1B54A32D192ED03ULL);
   unsigned steps = 0;
+  // every behaviour runs to its end (no early stop when another one fails):
+  // the round's counts and its reported failure are then a function of the seed
   for (; steps < depth; steps++) {
-    if (ss->stop) break;
     PState<SPEC, N> s{cur};
     const int B = cM.nfixed + s.nmsg();
     int cnt = 0;
@@ -897,7 +898,7 @@ __global__ __launch_bounds__(SIM_BLOCK) void k_simulate(const uint32_t* __restri
       if (eval_binding<SPEC, N>(s, cM, b, d) && r-- == 0) break;
     binds[w * depth + steps] = (uint16_t)b;
     if (d.err) {  // an evaluation error in Next (TLC stops with an error)
-      if (atomicCAS(&ss->stop, 0u, 2u) == 0u) { ss->walker = w; ss->steps = steps + 1; }
+      atomicMin(&ss->key, (w << 20) | ((unsigned long long)(steps + 1) << 2) | 2ULL);
       steps++;
       break;
     }
@@ -908,7 +909,7 @@ __global__ __launch_bounds__(SIM_BLOCK) void k_simulate(const uint32_t* __restri
     PState<SPEC, N> ns{cur};
     int bad = check_invariants<SPEC, N>(ns, cM, ierr);
     if (ierr || bad >= 0) {
-      if (atomicCAS(&ss->stop, 0u, ierr ? 3u : 1u) == 0u) { ss->walker = w; ss->steps = steps + 1; }
+      atomicMin(&ss->key, (w << 20) | ((unsigned long long)(steps + 1) << 2) | (ierr ? 3ULL : 1ULL));
       steps++;
       break;
     }

@@ -56,7 +56,12 @@ static int simulate_impl(rmc_model* m, const rmc_options* opt, unsigned long lon
   stb.ensure(sizeof(DevStatus));
   HIPCHK(hipMemcpyAsync(dinit.p, init.data(), W * 4, hipMemcpyHostToDevice, stream));
   HIPCHK(hipMemsetAsync(counters.p, 0, 16, stream));
-  HIPCHK(hipMemsetAsync(ssb.p, 0, sizeof(SimStatus), stream));
+  {
+    SimStatus s0;
+    memset(&s0, 0, sizeof s0);
+    s0.key = ~0ULL;
+    HIPCHK(hipMemcpyAsync(ssb.p, &s0, sizeof s0, hipMemcpyHostToDevice, stream));
+  }
   DevStatus hst;
   hst.err_key = hst.inv_err_key = hst.viol_key = ~0ULL;
   hst.cap_flags = 0;
@@ -66,6 +71,7 @@ static int simulate_impl(rmc_model* m, const rmc_options* opt, unsigned long lon
   unsigned long long round = 0;
   SimStatus ss;
   memset(&ss, 0, sizeof ss);
+  ss.key = ~0ULL;
   int status = 0;
   unsigned long long cnt[2] = {0, 0};
   while (done < behaviors) {
@@ -78,6 +84,11 @@ static int simulate_impl(rmc_model* m, const rmc_options* opt, unsigned long lon
     HIPCHK(hipMemcpyAsync(&hst, stb.p, sizeof hst, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipMemcpyAsync(cnt, counters.p, 16, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
+    if (ss.key != ~0ULL) {
+      ss.stop = (unsigned)(ss.key & 3u);
+      ss.steps = (unsigned)((ss.key >> 2) & 0x3FFFFu);
+      ss.walker = ss.key >> 20;
+    }
     done += n;
     round++;
     if (hst.cap_flags) {

@@ -56,3 +56,18 @@ def test_simulation_is_reproducible_per_seed():
     c = m.simulate(walkers=4096, depth=40, seed=12, behaviors=20000)
     assert (a["generated"], a["depth"]) == (b["generated"], b["depth"])
     assert a["generated"] != c["generated"]
+
+
+@pytest.mark.parametrize("name", sorted(UNSAFE))
+def test_simulation_violation_is_reproducible(name):
+    """The reported failure is the lowest-index failing behaviour of the round
+    and every behaviour runs to its end, so the counts and the trace at a
+    violation are a function of the seed (not of wave scheduling)."""
+    g = UNSAFE[name]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    runs = [m.simulate(walkers=1 << 14, depth=60, seed=5, behaviors=1 << 20) for _ in range(3)]
+    assert runs[0]["status"] == "violation"
+    for r in runs[1:]:
+        assert (r["generated"], r["behaviors"], r["depth"], r["violated"]) == \
+            (runs[0]["generated"], runs[0]["behaviors"], runs[0]["depth"], runs[0]["violated"])
+        assert r["trace"] == runs[0]["trace"]
