@@ -224,6 +224,15 @@ void build_actions(Model& M) {
     if (t[s].kind == K_MSG) M.msg_act_slot[t[s].id] = s;
     else
       for (int x = 0; x < size; x++) {
+        // bindings the constants disable for good are not evaluated at all
+        // (their ordinals stay reserved, so TLC's order is unchanged):
+        // AppendEntries / RequestVote(i, j) / SendPullEntriesRequest with i = j
+        // (Raft.tla:264, RaftFsync.tla:235, PullRaft.tla:397), Restart with
+        // MaxRestarts = 0 (Raft.tla:227), elections with MaxElections = 0
+        const int id = t[s].id, i = x % M.N, j = x / M.N;
+        if (t[s].kind == K_IJ && i == j && (id == A_APPENDENTRIES || id == A_RVIJ || id == A_SENDPULL)) continue;
+        if (id == A_RESTART && M.R == 0) continue;
+        if ((id == A_REQUESTVOTE || id == A_TIMEOUT) && M.E == 0) continue;
         if (nf >= MAXFIXED) throw std::runtime_error("too many fixed bindings");
         M.fb_act[nf] = (uint8_t)s;
         M.fb_x[nf] = (uint8_t)x;
