@@ -53,6 +53,13 @@ typedef struct {
   int grow_on_overflow; /* test: no fingerprint-set growth ahead of a chunk; a chunk that overflows the set
                            grows it and is redone (the safety net behind the pre-sizing) */
   double time_limit;    /* stop (status 4) at the first level boundary after this many seconds (0 = none) */
+  /* TLC's -checkpoint / -recover (its states/ directory, reference .gitignore:1): rmc_check snapshots the
+   * search -- fingerprint set, the next level's frontier, trace records, counts -- into checkpoint_dir at
+   * the first level boundary checkpoint_minutes after the last snapshot (0 = every level), and resumes
+   * from the snapshot in recover_dir (same model and constants; verified).  NULL = off. */
+  const char* checkpoint_dir;
+  double checkpoint_minutes;
+  const char* recover_dir;
 } rmc_options;
 
 typedef struct {

@@ -46,6 +46,7 @@ int main(int argc, char** argv) {
   std::string tla, cfg;
   bool json = false, simulate = false, cpu = false;
   int shards = 0;  // > 0: the fingerprint-sharded protocol with this many logical shards on one GPU
+  std::string metadir, recover;
   std::string dump_fmt, dump_file;
   unsigned long long sim_walkers = 1ULL << 20, sim_num = 0, sim_seed = 0;
   unsigned sim_depth = 100;
@@ -67,6 +68,9 @@ int main(int argc, char** argv) {
     else if (k == "-simulate") simulate = true;
     else if (k == "-cpu") cpu = true;
     else if (k == "-shards") shards = atoi(val().c_str());
+    else if (k == "-checkpoint") o.checkpoint_minutes = atof(val().c_str());  // TLC: minutes between checkpoints
+    else if (k == "-metadir") metadir = val();                                 // TLC: where states/ go
+    else if (k == "-recover") recover = val();
     else if (k == "-fpwidth") o.fp_bits = atoi(val().c_str());  // 64 (TLC's) or 128
     else if (k == "-depth") sim_depth = (unsigned)atoi(val().c_str());
     else if (k == "-num") sim_num = strtoull(val().c_str(), nullptr, 10);
@@ -84,7 +88,7 @@ int main(int argc, char** argv) {
     else tla = k;
   }
   if (tla.empty()) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-checkpoint MIN] [-metadir DIR] [-recover DIR] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }
@@ -122,6 +126,13 @@ int main(int argc, char** argv) {
     rmc_model_free(m);
     return r.status == 0 ? 0 : (r.status == 1 ? 12 : 13);
   }
+  // TLC takes a checkpoint every 30 minutes into <metadir>/ by default; here
+  // snapshots are taken when -checkpoint or -metadir is given
+  if (!metadir.empty() || o.checkpoint_minutes > 0) {
+    if (metadir.empty()) metadir = "states";
+    o.checkpoint_dir = metadir.c_str();
+  }
+  if (!recover.empty()) o.recover_dir = recover.c_str();
   printf("raftmc %s: model checking %s\n", rmc_version(), tla.c_str());
   int rc = cpu ? rmc_check_cpu(m, &o, &r) : shards > 0 ? rmc_check_logical(m, &o, shards, &r) : rmc_check(m, &o, &r);
   if (rc != 0) {

@@ -15,6 +15,8 @@
 #include <unordered_map>
 #include <set>
 #include <sstream>
+#include <sys/stat.h>
+#include <cerrno>
 #include <string>
 #include <vector>
 #include "rmc_internal.h"
@@ -721,6 +723,89 @@ void replay_trace(rmc_model* m, const std::vector<int>& binds, int last_b, int s
   }
 }
 
+// ---- checkpoint / recover (TLC -checkpoint / -recover, its states/ directory)
+// A snapshot is taken at a level boundary: the fingerprint set (raw entries),
+// the next level's frontier (packed rows), the trace records of every state
+// so far, and the counts.  checkpoint.meta is written last (after the binary
+// files are complete), so a directory without it holds no snapshot.
+struct Ckpt {
+  unsigned long long sig = 0, slots = 0, generated = 0, distinct = 0, cur_base = 0, cur_n = 0, hidden = 0;
+  unsigned depth = 0;
+  uint32_t kmax = 0;
+  int fpw = 1;
+  double rate = 4.0;
+  std::vector<std::pair<unsigned long long, unsigned long long>> levels;
+};
+unsigned long long model_signature(const rmc_model* m) {
+  const Model& M = m->M;
+  char b[320];
+  snprintf(b, sizeof b, "%s|%d|%d|%d|%d|%d|%d|%d|%d|%d|%d|%d|%d|%d|%d", m->module.c_str(), M.spec, M.N, M.V, M.E,
+           M.R, M.EQ, M.RQ, M.lfae, M.lfiq, M.ffbr, M.words, M.kmax, M.fpw, M.nperm);
+  std::string s = b;
+  for (int q = 0; q < M.ninv; q++) s += "|inv" + std::to_string(M.inv[q]);
+  for (auto& n : m->server_names) s += "|s:" + n;
+  for (auto& n : m->value_names) s += "|v:" + n;
+  return fnv1a64(s);
+}
+static void ckpt_write(const std::string& path, const void* dev, size_t bytes, void* stage, size_t stage_bytes) {
+  const std::string tmp = path + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) throw std::runtime_error("checkpoint: cannot write " + tmp);
+  for (size_t o = 0; o < bytes; o += stage_bytes) {
+    const size_t n = std::min(stage_bytes, bytes - o);
+    HIPCHK(hipMemcpy(stage, (const char*)dev + o, n, hipMemcpyDeviceToHost));
+    if (fwrite(stage, 1, n, f) != n) { fclose(f); throw std::runtime_error("checkpoint: short write to " + tmp); }
+  }
+  if (fclose(f) != 0 || rename(tmp.c_str(), path.c_str()) != 0)
+    throw std::runtime_error("checkpoint: cannot finish " + path);
+}
+static void ckpt_read(const std::string& path, void* dev, size_t bytes, void* stage, size_t stage_bytes) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("recover: cannot read " + path);
+  fseek(f, 0, SEEK_END);
+  if ((size_t)ftell(f) != bytes) { fclose(f); throw std::runtime_error("recover: " + path + " has the wrong size"); }
+  fseek(f, 0, SEEK_SET);
+  for (size_t o = 0; o < bytes; o += stage_bytes) {
+    const size_t n = std::min(stage_bytes, bytes - o);
+    if (fread(stage, 1, n, f) != n) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
+    HIPCHK(hipMemcpy((char*)dev + o, stage, n, hipMemcpyHostToDevice));
+  }
+  fclose(f);
+}
+static void ckpt_write_meta(const std::string& dir, const rmc_model* m, const Ckpt& c) {
+  const std::string path = dir + "/checkpoint.meta", tmp = path + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) throw std::runtime_error("checkpoint: cannot write " + tmp);
+  fprintf(f, "raftmc-checkpoint 1\nmodule %s\nsignature %016llx\nkmax %u\nfpw %d\nslots %llu\ngenerated %llu\n"
+             "distinct %llu\ndepth %u\ncur_base %llu\ncur_n %llu\nhidden %llu\nrate %.17g\nlevels %zu\n",
+          m->module.c_str(), c.sig, c.kmax, c.fpw, c.slots, c.generated, c.distinct, c.depth, c.cur_base, c.cur_n,
+          c.hidden, c.rate, c.levels.size());
+  for (auto& l : c.levels) fprintf(f, "%llu %llu\n", l.first, l.second);
+  if (fclose(f) != 0 || rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("checkpoint: cannot finish " + path);
+}
+static Ckpt ckpt_read_meta(const std::string& dir, const rmc_model* m) {
+  const std::string path = dir + "/checkpoint.meta";
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) throw std::runtime_error("recover: no checkpoint in " + dir + " (" + path + " missing)");
+  Ckpt c;
+  char module[128] = {0};
+  int ver = 0;
+  size_t nl = 0;
+  int ok = fscanf(f, "raftmc-checkpoint %d module %127s signature %llx kmax %u fpw %d slots %llu generated %llu "
+                     "distinct %llu depth %u cur_base %llu cur_n %llu hidden %llu rate %lg levels %zu",
+                  &ver, module, &c.sig, &c.kmax, &c.fpw, &c.slots, &c.generated, &c.distinct, &c.depth, &c.cur_base,
+                  &c.cur_n, &c.hidden, &c.rate, &nl);
+  if (ok != 14 || ver != 1) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
+  for (size_t k = 0; k < nl; k++) {
+    unsigned long long g = 0, d = 0;
+    if (fscanf(f, "%llu %llu", &g, &d) != 2) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
+    c.levels.push_back({g, d});
+  }
+  fclose(f);
+  if (m->module != module) throw std::runtime_error(std::string("recover: the checkpoint is of module ") + module);
+  return c;
+}
+
 int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   auto t0 = std::chrono::steady_clock::now();
   Model& M = m->M;
@@ -729,8 +814,19 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     throw std::runtime_error("fp_bits must be 64 or 128");
   uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
+  const bool recovering = opt->recover_dir && *opt->recover_dir;
+  Ckpt rc;
+  if (recovering) {  // the snapshot's row layout
+    rc = ckpt_read_meta(opt->recover_dir, m);
+    kmax = rc.kmax;
+  }
   finalize_model(m, kmax);
   M.fpw = opt->fp_bits == 128 ? 2 : 1;
+  if (recovering) {
+    if (M.kmax != rc.kmax || M.fpw != rc.fpw || model_signature(m) != rc.sig)
+      throw std::runtime_error(std::string("recover: the checkpoint in ") + opt->recover_dir +
+                               " is of a different model, constants or fingerprint width");
+  }
   const int ew = 2 * M.fpw;  // fingerprint-set entry width in 64-bit words
   HIPCHK(upload_model(M));
   hipStream_t stream;
@@ -743,8 +839,10 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   // this model ended with -- TLC's preallocated FPSet, -fpmem, in spirit) and
   // doubles before a chunk whose new states could take it past 0.75 load.
   unsigned long long slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 24, m->hint_slots);
+  if (recovering) slots = rc.slots;
   if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
+  if (recovering) fcap = std::max(fcap, rc.cur_n);
   const int maxsucc = M.nfixed + M.kmax;
   // 4M parents per launch: 4% less k_expand time than 2M on the bench cfg (2M: 4% less than 1M)
   unsigned long long chunk = opt->chunk_parents ? opt->chunk_parents : (1ULL << 22);
@@ -780,6 +878,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   size_t stb = scan_temp_bytes(chunk);
   scantmp.ensure(stb ? stb : 16);
   unsigned long long trcap = std::max(fcap * 4, m->hint_trcap);
+  if (recovering) trcap = std::max(trcap, rc.distinct + rc.distinct / 4);
   trp.ensure(trcap * 8);
   trb.ensure(trcap * 2);
 
@@ -841,8 +940,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
 
   // ---- level 1: Init (Raft.tla:213-218)
   std::vector<uint32_t> init = init_state(M);
-  HIPCHK(hipMemcpyAsync(fa.p, init.data(), W * 4, hipMemcpyHostToDevice, stream));
-  {
+  if (!recovering) HIPCHK(hipMemcpyAsync(fa.p, init.data(), W * 4, hipMemcpyHostToDevice, stream));
+  if (!recovering) {
     unsigned long long ent[4];
     if (M.fpw == 2) {
       host_fingerprint2(M, init.data(), ent);  // (a, b)
@@ -872,7 +971,35 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   unsigned long long bad_state = ~0ULL;  // global index of the violating / erroring state, if materialized
   unsigned long long bad_key = ~0ULL;
   bool bad_is_parent_key = false;
-  {
+  // pinned staging for checkpoint files (allocated on first use)
+  void* ck_stage = nullptr;
+  const size_t ck_stage_bytes = 64ULL << 20;
+  struct StageGuard {
+    void*& p;
+    ~StageGuard() { if (p) (void)hipHostFree(p); }
+  } ck_guard{ck_stage};
+  auto stage = [&]() {
+    if (!ck_stage) HIPCHK(hipHostMalloc(&ck_stage, ck_stage_bytes, hipHostMallocDefault));
+    return ck_stage;
+  };
+  if (recovering) {  // resume from the snapshot instead of Init
+    const std::string dir = opt->recover_dir;
+    ckpt_read(dir + "/fpset.bin", table.p, slots * ew * 8, stage(), ck_stage_bytes);
+    ckpt_read(dir + "/frontier.bin", fa.p, rc.cur_n * W * 4, stage(), ck_stage_bytes);
+    ckpt_read(dir + "/trace_parent.bin", trp.p, rc.distinct * 8, stage(), ck_stage_bytes);
+    ckpt_read(dir + "/trace_bind.bin", trb.p, rc.distinct * 2, stage(), ck_stage_bytes);
+    generated = rc.generated;
+    distinct = rc.distinct;
+    cur_n = rc.cur_n;
+    cur_base = rc.cur_base;
+    depth = rc.depth;
+    m->levels = rc.levels;
+    hst.hidden_coll = rc.hidden;
+    HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, hidden_coll), &hst.hidden_coll, 8,
+                          hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  if (!recovering) {
     int err = 0;
     int bad = host_check_invariants(M, init.data(), &err);
     if (err) { status = 2; message = "evaluation error in an invariant on the initial state"; bad_state = 0; }
@@ -883,14 +1010,15 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   unsigned long long expand_launches = 0, redos = 0;
   // hidden-variable collisions counted up to the last chunk that was kept: a
   // redone chunk's first k_mark has counted its collisions once already
-  unsigned long long coll_kept = 0;
+  unsigned long long coll_kept = recovering ? rc.hidden : 0;
   auto restore_coll = [&]() {
     HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, hidden_coll), &coll_kept, 8, hipMemcpyHostToDevice,
                           stream));
   };
   uint32_t* cur = fa.as<uint32_t>();
   uint32_t* nxt = fb.as<uint32_t>();
-  double rate = 4.0;  // new states per parent of the previous level (pre-sizes the table per chunk)
+  double rate = recovering ? rc.rate : 4.0;  // new states per parent of the previous level (pre-sizes the table per chunk)
+  auto last_ckpt = now();
   // the level that stopped the search (exact counts at the failing state, below)
   struct ChunkLog { unsigned long long c0, gen_before, new_before; };
   std::vector<ChunkLog> chunk_log;
@@ -1123,6 +1251,36 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
               depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s, table.bytes / 1073741824.0,
               A.table2.bytes / 1073741824.0, fa.bytes / 1073741824.0, fb.bytes / 1073741824.0, trp.bytes / 1073741824.0, trb.bytes / 1073741824.0,
               fr / 1073741824.0);
+    }
+    // ---- snapshot at this level boundary (TLC -checkpoint)
+    if (opt->checkpoint_dir && *opt->checkpoint_dir && cur_n > 0 &&
+        (opt->checkpoint_minutes <= 0 || secs(last_ckpt, now()) >= 60.0 * opt->checkpoint_minutes)) {
+      auto tc0 = now();
+      HIPCHK(hipStreamSynchronize(stream));
+      const std::string dir = opt->checkpoint_dir;
+      if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) throw std::runtime_error("checkpoint: cannot create " + dir);
+      (void)remove((dir + "/checkpoint.meta").c_str());  // the old snapshot is void from here on
+      ckpt_write(dir + "/fpset.bin", table.p, slots * ew * 8, stage(), ck_stage_bytes);
+      ckpt_write(dir + "/frontier.bin", cur, cur_n * W * 4, stage(), ck_stage_bytes);
+      ckpt_write(dir + "/trace_parent.bin", trp.p, distinct * 8, stage(), ck_stage_bytes);
+      ckpt_write(dir + "/trace_bind.bin", trb.p, distinct * 2, stage(), ck_stage_bytes);
+      Ckpt c;
+      c.sig = model_signature(m);
+      c.slots = slots;
+      c.generated = generated;
+      c.distinct = distinct;
+      c.cur_base = cur_base;
+      c.cur_n = cur_n;
+      c.hidden = coll_kept;
+      c.depth = depth;
+      c.kmax = (uint32_t)M.kmax;
+      c.fpw = M.fpw;
+      c.rate = rate;
+      c.levels = m->levels;
+      ckpt_write_meta(dir, m, c);
+      last_ckpt = now();
+      if (opt->verbose)
+        fprintf(stderr, "[rmc] checkpoint at depth %u in %s (%.3fs)\n", depth, dir.c_str(), secs(tc0, now()));
     }
   }
   } catch (OutOfDeviceMemory& oom) {

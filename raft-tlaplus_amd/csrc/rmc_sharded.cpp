@@ -211,6 +211,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   Model& M = m->M;
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
   if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("fp_bits 128 is offered by the single-GPU search (rmc_check) only");
+  if ((opt->checkpoint_dir && *opt->checkpoint_dir) || (opt->recover_dir && *opt->recover_dir))
+    throw std::runtime_error("checkpoint / recover are offered by the single-GPU search (rmc_check) only");
   uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);

@@ -30,7 +30,8 @@ class Options(ctypes.Structure):
                 ("msg_cap_K", ctypes.c_uint32), ("frontier_cap", ctypes.c_uint64),
                 ("chunk_parents", ctypes.c_uint32), ("verbose", ctypes.c_int),
                 ("max_depth", ctypes.c_int), ("grow_on_overflow", ctypes.c_int),
-                ("time_limit", ctypes.c_double)]
+                ("time_limit", ctypes.c_double), ("checkpoint_dir", ctypes.c_char_p),
+                ("checkpoint_minutes", ctypes.c_double), ("recover_dir", ctypes.c_char_p)]
 
 
 class Result(ctypes.Structure):
@@ -117,10 +118,18 @@ class Model:
 
     def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
                  chunk_parents=0, verbose=False, max_depth=0, workers=0, grow_on_overflow=False,
-                 time_limit=0.0, fp_bits=64):
+                 time_limit=0.0, fp_bits=64, checkpoint_dir=None, checkpoint_minutes=0.0, recover_dir=None):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
+        # the path bytes stay referenced by the Options object for the call
+        if checkpoint_dir is not None:
+            o._ckpt = str(checkpoint_dir).encode()
+            o.checkpoint_dir = o._ckpt
+            o.checkpoint_minutes = float(checkpoint_minutes)
+        if recover_dir is not None:
+            o._recover = str(recover_dir).encode()
+            o.recover_dir = o._recover
         o.deadlock_check = 1 if deadlock else 0
         o.hash_slots, o.msg_cap_K, o.frontier_cap = hash_slots, msg_cap_K, frontier_cap
         o.chunk_parents, o.verbose, o.max_depth, o.cpu_workers = chunk_parents, int(verbose), max_depth, workers

@@ -70,3 +70,11 @@ def test_cpu_engine_medium_violation():
     assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
         (g["generated"], g["distinct"], g["depth"], g["levels"])
     assert len(r["trace"]) == g["trace_len"]
+
+
+def test_cpu_engine_refuses_checkpoint(tmp_path):
+    """Snapshots are the GPU search's (rmc_check); the CPU engine says so instead of ignoring them."""
+    g = SMALL["raft_n3v1e1"]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    with pytest.raises(raftmc.RaftmcError, match="checkpoint"):
+        m.check_cpu(checkpoint_dir=tmp_path)

@@ -1,0 +1,77 @@
+"""GPU: TLC's -checkpoint / -recover (the reference's
+states/ directory, .gitignore:1).  A check stopped after some levels with a
+snapshot at every level boundary, then resumed from the snapshot, must give
+exactly the counts, per-level pairs, hidden-variable collisions and (at a
+violation) the counts and trace of an uninterrupted check."""
+import json
+import os
+
+import pytest
+
+import raftmc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SHIPPED = json.load(open(os.path.join(HERE, "golden", "shipped.json")))
+ORDER = json.load(open(os.path.join(HERE, "golden", "order.json")))
+V2 = json.load(open(os.path.join(HERE, "golden", "variant2.json")))
+UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
+
+pytestmark = pytest.mark.gpu
+
+
+def model(g):
+    if "cfg_path" in g:
+        return raftmc.Model(os.path.join(ROOT, "configs", g["module"] + ".tla"), os.path.join(ROOT, g["cfg_path"]))
+    return raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+
+
+CASES = [("shipped", "Raft_cfg"), ("order", "fsync_n2v2e2r1_hidden"), ("v2", "pull2_n3v1e2r1")]
+TABLES = {"shipped": SHIPPED, "order": ORDER, "v2": V2}
+
+
+@pytest.mark.parametrize("table,name", CASES)
+@pytest.mark.parametrize("fp_bits", [64, 128])
+def test_stop_snapshot_resume(tmp_path, table, name, fp_bits):
+    g = TABLES[table][name]
+    stop_at = max(2, g["depth"] // 2)
+    a = model(g).check(max_depth=stop_at, checkpoint_dir=tmp_path, checkpoint_minutes=0, fp_bits=fp_bits)
+    assert a["status"] == "stopped" and a["depth"] == stop_at
+    assert (tmp_path / "checkpoint.meta").exists()
+    r = model(g).check(recover_dir=tmp_path, fp_bits=fp_bits)
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+def test_resume_then_snapshot_again(tmp_path):
+    """A resumed check takes snapshots too: three legs reach the uninterrupted result."""
+    g = SHIPPED["Raft_cfg"]
+    d1, d2 = tmp_path / "a", tmp_path / "b"
+    model(g).check(max_depth=10, checkpoint_dir=d1, checkpoint_minutes=0)
+    model(g).check(max_depth=20, recover_dir=d1, checkpoint_dir=d2, checkpoint_minutes=0)
+    r = model(g).check(recover_dir=d2)
+    assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
+        (g["generated"], g["distinct"], g["depth"], g["levels"])
+
+
+@pytest.mark.parametrize("name", sorted(UNSAFE))
+def test_resume_finds_the_violation(tmp_path, name):
+    """Resumed before the violating level: the same violation, counts at it and trace."""
+    g = UNSAFE[name]
+    full = model(g).check()
+    model(g).check(max_depth=max(2, g["depth"] - 3), checkpoint_dir=tmp_path, checkpoint_minutes=0)
+    r = model(g).check(recover_dir=tmp_path)
+    assert r["status"] == "violation" and r["violated"] == g["violated"]
+    assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
+    assert r["trace"] == full["trace"]
+
+
+def test_recover_refuses_another_model(tmp_path):
+    g = SHIPPED["Raft_cfg"]
+    model(g).check(max_depth=5, checkpoint_dir=tmp_path, checkpoint_minutes=0)
+    other = ORDER["raft_n2v2e2r2_order"]
+    with pytest.raises(raftmc.RaftmcError, match="different model"):
+        model(other).check(recover_dir=tmp_path)
+    with pytest.raises(raftmc.RaftmcError, match="no checkpoint"):
+        model(g).check(recover_dir=tmp_path / "missing")
