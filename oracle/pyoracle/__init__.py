@@ -16,9 +16,10 @@ from .tlc import bfs, EvalError
 def make_spec(module, cfg):
     from .raft import RaftSpec
     from .variants import FlexibleRaftSpec, RaftFsyncSpec, PullRaftSpec, PullRaftVariant2Spec
+    from .kraft import KRaftSpec
     table = {"Raft": RaftSpec, "FlexibleRaft": FlexibleRaftSpec,
              "RaftFsync": RaftFsyncSpec, "PullRaft": PullRaftSpec,
-             "PullRaftVariant2": PullRaftVariant2Spec}
+             "PullRaftVariant2": PullRaftVariant2Spec, "KRaft": KRaftSpec}
     if module not in table:
         raise ValueError("oracle: unsupported module %r" % module)
     return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]))

@@ -82,12 +82,13 @@ def _field_key(x):
     """A record field's key.  A field that holds either the model value Nil or a
     record (PullRaftVariant2.tla:369-375, mlastCommonEntry) compares Nil below
     every record: TLC's untyped model value is less than any non-model value and
-    a record greater than a model value.  Record-valued fields of the other
+    a record greater than a model value.  A field holding Nil or a server
+    (KRaft.tla:500, mleader) compares by model-value name: Nil below n1, n2, ...  Record-valued fields of the other
     specs keep their relative order (both sides wrapped the same way)."""
     if isinstance(x, Rec):
         return (1, tlc_key(x))
-    if type(x) is int and x == NIL:
-        return (0,)
+    if type(x) is int:  # Nil (the model value) below the servers in a server-or-Nil field (KRaft mleader)
+        return (0,) if x == NIL else (1, x)
     return tlc_key(x)
 
 

@@ -219,6 +219,7 @@ void build_actions(Model& M) {
   int off = 0, nf = 0;
   for (int a = 0; a < A_NUM; a++) M.msg_act_slot[a] = 0;
   for (int s = 0; s < M.nact; s++) {
+    M.act_fb_first[s] = (uint8_t)nf;
     M.act_id[s] = t[s].id;
     M.act_kind[s] = t[s].kind;
     M.act_off[s] = off;
@@ -238,8 +239,10 @@ void build_actions(Model& M) {
         if (nf >= MAXFIXED) throw std::runtime_error("too many fixed bindings");
         M.fb_act[nf] = (uint8_t)s;
         M.fb_x[nf] = (uint8_t)x;
+        M.fb_desc[nf] = (uint32_t)s | (uint32_t)x << 8 | (uint32_t)id << 16 | (uint32_t)i << 24 | (uint32_t)j << 28;
         nf++;
       }
+    M.act_fb_end[s] = (uint8_t)nf;
     off += size;
   }
   M.nfixed = nf;
@@ -1375,18 +1378,25 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   }
   res->hidden_var_collisions = fin.hidden_coll;
   if (opt->verbose) {
-    unsigned long long stp[16];
+    unsigned long long stp[32];
     read_stamps(stp);
-    double tot = (double)(stp[0] + stp[2] + stp[3]);
+    double tot = (double)(stp[0] + stp[15] + stp[16] + stp[17] + stp[1] + stp[2] + stp[3]);
     if (tot > 0)
-      fprintf(stderr, "[rmc] k_expand phase shares: stage %.1f%%, bindings %.1f%%, fp+insert %.1f%% "
-              "(the same without inserts: %.1f%%); "
+      fprintf(stderr, "[rmc] k_expand phase B fixed split: guard masks %.1f%%, prefix + chunk table %.1f%%, chunks %.1f%%\n",
+              100 * stp[16] / tot, 100 * stp[17] / tot, 100 * stp[1] / tot);
+    if (tot > 0)
+      fprintf(stderr, "[rmc] k_expand phase shares: stage %.1f%%, message sums %.1f%%, bindings %.1f%% (fixed %.1f%%, "
+              "messages %.1f%%), fp+insert %.1f%% (the same without inserts: %.1f%%); "
               "fingerprints %llu, with signature ties %llu, permutations hashed under ties %llu\n",
-              100 * stp[0] / tot, 100 * stp[2] / tot, 100 * stp[3] / tot, 100 * stp[7] / tot, stp[4], stp[5], stp[6]);
+              100 * stp[0] / tot, 100 * stp[15] / tot, 100 * (stp[1] + stp[2]) / tot, 100 * stp[1] / tot,
+              100 * stp[2] / tot, 100 * stp[3] / tot, 100 * stp[7] / tot, stp[4], stp[5], stp[6]);
     if (stp[8])
       fprintf(stderr, "[rmc] phase B: %llu parents, %.2f message bindings and %.2f live ones per parent (%d fixed); "
               "wave steps %llu, with live messages only %llu\n", stp[8], (double)stp[9] / stp[8],
               (double)stp[10] / stp[8], M.nfixed, stp[11], stp[12]);
+    if (stp[8])
+      fprintf(stderr, "[rmc] phase B fixed bindings: %.2f (parent, binding) pairs per parent pass may_enable; "
+              "%.2f wave chunks per 64 parents\n", (double)stp[13] / stp[8], 64.0 * stp[14] / stp[8]);
     fprintf(stderr, "[rmc] fingerprint set: 2^%d slots, load %.3f, %llu growths, %llu chunk redos\n",
             __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);
   }
@@ -1733,8 +1743,9 @@ int rmc_selftest_host_bfs(rmc_model* m, uint32_t kmax, uint64_t max_distinct, ui
           int ord = 0, act = 0, err = 0;
           if (host_eval_apply(M, S, b, t.data(), &ord, &act, &err) != 1) continue;
           if (err) { out3[0] = gen; out3[1] = distinct; out3[2] = depth; return -10 - err; }
-          if (host_fp_check(M, S, b, t.data())) {
-            g_last_error = "selftest: incremental fingerprint differs from the materialized state's";
+          if (const int fc = host_fp_check(M, S, b, t.data())) {
+            g_last_error = fc == 2 ? "selftest: may_enable rejects an enabled fixed binding"
+                                   : "selftest: incremental fingerprint differs from the materialized state's";
             return -2;
           }
           succ.push_back({ord, t});

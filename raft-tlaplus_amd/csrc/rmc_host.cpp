@@ -37,12 +37,17 @@ static int fp2_t(const Model& M, const uint32_t* S, unsigned long long* ab) {
 
 // Test hook: the three ways the fingerprint of a successor is computed agree
 // (delta_fp from parent + delta, delta_fp_sums from the parent's message sums
-// as k_expand does, state_fp of the materialized row).  0 = agree.
+// as k_expand does, state_fp of the materialized row).  0 = agree; 2 = the
+// guard prefilter may_enable rejects an enabled binding.
 template <int SPEC, int N>
 static int fp_check_t(const Model& M, const uint32_t* parent, int b, const uint32_t* row) {
   PState<SPEC, N> s{parent};
   Delta d;
-  if (!eval_binding<SPEC, N>(s, M, b, d) || d.err) return 0;
+  if (!eval_binding<SPEC, N>(s, M, b, d)) return 0;
+  // k_expand evaluates a fixed binding only if may_enable passes: it must hold
+  // for every enabled binding (and every one that raises an error)
+  if (b < M.nfixed && !may_enable<SPEC, N>(s, M, b)) return 2;
+  if (d.err) return 0;
   MsgSums<N> ms{};
   for (int k = 0; k < s.nmsg(); k++) {
     int src, dst;

@@ -49,7 +49,7 @@ __device__ __forceinline__ unsigned long long order_key(unsigned long long pg, i
 // summed over blocks (thread 0's shader-clock deltas, with an extra barrier
 // between phases A and B).  Read the shares, not the absolute time.
 #ifdef RMC_STAMPS
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[32];
 #define STAMP(i)                                                   \
   do {                                                             \
     __syncthreads();                                               \
@@ -66,9 +66,9 @@ __device__ unsigned long long g_stamps[16];
 #endif
 void read_stamps(unsigned long long* out) {
 #ifdef RMC_STAMPS
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 16 * sizeof(unsigned long long));
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 32 * sizeof(unsigned long long));
 #else
-  for (int i = 0; i < 16; i++) out[i] = 0;
+  for (int i = 0; i < 32; i++) out[i] = 0;
 #endif
 }
 
@@ -81,20 +81,32 @@ struct Tile {
 // Dynamic LDS layout of k_expand (bytes; the launch computes the same).
 constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
 struct ExpandLds {
-  int Wp, off_Ms, off_Ord, off_Base, off_Live, bytes;
+  int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, bytes;
 };
-__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes) {
+__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes, int nfixed, int nord) {
   ExpandLds L;
   L.Wp = words | 1;  // odd row stride: lane-per-parent LDS reads are bank-conflict free
   int o = (PB * L.Wp * 4 + 7) & ~7;
   L.off_Ms = o;  // per-parent message sums (MsgSums<N>, 8 B aligned)
   o += PB * msbytes;
+  L.off_Mask = o;  // per fixed binding: the tile's parents that pass may_enable (64-bit masks)
+  o += nfixed * 8;
+  L.off_BOff = o;  // exclusive prefix over fixed bindings of the passing pairs
+  o += (nfixed + 1) * 4;
   L.off_Ord = o;  // per parent: bitmask over TLC ordinals of its enabled bindings
   o += PB * ordw * 4;
   L.off_Base = o;  // exclusive prefix over the tile's parents of their successor counts
   o += (PB + 1) * 4;
   L.off_Live = o;  // per parent: bitmask over DOMAIN messages that can enable an action (msg_live)
   o += PB * LIVE_WORDS * 4;
+  // the model's binding tables, staged once per block: a lane's own binding
+  // then costs LDS reads instead of dependent vector loads of __constant__ data
+  L.off_Desc = o;  // fixed binding -> descriptor (Model::fb_desc)
+  o += nfixed * 4;
+  L.off_O2b = o;  // TLC ordinal -> binding (Model::ord2b)
+  o += ((nord + 1) & ~1) * 2;
+  L.off_MOff = o;  // message action id -> its first ordinal
+  o += ((A_NUM + 1) & ~1) * 2;
   L.bytes = o;
   return L;
 }
@@ -109,6 +121,15 @@ __device__ __forceinline__ int select_bit(const uint32_t* w, int j) {  // j-th s
     }
     j -= c;
   }
+}
+__device__ __forceinline__ int select_bit64(unsigned long long x, int r) {  // r-th set bit of x (0-based), in registers
+  int pos = 0, c;
+  c = __popc((uint32_t)x); if (r >= c) { r -= c; x >>= 32; pos += 32; }
+  c = __popc((uint32_t)x & 0xFFFFu); if (r >= c) { r -= c; x >>= 16; pos += 16; }
+  c = __popc((uint32_t)x & 0xFFu); if (r >= c) { r -= c; x >>= 8; pos += 8; }
+  c = __popc((uint32_t)x & 0xFu); if (r >= c) { r -= c; x >>= 4; pos += 4; }
+  c = __popc((uint32_t)x & 0x3u); if (r >= c) { r -= c; x >>= 2; pos += 2; }
+  return pos + (r >= (int)(x & 1u) ? 1 : 0);
 }
 __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set bits below `bit`
   int r = 0;
@@ -162,15 +183,21 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   constexpr int PB = Tile<N>::PB;
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG, sSeg;
+  __shared__ int sAFirst[MAXACT], sAEnd[MAXACT], sAChunk[MAXACT + 1];
   const int tid = threadIdx.x;
   using MS = typename SumsOf<N, FPW>::T;
   const int words = cM.words, ordw = cM.ord_words;
-  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS));
+  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS), cM.nfixed, cM.ordinal_limit);
   uint32_t* sS = (uint32_t*)lds;
   MS* sMS = (MS*)(lds + L.off_Ms);
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
   uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
   uint32_t* sLive = (uint32_t*)(lds + L.off_Live);
+  unsigned long long* sMask = (unsigned long long*)(lds + L.off_Mask);
+  uint32_t* sBOff = (uint32_t*)(lds + L.off_BOff);
+  uint32_t* sDesc = (uint32_t*)(lds + L.off_Desc);
+  uint16_t* sO2b = (uint16_t*)(lds + L.off_O2b);
+  uint16_t* sMOff = (uint16_t*)(lds + L.off_MOff);
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
 #ifdef RMC_STAMPS
@@ -185,6 +212,9 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
   for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
   for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
+  for (int q = tid; q < cM.nfixed; q += 256) sDesc[q] = cM.fb_desc[q];
+  for (int q = tid; q < cM.ordinal_limit; q += 256) sO2b[q] = cM.ord2b[q];
+  for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
   __syncthreads();
   STAMP(0);
   // ---- B: enabled bindings, lane per parent
@@ -213,20 +243,107 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
         }
       }
     }
+    STAMP(15);  // message sums done (diagnostic build: phase B split)
+    // eval_one: one (parent pp, binding b) pair; enabled -> the ordinal bit,
+    // errors and message-capacity overflow flagged
+    auto record = [&](int pp, int b, const Delta& d) {
+      if (d.err) {
+        if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pbase + p0 + pp, d.ordinal, b));
+        else atomicOr(&st->cap_flags, 1u << d.err);
+      } else {
+        int adds = 0;
+#pragma unroll
+        for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
+        if (h_nmsg(sS[pp * L.Wp]) + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
+      }
+      atomicOr(&sOrd[pp * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
+    };
+    // Fixed bindings.  (1) guard masks: wave w0 takes bindings w0, w0+4, ...,
+    // its lanes the tile's parents; bit p of sMask[b] = may_enable(parent p,
+    // b), the guard's leading conjuncts.  (2) The pairs that pass, grouped by
+    // action and padded to whole waves: every wave step runs ONE action's code
+    // (a scalar branch) on 64 (parent, binding) pairs, instead of one binding
+    // for 64 parents of which most fail its guard.
+    const int w0 = tid / PB;
+    for (int b = w0; b < cM.nfixed; b += bstride) {
+      bool g = false;
+      if (p < np) {
+        PState<SPEC, N> s{sS + p * L.Wp};
+        g = may_enable<SPEC, N>(s, cM, b);
+      }
+      const unsigned long long m = __ballot(g);
+      if (p == 0) sMask[b] = m;
+    }
     __syncthreads();
+    STAMP(16);  // guard masks done
+    if (tid < WAVE) {  // sBOff = exclusive prefix over bindings of the pairs that pass
+      unsigned carry = 0;
+      for (int b0 = 0; b0 < cM.nfixed; b0 += WAVE) {
+        const int b = b0 + tid;
+        const unsigned c = b < cM.nfixed ? (unsigned)__popcll(sMask[b]) : 0u;
+        unsigned incl = c;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+          unsigned y = __shfl_up(incl, o, WAVE);
+          if (tid >= o) incl += y;
+        }
+        if (b < cM.nfixed) sBOff[b] = carry + incl - c;
+        carry += __shfl(incl, WAVE - 1, WAVE);
+      }
+      if (tid == 0) sBOff[cM.nfixed] = carry;
+    }
+    __syncthreads();
+    if (tid < WAVE) {  // per action slot (lane): its first wave-sized chunk of passing pairs
+      const int a = tid;
+      int c = 0;
+      if (a < cM.nact) {
+        const int f = cM.act_fb_first[a], e = cM.act_fb_end[a];
+        sAFirst[a] = f;
+        sAEnd[a] = e;
+        c = ((int)(sBOff[e] - sBOff[f]) + WAVE - 1) / WAVE;
+      }
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < WAVE; o <<= 1) {
+        int y = __shfl_up(incl, o, WAVE);
+        if (tid >= o) incl += y;
+      }
+      if (a <= cM.nact) sAChunk[a] = incl - c;
+    }
+    __syncthreads();
+    STAMP(17);  // pair prefix + action chunk table done
+    {
+      const int nchunks = sAChunk[cM.nact];
+      for (int c = w0; c < nchunks; c += bstride) {
+        int a = 0;
+        while (sAChunk[a + 1] <= c) a++;
+        a = __builtin_amdgcn_readfirstlane(a);  // wave-uniform: the action dispatch is a scalar branch
+        const int g = (int)sBOff[sAFirst[a]] + (c - sAChunk[a]) * WAVE + p;
+        if (g < (int)sBOff[sAEnd[a]]) {
+          int lo = sAFirst[a], hi = sAEnd[a] - 1;  // binding: sBOff[lo] <= g < sBOff[lo + 1]
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)sBOff[mid] <= g) lo = mid; else hi = mid - 1;
+          }
+          const int pp = select_bit64(sMask[lo], g - (int)sBOff[lo]);
+          PState<SPEC, N> s{sS + pp * L.Wp};
+          Delta d;
+          if (eval_fixed<SPEC, N>(s, cM, a, cM.fb_x[lo], d)) record(pp, lo, d);
+        }
+      }
+    }
+    STAMP(1);  // fixed bindings done (diagnostic build: phase B split)
     if (p < np) {
       PState<SPEC, N> s{sS + p * L.Wp};
       const int nm = s.nmsg();
-      const int B = cM.nfixed + nm;
-      const unsigned long long pg = pbase + p0 + p;
 #ifdef RMC_STAMPS
       {  // binding statistics: message bindings, live ones (act_message's fast reject passes), wave steps
+        const int B = cM.nfixed + nm;
         int live = 0;
         for (int k = 0; k < nm; k++) {
           const uint32_t w = s.msg(k);
           live += !(msg_count(w) == 0 && msg_term<SPEC>(w) <= a_term(s.A(msg_dst<SPEC>(w))));
         }
-        const int w0 = tid / PB;
         int steps = (B - w0 + bstride - 1) / bstride, lsteps = (cM.nfixed + live - w0 + bstride - 1) / bstride;
         for (int o = 32; o > 0; o >>= 1) {
           steps = max(steps, __shfl_xor(steps, o, WAVE));
@@ -241,36 +358,27 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           atomicAdd(&g_stamps[11], (unsigned long long)steps);
           atomicAdd(&g_stamps[12], (unsigned long long)lsteps);
         }
+        if (tid == 0) atomicAdd(&g_stamps[13], (unsigned long long)sBOff[cM.nfixed]);  // fixed pairs passing the guard
+        if (tid == 0) atomicAdd(&g_stamps[14], (unsigned long long)sAChunk[cM.nact]);  // their wave chunks
       }
 #endif
-      // fixed bindings (wave-uniform: every lane on the same binding), then
       // the parent's live messages, every 4th one per wave
-      auto eval_one = [&](int b) {
-        Delta d;
-        if (!eval_binding<SPEC, N>(s, cM, b, d)) return;
-        if (d.err) {
-          if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pg, d.ordinal, b));
-          else atomicOr(&st->cap_flags, 1u << d.err);
-        } else {
-          int adds = 0;
-#pragma unroll
-          for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
-          if (nm + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
-        }
-        atomicOr(&sOrd[p * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
-      };
-      const int w0 = tid / PB;
-      for (int b = w0; b < cM.nfixed; b += bstride) eval_one(b);
       int t = 0;
       for (int q = 0; q < LIVE_WORDS; q++) {
         uint32_t x = sLive[p * LIVE_WORDS + q];
         while (x) {
           const int k = 32 * q + __ffs(x) - 1;
           x &= x - 1u;
-          if ((t++ & (bstride - 1)) == w0) eval_one(cM.nfixed + k);
+          if ((t++ & (bstride - 1)) == w0) {
+            Delta d;
+            d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0; d.act = -1;
+            if (act_message<SPEC, N>(s, cM, k, d)) {
+              d.ordinal = sMOff[d.act] + k;
+              record(p, cM.nfixed + k, d);
+            }
+          }
         }
       }
-      (void)B;
     }
   }
   __syncthreads();
@@ -325,10 +433,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
         if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
       }
       const int p = lo;
-      const int b = cM.ord2b[select_bit(sOrd + p * ordw, idx - (int)sBase[p])];
+      const int ord = select_bit(sOrd + p * ordw, idx - (int)sBase[p]);
+      const int b = sO2b[ord];
       PState<SPEC, N> s{sS + p * L.Wp};
       Delta d;
-      eval_binding<SPEC, N>(s, cM, b, d);
+      eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
       if constexpr (FPW == 2) {
         if (!d.err) acc ^= delta_fp_sums2<SPEC, N>(s, cM, d, sMS[p]).b;
       } else {
@@ -357,10 +466,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
     }
     const int p = lo;
-    const int b = cM.ord2b[select_bit(sOrd + p * ordw, idx - (int)sBase[p])];
+    const int ord = select_bit(sOrd + p * ordw, idx - (int)sBase[p]);
+    const int b = sO2b[ord];
     PState<SPEC, N> s{sS + p * L.Wp};
     Delta d;
-    eval_binding<SPEC, N>(s, cM, b, d);
+    eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
     const unsigned long long t = gbase + (unsigned long long)idx;
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = CAND_DUP;
@@ -476,6 +586,7 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   // winner list: (rank << 16 | candidate index in the tile) and the candidate's ordinal/binding word,
   // both read coalesced in the compaction pass instead of per winner later
   __shared__ uint32_t sOff[PB + 1], sPos[PB], sList[MAT_LIST], sListOb[MAT_LIST];
+  __shared__ uint32_t sDesc[MAXFIXED];  // Model::fb_desc (see k_expand)
   __shared__ int sCount;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int words = cM.words, Wp = words | 1;
@@ -489,6 +600,7 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
     int p = q / words;
     sS[p * Wp + (q - p * words)] = src[q];
   }
+  for (int q = tid; q < cM.nfixed; q += MAT_T) sDesc[q] = cM.fb_desc[q];
   if (tid < np) {
     sOff[tid] = par_off[p0 + tid] - start;
     sPos[tid] = par_pos[p0 + tid];
@@ -529,7 +641,7 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
       const int rank = (int)(sList[e] >> 16);
       PState<SPEC, N> s{sS + p * Wp};
       Delta d;
-      eval_binding<SPEC, N>(s, cM, b, d);
+      eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, (int)(ob >> 16), d);
       const unsigned long long dst = (unsigned long long)sPos[p] + rank;
       uint32_t* o = out + dst * (unsigned long long)words;
       int nn = 0;
@@ -768,7 +880,8 @@ struct Launch {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
-    ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T));
+    ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T), M.nfixed,
+                             M.ordinal_limit);
     hipLaunchKernelGGL((k_expand<SPEC, N, FPW>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.floor, a.sharded, a.shard_self, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val);

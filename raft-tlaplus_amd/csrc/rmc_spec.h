@@ -82,6 +82,9 @@ struct Model {
   int nact, act_id[MAXACT], act_kind[MAXACT], act_off[MAXACT];
   int nfixed;
   uint8_t fb_act[MAXFIXED], fb_x[MAXFIXED];  // fixed binding -> (action slot, binding index)
+  // fixed binding -> slot | x << 8 | act_id << 16 | i << 24 | j-or-v << 28 (one load instead of a chain)
+  uint32_t fb_desc[MAXFIXED];
+  uint8_t act_fb_first[MAXACT], act_fb_end[MAXACT];  // action slot -> its fixed bindings [first, end)
   int msg_act_slot[A_NUM];                   // action slot of each message action
   int ordinal_limit;
   int fpw;                    // fingerprint width in 64-bit words (1: 64-bit, 2: 128-bit)
@@ -912,35 +915,83 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
   return false;
 }
 
+// A fixed binding given as (action id, its bound server i, its second bound
+// variable jv) with its TLC ordinal already known: no table lookups, so a lane
+// with its own binding issues no dependent loads before the action's guard.
+template <int SPEC, int N>
+RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int i, int jv, int ordinal, Delta& d) {
+  d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
+  d.act = act;
+  d.ordinal = ordinal;
+  switch (act) {
+    case A_RESTART: return act_restart(s, M, i, d);
+    case A_REQUESTVOTE: return act_requestvote(s, M, i, d);
+    case A_TIMEOUT: return act_timeout(s, M, i, d);
+    case A_RVIJ: return act_rvij(s, M, i, jv, d);
+    case A_BECOMELEADER: return act_becomeleader(s, M, i, d);
+    case A_CLIENT: return act_client(s, M, i, jv, d);
+    case A_ADVCOMMIT: return act_advcommit(s, M, i, d);
+    case A_APPENDENTRIES: return act_appendentries(s, M, i, jv, d);
+    case A_ADVFSYNC: return act_advfsync(s, M, i, d);
+    case A_SENDPULL: return act_sendpull(s, M, i, jv, d);
+  }
+  return false;
+}
+// A fixed binding: action slot `slot` (a K_I / K_IV / K_IJ action of Next)
+// with bound-variable index x (first bound variable fastest).
+template <int SPEC, int N>
+RMC_HD bool eval_fixed(const PState<SPEC, N>& s, const Model& M, int slot, int x, Delta& d) {
+  return eval_fixed_id(s, M, M.act_id[slot], x % N, x / N, M.act_off[slot] + x, d);
+}
+// Binding b whose TLC ordinal is known (k_expand phase C, k_materialize):
+// desc = M.fb_desc[b] for a fixed binding (staged in LDS by the kernels).
+template <int SPEC, int N>
+RMC_HD bool eval_known(const PState<SPEC, N>& s, const Model& M, int b, uint32_t desc, int ordinal, Delta& d) {
+  if (b < M.nfixed)
+    return eval_fixed_id(s, M, (int)((desc >> 16) & 0xFFu), (int)((desc >> 24) & 15u), (int)(desc >> 28), ordinal, d);
+  d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
+  d.act = -1;
+  const bool en = act_message(s, M, b - M.nfixed, d);
+  d.ordinal = ordinal;
+  return en;
+}
+
 // Evaluate binding b (fixed bindings first, then one per DOMAIN element).
 template <int SPEC, int N>
 RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta& d) {
+  if (b < M.nfixed) return eval_fixed(s, M, M.fb_act[b], M.fb_x[b], d);
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
-  if (b < M.nfixed) {
-    int slot = M.fb_act[b], x = M.fb_x[b];
-    int act = M.act_id[slot];
-    d.act = act;
-    d.ordinal = M.act_off[slot] + x;
-    int i = x % N, jv = x / N;  // first bound variable fastest
-    switch (act) {
-      case A_RESTART: return act_restart(s, M, i, d);
-      case A_REQUESTVOTE: return act_requestvote(s, M, i, d);
-      case A_TIMEOUT: return act_timeout(s, M, i, d);
-      case A_RVIJ: return act_rvij(s, M, i, jv, d);
-      case A_BECOMELEADER: return act_becomeleader(s, M, i, d);
-      case A_CLIENT: return act_client(s, M, i, jv, d);
-      case A_ADVCOMMIT: return act_advcommit(s, M, i, d);
-      case A_APPENDENTRIES: return act_appendentries(s, M, i, jv, d);
-      case A_ADVFSYNC: return act_advfsync(s, M, i, d);
-      case A_SENDPULL: return act_sendpull(s, M, i, jv, d);
-    }
-    return false;
-  }
   int k = b - M.nfixed;
   d.act = -1;
   bool en = act_message(s, M, k, d);
   if (en) d.ordinal = M.act_off[M.msg_act_slot[d.act]] + k;
   return en;
+}
+
+// A necessary condition for fixed binding b to be enabled (or to raise an
+// evaluation error): the leading conjuncts of each action's guard, which read
+// one header field or one server's state word.  may_enable false implies
+// eval_binding returns false without an error, so k_expand evaluates only the
+// (parent, binding) pairs that pass it.
+template <int SPEC, int N>
+RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
+  const uint32_t desc = M.fb_desc[b];
+  const int i = (int)((desc >> 24) & 15u), jv = (int)(desc >> 28);
+  const uint32_t a = s.A(i);
+  const int st = a_st(a);
+  switch ((int)((desc >> 16) & 0xFFu)) {
+    case A_RESTART: return h_rctr(s.hdr()) < M.R;
+    case A_REQUESTVOTE:
+    case A_TIMEOUT: return h_ectr(s.hdr()) < M.E && (st == FOLLOWER || st == CANDIDATE);
+    case A_RVIJ: return st == CANDIDATE && i != jv;
+    case A_BECOMELEADER: return st == CANDIDATE;
+    case A_CLIENT: return st == LEADER && h_acked(s.hdr(), jv) == 0;
+    case A_ADVCOMMIT: return st == LEADER;
+    case A_APPENDENTRIES: return st == LEADER && i != jv && !(SPEC == RAFT && ((a_pending(a) >> jv) & 1));
+    case A_ADVFSYNC: return a_fsync(a) < a_len(a);
+    case A_SENDPULL: return st == FOLLOWER && i != jv && a_voted(a) == jv;
+  }
+  return true;
 }
 
 // Write parent + delta as a packed row of M.words words (a multiple of 4),
@@ -1335,7 +1386,7 @@ RMC_HD uint64_t canon_from_sums(const Model& M, const DeltaView<SPEC, N>& V, con
   uint64_t best = ~0ULL;
   const int np = ties ? M.nperm : 1;
 #if defined(RMC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-  extern __device__ unsigned long long g_stamps[16];
+  extern __device__ unsigned long long g_stamps[32];
   atomicAdd(&g_stamps[4], 1ULL);
   if (ties) atomicAdd(&g_stamps[5], 1ULL);
 #endif
