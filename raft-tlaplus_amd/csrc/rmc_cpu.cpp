@@ -387,6 +387,7 @@ int check_cpu(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   RMC_CPU(FSYNC, 2) RMC_CPU(FSYNC, 3) RMC_CPU(FSYNC, 4) RMC_CPU(FSYNC, 5)
   RMC_CPU(PULL, 2) RMC_CPU(PULL, 3) RMC_CPU(PULL, 4) RMC_CPU(PULL, 5)
   RMC_CPU(PULL2, 2) RMC_CPU(PULL2, 3) RMC_CPU(PULL2, 4) RMC_CPU(PULL2, 5)
+  RMC_CPU(KRAFT, 2) RMC_CPU(KRAFT, 3)
 #undef RMC_CPU
   throw std::runtime_error("unsupported model shape");
 }

@@ -182,6 +182,7 @@ int spec_of_module(const std::string& m) {
   if (m == "RaftFsync") return FSYNC;
   if (m == "PullRaft") return PULL;
   if (m == "PullRaftVariant2") return PULL2;
+  if (m == "KRaft") return KRAFT;
   return -1;
 }
 
@@ -191,7 +192,10 @@ const char* act_label(int a) {
                             "HandleRequestVoteRequest", "HandleRequestVoteResponse", "RejectAppendEntriesRequest",
                             "AcceptAppendEntriesRequest", "HandleAppendEntriesResponse", "RejectPullEntriesRequest",
                             "AcceptPullEntriesRequest", "LearnOfLeader", "SendPullEntriesRequest",
-                            "HandleSuccessPullEntriesResponse", "HandleFailPullEntriesResponse"};
+                            "HandleSuccessPullEntriesResponse", "HandleFailPullEntriesResponse",
+                            "RejectFetchRequest", "DivergingFetchRequest", "AcceptFetchRequest",
+                            "HandleBeginQuorumRequest", "SendFetchRequest", "HandleSuccessFetchResponse",
+                            "HandleDivergingFetchResponse", "HandleErrorFetchResponse"};
   return (a >= 0 && a < A_NUM) ? n[a] : "?";
 }
 
@@ -214,6 +218,11 @@ void build_actions(Model& M) {
            {A_BECOMELEADER, K_I}, {A_CLIENT, K_IV}, {A_REJPULL, K_MSG}, {A_ACCPULL, K_MSG}, {A_LEARN, K_MSG},
            {A_SENDPULL, K_IJ}, {A_HSUCC, K_MSG}, {A_HFAIL, K_MSG}};
       break;
+    case KRAFT:  // KRaft.tla:823-840
+      t = {{A_RESTART, K_I}, {A_REQUESTVOTE, K_I}, {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG}, {A_BECOMELEADER, K_I},
+           {A_CLIENT, K_IV}, {A_KREJFETCH, K_MSG}, {A_KDIVFETCH, K_MSG}, {A_KACCFETCH, K_MSG}, {A_KHBQ, K_MSG},
+           {A_KSENDFETCH, K_IJ}, {A_KHSUCC, K_MSG}, {A_KHDIV, K_MSG}, {A_KHERR, K_MSG}};
+      break;
   }
   M.nact = (int)t.size();
   int off = 0, nf = 0;
@@ -233,7 +242,9 @@ void build_actions(Model& M) {
         // (Raft.tla:264, RaftFsync.tla:235, PullRaft.tla:397), Restart with
         // MaxRestarts = 0 (Raft.tla:227), elections with MaxElections = 0
         const int id = t[s].id, i = x % M.N, j = x / M.N;
-        if (t[s].kind == K_IJ && i == j && (id == A_APPENDENTRIES || id == A_RVIJ || id == A_SENDPULL)) continue;
+        if (t[s].kind == K_IJ && i == j &&
+            (id == A_APPENDENTRIES || id == A_RVIJ || id == A_SENDPULL || id == A_KSENDFETCH))  // KRaft.tla:608
+          continue;
         if (id == A_RESTART && M.R == 0) continue;
         if ((id == A_REQUESTVOTE || id == A_TIMEOUT) && M.E == 0) continue;
         if (nf >= MAXFIXED) throw std::runtime_error("too many fixed bindings");
@@ -301,6 +312,7 @@ unsigned long long known_spec_hash(const std::string& module) {
       {"PullRaft", 0x158f1b6f8dd861a3ULL},      // specifications/pull-raft/PullRaft.tla
       {"RaftFsync", 0x8135c01b3aedbce3ULL},     // specifications/raft-and-fsync/RaftFsync.tla
       {"PullRaftVariant2", 0xa830c4c4ebcf30b0ULL},  // specifications/pull-raft/PullRaftVariant2.tla
+      {"KRaft", 0xb2b4f50a062d58efULL},             // specifications/pull-raft/KRaft.tla
   };
   auto it = k.find(module);
   return it == k.end() ? 0 : it->second;
@@ -314,7 +326,7 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     int spec = spec_of_module(module);
     if (spec < 0)
       throw std::runtime_error("unsupported module '" + module +
-                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft, PullRaftVariant2)");
+                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft, PullRaftVariant2, KRaft)");
     if (!tla_text.empty() && tla_text.find("MODULE " + module) == std::string::npos)
       throw std::runtime_error("the .tla file does not declare MODULE " + module);
     if (!tla_text.empty()) {
@@ -385,6 +397,11 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     M.E = geti("MaxElections");
     M.R = geti("MaxRestarts");
     if (M.E < 0 || M.E > 14 || M.R < 0 || M.R > 15) throw std::runtime_error("MaxElections/MaxRestarts out of range");
+    // KRaft's records pack into one 32-bit DOMAIN word only with 2-bit epochs and
+    // offsets (rmc_spec.h kr_encode), and its fingerprint relates mleader to a
+    // message's two servers (kr_body), which is exact for N <= 3
+    if (spec == KRAFT && (M.N > 3 || M.E > 2 || M.V > 3))
+      throw std::runtime_error("the KRaft lowering supports |Server| <= 3, MaxElections <= 2, |Value| <= 3");
     if (spec == FLEX) { M.EQ = geti("ElectionQuorumSize"); M.RQ = geti("ReplicationQuorumSize"); }
     if (spec == FSYNC) {
       M.lfae = getb("LeaderFsyncBeforeAppendEntries");
@@ -396,9 +413,11 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
       int id = n == "LeaderHasAllAckedValues" ? 0 : n == "NoLogDivergence" ? 1
                                                : n == "CommittedEntriesReachMajority" ? 2
                                                : n == "TestInv" ? -2 : -1;
+      if (spec == KRAFT && n == "NeverTwoLeadersInSameEpoch") id = 3;  // KRaft.tla:916-921
+      if (spec == KRAFT && n == "NoIllegalState") id = 4;              // KRaft.tla:887-889
       if (id == -2) continue;  // TestInv == TRUE
       if (id < 0) throw std::runtime_error("unsupported invariant " + n);
-      if (M.ninv >= 3) throw std::runtime_error("too many invariants");
+      if (M.ninv >= 5) throw std::runtime_error("too many invariants");
       M.inv[M.ninv++] = id;
       m->inv_names.push_back(n);
     }
@@ -423,6 +442,10 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
       case PULL2:  // declaration order, PullRaftVariant2.tla:56-106
         m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentTerm", "state", "leader",
                         "votedFor", "log", "commitIndex", "votesGranted", "votesLastEntry", "matchIndex"};
+        break;
+      case KRAFT:  // declaration order, KRaft.tla:100-144
+        m->var_order = {"messages", "acked", "electionCtr", "restartCtr", "currentEpoch", "state", "votedFor",
+                        "leader", "pendingFetch", "log", "highWatermark", "votesGranted", "endOffset"};
         break;
     }
   } catch (std::exception& e) {
@@ -463,9 +486,10 @@ std::vector<uint32_t> init_state(const Model& M) {
   for (int i = 0; i < M.N; i++) {
     uint32_t a = 1u | (FOLLOWER << 4) | ((uint32_t)NILS << 6);  // currentTerm 1, Follower, votedFor Nil
     if (M.spec == PULL2) a |= (uint32_t)NILS << 15;          // leader and votedFor Nil (PullRaftVariant2.tla:224-225)
+    if (M.spec == KRAFT) a = kr_set_st(a | ((uint32_t)NILS << 15), KS_UNATTACHED);  // KRaft.tla:397-401
     S[1 + 4 * i] = a;
     S[2 + 4 * i] = 0;
-    S[3 + 4 * i] = pullish(M.spec) ? 0u : all_rows(M.N, 1);  // nextIndex = 1; Variant2: votesLastEntry Nil
+    S[3 + 4 * i] = (pullish(M.spec) || M.spec == KRAFT) ? 0u : all_rows(M.N, 1);  // nextIndex 1 / Nil / pendingFetch Nil
     S[4 + 4 * i] = 0;                                        // matchIndex = 0
   }
   return S;
@@ -481,7 +505,45 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
     return o + ")";
   };
   auto entry = [&](int t, int v) {
-    return "[term |-> " + std::to_string(t) + ", value |-> " + m->value_names.at(v) + "]";
+    return std::string(M.spec == KRAFT ? "[epoch |-> " : "[term |-> ") + std::to_string(t) + ", value |-> " +
+           m->value_names.at(v) + "]";
+  };
+  // KRaft records in TLC's field order (KRaft.tla:450-455, :498-504, :553-556, :578-587, :616-621, :641-677, :725-734)
+  auto kerr = [](int e) { return std::string(e == KE_FENCED ? "FencedLeaderEpoch" : e == KE_NIL ? "Nil" : e == KE_NOTLEADER ? "NotLeader" : "UnknownLeader"); };
+  auto kld = [&](int l) { return l < 0 ? std::string("Nil") : m->server_names.at(l); };
+  auto kfetch = [&](int dst, int epoch, int fo, int lfe, int src) {
+    return "[mdest |-> " + sv(dst) + ", mepoch |-> " + std::to_string(epoch) + ", mfetchOffset |-> " + std::to_string(fo) +
+           ", mlastFetchedEpoch |-> " + std::to_string(lfe) + ", msource |-> " + sv(src) + ", mtype |-> FetchRequest]";
+  };
+  auto kmsg = [&](uint32_t mw) {
+    const KMsg f = kr_decode(mw);
+    const std::string ep = std::to_string(f.epoch);
+    switch (f.cls) {
+      case 0: return "[mdest |-> " + sv(f.dst) + ", mepoch |-> " + ep + ", msource |-> " + sv(f.src) + ", mtype |-> BeginQuorumRequest]";
+      case 1: return "[mdest |-> " + sv(f.dst) + ", mepoch |-> " + ep + ", merror |-> " + kerr(f.err) + ", msource |-> " + sv(f.src) + ", mtype |-> BeginQuorumResponse]";
+      case 2:
+        if (f.granted)
+          return "[mdest |-> " + sv(f.dst) + ", mepoch |-> " + ep + ", mlastLogEpoch |-> " + std::to_string(f.f1) +
+                 ", mlastLogOffset |-> " + std::to_string(f.f2) + ", msource |-> " + sv(f.src) + ", mtype |-> RequestVoteRequest]";
+        return kfetch(f.dst, f.epoch, f.f1, f.f2, f.src);
+      case 3:
+        return "[mdest |-> " + sv(f.dst) + ", mepoch |-> " + ep + ", merror |-> " + kerr(f.err) + ", mleader |-> " + kld(f.leader) +
+               ", msource |-> " + sv(f.src) + ", mtype |-> RequestVoteResponse, mvoteGranted |-> " + (f.granted ? "TRUE" : "FALSE") + "]";
+      default: {
+        const std::string corr = "[correlation |-> " + kfetch(f.src, f.cepoch, f.cfo, f.clfe, f.dst) + ", mdest |-> " + sv(f.dst);
+        const std::string tail = ", mhwm |-> " + std::to_string(f.hwm) + ", mleader |-> " + kld(f.leader);
+        if (f.cls == KR_NOTOK)
+          return corr + ", mepoch |-> " + ep + ", merror |-> " + kerr(f.err) + tail + ", mresult |-> NotOk, msource |-> " +
+                 sv(f.src) + ", mtype |-> FetchResponse]";
+        if (f.cls == KR_OK)
+          return corr + ", mentries |-> " + (f.elen ? "<<" + entry(f.eepoch, f.evalue) + ">>" : std::string("<<>>")) +
+                 ", mepoch |-> " + ep + ", merror |-> Nil" + tail + ", mresult |-> Ok, msource |-> " + sv(f.src) +
+                 ", mtype |-> FetchResponse]";
+        return corr + ", mdivergingEndOffset |-> " + std::to_string(f.divend) + ", mdivergingEpoch |-> " +
+               std::to_string(f.divepoch) + ", mepoch |-> " + ep + ", merror |-> Nil" + tail +
+               ", mresult |-> Diverging, msource |-> " + sv(f.src) + ", mtype |-> FetchResponse]";
+      }
+    }
   };
   std::vector<std::pair<std::string, std::string>> o;
   int nm = h_nmsg(S[0]);
@@ -493,6 +555,10 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
         val = "(";
         for (int k = 0; k < nm; k++) {
           const uint32_t mw = S[1 + 4 * M.N + k];
+          if (M.spec == KRAFT) {
+            val += (k ? " @@\n  " : "") + kmsg(mw) + " :> " + std::to_string(msg_count(mw));
+            continue;
+          }
           MsgF f = M.spec == PULL2 ? msg_decode<PULL2>(mw) : M.spec == PULL ? msg_decode<PULL>(mw) : msg_decode<RAFT>(mw);
           std::string r;
           auto B = [](int x) { return std::string(x ? "TRUE" : "FALSE"); };
@@ -563,13 +629,31 @@ std::vector<std::pair<std::string, std::string>> state_vars(const rmc_model* m, 
       val += ")";
     } else if (var == "electionCtr") val = std::to_string(h_ectr(S[0]));
     else if (var == "restartCtr") val = std::to_string(h_rctr(S[0]));
-    else if (var == "currentTerm") val = fn([&](int i) { return std::to_string(a_term(S[1 + 4 * i])); });
+    else if (var == "currentTerm" || var == "currentEpoch") val = fn([&](int i) { return std::to_string(a_term(S[1 + 4 * i])); });
+    else if (var == "state" && M.spec == KRAFT)
+      val = fn([&](int i) {
+        static const char* names[] = {"Follower", "Candidate", "Leader", "Unattached", "Voted", "IllegalState", "?", "?"};
+        return std::string(names[kr_st(S[1 + 4 * i])]);
+      });
+    else if (var == "pendingFetch")
+      val = fn([&](int i) {
+        const uint32_t c = S[3 + 4 * i];
+        if (!(c & 1u)) return std::string("Nil");
+        return kfetch((int)getb(c, 7, 3), (int)getb(c, 1, 2), (int)getb(c, 3, 2), (int)getb(c, 5, 2), i);
+      });
+    else if (var == "highWatermark") val = fn([&](int i) { return std::to_string(a_commit(S[1 + 4 * i])); });
+    else if (var == "endOffset")
+      val = fn([&](int i) {
+        std::string o2 = "(";
+        for (int j = 0; j < M.N; j++) o2 += (j ? " @@ " : "") + m->server_names[j] + " :> " + std::to_string(row_get(S[4 + 4 * i], j));
+        return o2 + ")";
+      });
     else if (var == "state")
       val = fn([&](int i) {
         int st = a_st(S[1 + 4 * i]);
         return std::string(st == FOLLOWER ? "Follower" : st == CANDIDATE ? "Candidate" : "Leader");
       });
-    else if (var == "votedFor" && M.spec == PULL2) val = fn([&](int i) { return sv(a_votedfor2(S[1 + 4 * i])); });
+    else if (var == "votedFor" && (M.spec == PULL2 || M.spec == KRAFT)) val = fn([&](int i) { return sv(a_votedfor2(S[1 + 4 * i])); });
     else if (var == "votedFor" || var == "leader") val = fn([&](int i) { return sv(a_voted(S[1 + 4 * i])); });
     else if (var == "votesLastEntry")
       val = fn([&](int i) {

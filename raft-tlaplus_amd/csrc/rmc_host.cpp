@@ -97,6 +97,8 @@ static int inv_t(const Model& M, const uint32_t* S, int* err) {
     case PULL2 * 8 + 3: return FN<PULL2, 3>(__VA_ARGS__);        \
     case PULL2 * 8 + 4: return FN<PULL2, 4>(__VA_ARGS__);        \
     case PULL2 * 8 + 5: return FN<PULL2, 5>(__VA_ARGS__);        \
+    case KRAFT * 8 + 2: return FN<KRAFT, 2>(__VA_ARGS__);        \
+    case KRAFT * 8 + 3: return FN<KRAFT, 3>(__VA_ARGS__);        \
   }
 
 int host_eval_apply(const Model& M, const uint32_t* parent, int binding, uint32_t* out, int* ordinal, int* act,
@@ -137,8 +139,9 @@ namespace rmc {
 std::vector<uint32_t> selftest_init_state(const Model& M) {
   std::vector<uint32_t> S(M.words, 0u);
   for (int i = 0; i < M.N; i++) {
-    S[1 + 4 * i] = 1u | ((uint32_t)NILS << 6) | (M.spec == PULL2 ? (uint32_t)NILS << 15 : 0u);
-    S[3 + 4 * i] = pullish(M.spec) ? 0u : all_rows(M.N, 1);
+    S[1 + 4 * i] = 1u | ((uint32_t)NILS << 6) | ((M.spec == PULL2 || M.spec == KRAFT) ? (uint32_t)NILS << 15 : 0u);
+    if (M.spec == KRAFT) S[1 + 4 * i] = kr_set_st(S[1 + 4 * i], KS_UNATTACHED);
+    S[3 + 4 * i] = (pullish(M.spec) || M.spec == KRAFT) ? 0u : all_rows(M.N, 1);
   }
   return S;
 }
@@ -169,5 +172,28 @@ extern "C" int rmc_selftest_encode_msg(int spec, const int* f, uint32_t* out) {
            d.midx == m.midx && d.lci == m.lci && d.lct == m.lct && d.lcenil == m.lcenil && d.count == m.count &&
            (int)((*out >> sp) & 7u) == m.src && (int)((*out >> dp) & 7u) == m.dst && term == m.term &&
            type == m.type;
+  return ok ? 0 : 1;
+}
+
+// KRaft record probe (tests/test_kraft.py): f = cls, dst, src, epoch, err,
+// leader (-1 Nil), granted, f1, f2, cepoch, cfo, clfe, elen, eepoch, evalue,
+// hwm, divend, divepoch, count.  Packs with kr_encode and checks that
+// kr_decode, the source/destination positions and the epoch read it back.
+extern "C" int rmc_selftest_encode_kmsg(const int* f, uint32_t* out) {
+  using namespace rmc;
+  KMsg m = kmsg_zero();
+  m.cls = f[0]; m.dst = f[1]; m.src = f[2]; m.epoch = f[3]; m.err = f[4]; m.leader = f[5]; m.granted = f[6];
+  m.f1 = f[7]; m.f2 = f[8]; m.cepoch = f[9]; m.cfo = f[10]; m.clfe = f[11]; m.elen = f[12]; m.eepoch = f[13];
+  m.evalue = f[14]; m.hwm = f[15]; m.divend = f[16]; m.divepoch = f[17]; m.count = f[18];
+  *out = kr_encode(m);
+  const KMsg d = kr_decode(*out);
+  int sp, dp;
+  msg_srcdst_pos<KRAFT>(*out, sp, dp);
+  const int ok = d.cls == m.cls && d.dst == m.dst && d.src == m.src && d.epoch == m.epoch && d.err == m.err &&
+                 d.leader == m.leader && d.granted == m.granted && d.f1 == m.f1 && d.f2 == m.f2 &&
+                 d.cepoch == m.cepoch && d.cfo == m.cfo && d.clfe == m.clfe && d.elen == m.elen &&
+                 d.eepoch == m.eepoch && d.evalue == m.evalue && d.hwm == m.hwm && d.divend == m.divend &&
+                 d.divepoch == m.divepoch && d.count == m.count && (int)((*out >> sp) & 7u) == m.src &&
+                 (int)((*out >> dp) & 7u) == m.dst && msg_term<KRAFT>(*out) == m.epoch;
   return ok ? 0 : 1;
 }

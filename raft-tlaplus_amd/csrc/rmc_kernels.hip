@@ -336,6 +336,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     if (p < np) {
       PState<SPEC, N> s{sS + p * L.Wp};
       const int nm = s.nmsg();
+      (void)nm;
 #ifdef RMC_STAMPS
       {  // binding statistics: message bindings, live ones (act_message's fast reject passes), wave steps
         const int B = cM.nfixed + nm;
@@ -913,6 +914,10 @@ static void dispatch(int spec, int N, bool expand, const LevelArgs& a, hipStream
     case FSYNC: dispatch_n<FSYNC>(N, expand, a, s); break;
     case PULL: dispatch_n<PULL>(N, expand, a, s); break;
     case PULL2: dispatch_n<PULL2>(N, expand, a, s); break;
+    case KRAFT:  // the KRaft lowering is for N <= 3 (model load enforces it)
+      if (N == 2) expand ? Launch::expand<KRAFT, 2>(a, s) : Launch::materialize<KRAFT, 2>(a, s);
+      if (N == 3) expand ? Launch::expand<KRAFT, 3>(a, s) : Launch::materialize<KRAFT, 3>(a, s);
+      break;
   }
 }
 
@@ -1048,6 +1053,7 @@ void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long w
   RMC_SIM(FSYNC, 2) RMC_SIM(FSYNC, 3) RMC_SIM(FSYNC, 4) RMC_SIM(FSYNC, 5)
   RMC_SIM(PULL, 2) RMC_SIM(PULL, 3) RMC_SIM(PULL, 4) RMC_SIM(PULL, 5)
   RMC_SIM(PULL2, 2) RMC_SIM(PULL2, 3) RMC_SIM(PULL2, 4) RMC_SIM(PULL2, 5)
+  RMC_SIM(KRAFT, 2) RMC_SIM(KRAFT, 3)
 #undef RMC_SIM
 }
 

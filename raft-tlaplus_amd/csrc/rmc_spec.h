@@ -46,15 +46,18 @@
 
 namespace rmc {
 
-enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3, PULL2 = 4 };
+enum SpecKind { RAFT = 0, FLEX = 1, FSYNC = 2, PULL = 3, PULL2 = 4, KRAFT = 5 };
 // the pull family (PullRaft, PullRaftVariant2): no nextIndex, LeaderNotify, pull replication
 constexpr bool pullish(int spec) { return spec == PULL || spec == PULL2; }
 enum SrvState { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
-enum MType { RVREQ = 0, RVRESP = 1, AEREQ = 2, AERESP = 3, LNREQ = 4, PEREQ = 5, PERESP = 6 };
+enum MType { RVREQ = 0, RVRESP = 1, AEREQ = 2, AERESP = 3, LNREQ = 4, PEREQ = 5, PERESP = 6,
+             KBQREQ = 7, KBQRESP = 8, KFREQ = 9, KFRESP = 10 };  // KRaft's BeginQuorum*, Fetch*
 enum ActId {
   A_RESTART = 0, A_REQUESTVOTE, A_TIMEOUT, A_RVIJ, A_BECOMELEADER, A_CLIENT, A_ADVCOMMIT,
   A_APPENDENTRIES, A_ADVFSYNC, A_UPDATETERM, A_HRVREQ, A_HRVRESP, A_REJAE, A_ACCAE, A_HAERESP,
-  A_REJPULL, A_ACCPULL, A_LEARN, A_SENDPULL, A_HSUCC, A_HFAIL, A_NUM
+  A_REJPULL, A_ACCPULL, A_LEARN, A_SENDPULL, A_HSUCC, A_HFAIL,
+  // KRaft (pull-raft/KRaft.tla:823-840)
+  A_KREJFETCH, A_KDIVFETCH, A_KACCFETCH, A_KHBQ, A_KSENDFETCH, A_KHSUCC, A_KHDIV, A_KHERR, A_NUM
 };
 enum ActKind { K_I = 0, K_IV = 1, K_IJ = 2, K_MSG = 3 };
 enum ErrCode {
@@ -78,7 +81,7 @@ struct Model {
   int kmax, words;  // words = 1 + 4N + kmax
   int nperm;
   uint32_t perm[MAXPERM];  // permutation p maps server j -> (perm[p] >> 3j) & 7
-  int ninv, inv[3];        // invariant ids in cfg order: 0 LHAAV, 1 NLD, 2 CERM
+  int ninv, inv[5];        // invariant ids in cfg order: 0 LHAAV, 1 NLD, 2 CERM, 3 NTLISE, 4 NIS (KRaft)
   int nact, act_id[MAXACT], act_kind[MAXACT], act_off[MAXACT];
   int nfixed;
   uint8_t fb_act[MAXFIXED], fb_x[MAXFIXED];  // fixed binding -> (action slot, binding index)
@@ -117,7 +120,9 @@ RMC_HD int a_pending(uint32_t a) { return (int)getb(a, 25, 7); }
 // PullRaftVariant2.tla:114); PullRaft's view keeps acked, so only the counters
 // (PullRaft.tla:123).
 template <int SPEC>
-RMC_HD uint32_t hidden_of(uint32_t h) { return SPEC == 3 /* PULL */ ? (h >> 8) & 0xFFu : (h >> 8) & 0xFFFFu; }
+RMC_HD uint32_t hidden_of(uint32_t h) {
+  return (SPEC == 3 /* PULL */ || SPEC == 5 /* KRAFT, KRaft.tla:154 */) ? (h >> 8) & 0xFFu : (h >> 8) & 0xFFFFu;
+}
 // PullRaftVariant2: votedFor[i] (bits 15-17 of A) and votesLastEntry row (C)
 RMC_HD int a_votedfor2(uint32_t a) { return (int)getb(a, 15, 3); }
 RMC_HD int vle_slot(int i, int j) { return j - (j > i ? 1 : 0); }
@@ -277,6 +282,12 @@ RMC_HD MsgF msg_decode(uint32_t w) {
 template <int SPEC>
 RMC_HD void msg_srcdst_pos(uint32_t w, int& sp, int& dp) {
   int cls = (int)(w >> 30);
+  if (SPEC == KRAFT) {  // 3-bit classes (kr_encode): the FetchResponses' servers are their correlation's
+    const int c3 = (int)(w >> 29);
+    dp = c3 >= 4 ? 17 : 26;
+    sp = c3 >= 4 ? 26 : c3 == 0 ? 21 : c3 == 1 ? 19 : 16;
+    return;
+  }
   if (SPEC == PULL2) {
     if (cls == 0 || cls == 1) { dp = 27; sp = 16; }
     else if (cls == 2) { dp = 24; sp = 14; }
@@ -294,6 +305,10 @@ RMC_HD void msg_srcdst_pos(uint32_t w, int& sp, int& dp) {
 template <int SPEC>
 RMC_HD int msg_type(uint32_t w) {
   int cls = (int)(w >> 30);
+  if (SPEC == KRAFT) {
+    const int c3 = (int)(w >> 29);
+    return c3 == 0 ? KBQREQ : c3 == 1 ? KBQRESP : c3 == 2 ? (((w >> 23) & 1u) ? RVREQ : KFREQ) : c3 == 3 ? RVRESP : KFRESP;
+  }
   if (SPEC == PULL2) {
     if (cls == 0) return LNREQ;
     if (cls == 1) return ((w >> 26) & 1u) ? (((w >> 11) & 1u) ? RVREQ : PEREQ) : PERESP;
@@ -314,6 +329,10 @@ template <int SPEC>
 RMC_HD int msg_term(uint32_t w) {
   int cls = (int)(w >> 30);
   int pos;
+  if (SPEC == KRAFT) {  // mepoch, 2 bits
+    const int c3 = (int)(w >> 29);
+    return (int)((w >> (c3 <= 3 ? 24 : c3 == 4 ? 15 : c3 == 5 ? 10 : 11)) & 3u);
+  }
   if (SPEC == PULL2) {
     if (cls == 0) pos = 12;
     else if (cls == 1) pos = ((w >> 26) & 1u) ? 12 : 11;
@@ -338,6 +357,118 @@ RMC_HD int msg_dst(uint32_t w) {
 }
 RMC_HD uint32_t msg_rec(uint32_t w) { return w >> 3; }
 RMC_HD int msg_count(uint32_t w) { return (int)(w & 7u); }
+
+// ------------------------------------------------------------ KRaft messages
+// KRaft (pull-raft/KRaft.tla) records, MSB-first in TLC's order (field count,
+// then sorted field names with their values), class in bits 29-31:
+//   c0 BeginQuorumRequest  (4 fields) mdest 26 | mepoch 24 | msource 21
+//   c1 BeginQuorumResponse (5)        mdest 26 | mepoch 24 | merror 22 | msource 19
+//   c2 6 fields: mdest 26 | mepoch 24 | then the third name: mfetchOffset (0,
+//      FetchRequest: mfetchOffset 21 | mlastFetchedEpoch 19) < mlastLogEpoch (1,
+//      RequestVoteRequest: mlastLogEpoch 21 | mlastLogOffset 19) at bit 23 | msource 16
+//   c3 RequestVoteResponse (7)        mdest 26 | mepoch 24 | merror 22 | mleader 19 | msource 16 | mvoteGranted 15
+//   c4 FetchResponse NotOk (9)  correlation | mepoch 15 | merror 13 | mhwm 11 | mleader 8
+//   c5 FetchResponse Ok (10)    correlation | mentries (length 16, epoch 14, value 12) | mepoch 10 | mhwm 8 | mleader 5
+//   c6 FetchResponse Diverging (11) correlation | mdivergingEndOffset 15 | mdivergingEpoch 13 | mepoch 11 | mhwm 9 | mleader 6
+// correlation (the FetchRequest answered; its name sorts first) = mdest 26 |
+// mepoch 24 | mfetchOffset 22 | mlastFetchedEpoch 20 | msource 17; the
+// response's own mdest / msource are its correlation's msource / mdest, and
+// its constant fields (mresult per class; merror = Nil for Ok / Diverging,
+// KRaft.tla:670, :729) are not stored.  Value codes keep TLC's order: servers
+// by name, mleader Nil 0 < servers 1.., merror FencedLeaderEpoch 0 < Nil 1 <
+// NotLeader 2 < UnknownLeader 3 (model values by name); epochs and offsets 2
+// bits (the model loader requires MaxElections <= 2, |Value| <= 3, N <= 3).
+enum KErr { KE_FENCED = 0, KE_NIL = 1, KE_NOTLEADER = 2, KE_UNKNOWN = 3 };
+enum KRes { KR_NOTOK = 4, KR_OK = 5, KR_DIV = 6 };  // = the FetchResponse's class
+struct KMsg {
+  int cls, dst, src, epoch, err, leader;  // leader: -1 = Nil
+  int granted, f1, f2;                    // RVReq: lastLogEpoch, lastLogOffset; FetchReq: fetchOffset, lastFetchedEpoch
+  int cepoch, cfo, clfe;                  // FetchResponse: correlation's mepoch, mfetchOffset, mlastFetchedEpoch
+  int elen, eepoch, evalue, hwm, divend, divepoch;
+  int count;
+};
+RMC_HD KMsg kmsg_zero() {
+  KMsg m;
+  m.cls = m.dst = m.src = m.epoch = m.err = m.granted = m.f1 = m.f2 = 0;
+  m.cepoch = m.cfo = m.clfe = m.elen = m.eepoch = m.evalue = m.hwm = m.divend = m.divepoch = m.count = 0;
+  m.leader = -1;
+  m.err = KE_NIL;
+  return m;
+}
+RMC_HD uint32_t kbits(int v, int pos, int w) { return ((uint32_t)v & ((1u << w) - 1u)) << pos; }
+RMC_HD uint32_t kr_encode(const KMsg& m) {
+  uint32_t w = (uint32_t)m.cls << 29;
+  const int ld = m.leader < 0 ? 0 : m.leader + 1;
+  switch (m.cls) {
+    case 0: w |= kbits(m.dst, 26, 3) | kbits(m.epoch, 24, 2) | kbits(m.src, 21, 3); break;
+    case 1: w |= kbits(m.dst, 26, 3) | kbits(m.epoch, 24, 2) | kbits(m.err, 22, 2) | kbits(m.src, 19, 3); break;
+    case 2:
+      w |= kbits(m.dst, 26, 3) | kbits(m.epoch, 24, 2) | kbits(m.granted, 23, 1) | kbits(m.f1, 21, 2) |
+           kbits(m.f2, 19, 2) | kbits(m.src, 16, 3);
+      break;
+    case 3:
+      w |= kbits(m.dst, 26, 3) | kbits(m.epoch, 24, 2) | kbits(m.err, 22, 2) | kbits(ld, 19, 3) | kbits(m.src, 16, 3) |
+           kbits(m.granted, 15, 1);
+      break;
+    default:  // FetchResponse: correlation (a request from dst to src)
+      w |= kbits(m.src, 26, 3) | kbits(m.cepoch, 24, 2) | kbits(m.cfo, 22, 2) | kbits(m.clfe, 20, 2) | kbits(m.dst, 17, 3);
+      if (m.cls == KR_NOTOK) w |= kbits(m.epoch, 15, 2) | kbits(m.err, 13, 2) | kbits(m.hwm, 11, 2) | kbits(ld, 8, 3);
+      else if (m.cls == KR_OK)
+        w |= kbits(m.elen, 16, 1) | kbits(m.eepoch, 14, 2) | kbits(m.evalue, 12, 2) | kbits(m.epoch, 10, 2) |
+             kbits(m.hwm, 8, 2) | kbits(ld, 5, 3);
+      else
+        w |= kbits(m.divend, 15, 2) | kbits(m.divepoch, 13, 2) | kbits(m.epoch, 11, 2) | kbits(m.hwm, 9, 2) |
+             kbits(ld, 6, 3);
+      break;
+  }
+  return w | ((uint32_t)m.count & 7u);
+}
+RMC_HD int kget(uint32_t w, int pos, int wd) { return (int)((w >> pos) & ((1u << wd) - 1u)); }
+RMC_HD KMsg kr_decode(uint32_t w) {
+  KMsg m = kmsg_zero();
+  m.count = (int)(w & 7u);
+  m.cls = (int)(w >> 29);
+  int ld = 0;
+  switch (m.cls) {
+    case 0: m.dst = kget(w, 26, 3); m.epoch = kget(w, 24, 2); m.src = kget(w, 21, 3); break;
+    case 1: m.dst = kget(w, 26, 3); m.epoch = kget(w, 24, 2); m.err = kget(w, 22, 2); m.src = kget(w, 19, 3); break;
+    case 2:
+      m.dst = kget(w, 26, 3); m.epoch = kget(w, 24, 2); m.granted = kget(w, 23, 1); m.f1 = kget(w, 21, 2);
+      m.f2 = kget(w, 19, 2); m.src = kget(w, 16, 3);
+      break;
+    case 3:
+      m.dst = kget(w, 26, 3); m.epoch = kget(w, 24, 2); m.err = kget(w, 22, 2); ld = kget(w, 19, 3);
+      m.src = kget(w, 16, 3); m.granted = kget(w, 15, 1);
+      break;
+    default:
+      m.src = kget(w, 26, 3); m.cepoch = kget(w, 24, 2); m.cfo = kget(w, 22, 2); m.clfe = kget(w, 20, 2);
+      m.dst = kget(w, 17, 3);
+      if (m.cls == KR_NOTOK) { m.epoch = kget(w, 15, 2); m.err = kget(w, 13, 2); m.hwm = kget(w, 11, 2); ld = kget(w, 8, 3); }
+      else if (m.cls == KR_OK) {
+        m.elen = kget(w, 16, 1); m.eepoch = kget(w, 14, 2); m.evalue = kget(w, 12, 2); m.epoch = kget(w, 10, 2);
+        m.hwm = kget(w, 8, 2); ld = kget(w, 5, 3);
+      } else {
+        m.divend = kget(w, 15, 2); m.divepoch = kget(w, 13, 2); m.epoch = kget(w, 11, 2); m.hwm = kget(w, 9, 2);
+        ld = kget(w, 6, 3);
+      }
+      break;
+  }
+  m.leader = ld - 1;
+  return m;
+}
+// The fingerprint's view of a KRaft message body: msource / mdest masked (the
+// pair sums key them) and mleader as its relation to them (Nil, = source, =
+// destination, the third server): a function of the relabelled message that
+// is injective for N <= 3.
+RMC_HD uint32_t kr_body(uint32_t w, int sp, int dp) {
+  uint32_t r = w & ~((7u << sp) | (7u << dp));
+  const int c3 = (int)(w >> 29);
+  if (c3 < 3) return r;
+  const int lp = c3 == 3 ? 19 : c3 == 4 ? 8 : c3 == 5 ? 5 : 6;
+  const int ld = (int)((w >> lp) & 7u), src = (int)((w >> sp) & 7u), dst = (int)((w >> dp) & 7u);
+  const uint32_t rel = ld == 0 ? 0u : ld - 1 == src ? 1u : ld - 1 == dst ? 2u : 3u;
+  return (r & ~(7u << lp)) | (rel << lp);
+}
 
 // ------------------------------------------------------------------ delta
 // A successor = parent + (one server's words replaced) + (message ops) +
@@ -488,6 +619,315 @@ RMC_HD int last_common_entry(uint32_t a, uint32_t b, int lastIndex, int lastTerm
   }
   term = idx ? e_term(b, idx - 1) : 0;
   return idx;
+}
+
+// ------------------------------------------------------------------ KRaft
+// pull-raft/KRaft.tla.  Server words: A = currentEpoch 0-3 | state 4-5 (+ bit
+// 25) | leader 6-8 | Len(log) 9-11 | highWatermark 12-14 | votedFor 15-17 |
+// votesGranted 18-24; B = log ([epoch, value] entries, as Raft's [term, value]);
+// C = pendingFetch (valid 0 | mepoch 1-2 | mfetchOffset 3-4 |
+// mlastFetchedEpoch 5-6 | mdest 7-9; msource is the server itself);
+// D = endOffset row.  States: Follower 0, Candidate 1, Leader 2, Unattached 3,
+// Voted 4, IllegalState 5 (only Leader has low bits 2, so a_st() == LEADER
+// stays exact for the shared invariants).
+enum KState { KS_FOLLOWER = 0, KS_CANDIDATE = 1, KS_LEADER = 2, KS_UNATTACHED = 3, KS_VOTED = 4, KS_ILLEGAL = 5 };
+RMC_HD int kr_st(uint32_t a) { return (int)(getb(a, 4, 2) | (getb(a, 25, 1) << 2)); }
+RMC_HD uint32_t kr_set_st(uint32_t a, int st) { return setb(setb(a, 4, 2, (uint32_t)st & 3u), 25, 1, (uint32_t)st >> 2); }
+RMC_HD int kr_leader(uint32_t a) { int l = a_voted(a); return l == NILS ? -1 : l; }  // -1 = Nil
+RMC_HD uint32_t kr_set_leader(uint32_t a, int l) { return setb(a, 6, 3, l < 0 ? (uint32_t)NILS : (uint32_t)l); }
+RMC_HD int kr_last_epoch(uint32_t a, uint32_t b) { int L = a_len(a); return L ? e_term(b, L - 1) : 0; }
+RMC_HD uint32_t kr_pf(int epoch, int fo, int lfe, int dest) {
+  return 1u | ((uint32_t)epoch << 1) | ((uint32_t)fo << 3) | ((uint32_t)lfe << 5) | ((uint32_t)dest << 7);
+}
+// CompareEntries (KRaft.tla:247-251)
+RMC_HD int kr_cmp(int o1, int e1, int o2, int e2) {
+  if (e1 > e2) return 1;
+  if (e1 == e2 && o1 > o2) return 1;
+  if (e1 == e2 && o1 == o2) return 0;
+  return -1;
+}
+// a transition record [state, epoch, leader] (KRaft.tla:329-349)
+struct KTr { int st, epoch, leader; };
+RMC_HD KTr kr_illegal() { return KTr{KS_ILLEGAL, 0, -1}; }  // SetIllegalState (:329-330)
+template <int SPEC, int N>
+RMC_HD KTr kr_maybe_transition(const PState<SPEC, N>& s, int i, int leaderId, int epoch) {  // :351-367
+  const uint32_t a = s.A(i);
+  const int st = kr_st(a), cur = a_term(a), ld = kr_leader(a);
+  // HasConsistentLeader (:316-327)
+  const bool consistent = leaderId == i ? st == KS_LEADER : (epoch != cur || leaderId < 0 || ld < 0 || ld == leaderId);
+  if (!consistent) return kr_illegal();
+  // TransitionToFollower (:344-349)
+  auto to_follower = [&]() {
+    if (cur == epoch && (st == KS_FOLLOWER || st == KS_LEADER)) return kr_illegal();
+    return KTr{KS_FOLLOWER, epoch, leaderId};
+  };
+  if (epoch > cur) return leaderId < 0 ? KTr{KS_UNATTACHED, epoch, -1} : to_follower();
+  if (leaderId >= 0 && ld < 0) return to_follower();
+  return KTr{st, cur, ld};
+}
+// MaybeHandleCommonResponse (:369-392)
+template <int SPEC, int N>
+RMC_HD KTr kr_common_response(const PState<SPEC, N>& s, int i, int leaderId, int epoch, int err, bool& handled) {
+  const uint32_t a = s.A(i);
+  const int cur = a_term(a);
+  handled = true;
+  if (epoch < cur) return KTr{kr_st(a), cur, kr_leader(a)};
+  if (epoch > cur || err != KE_NIL) return kr_maybe_transition(s, i, leaderId, epoch);
+  if (leaderId >= 0 && kr_leader(a) < 0) return KTr{KS_FOLLOWER, cur, leaderId};
+  handled = false;
+  return KTr{kr_st(a), cur, kr_leader(a)};
+}
+RMC_HD uint32_t kr_apply(uint32_t a, const KTr& t) {
+  return kr_set_leader(setb(kr_set_st(a, t.st), 0, 4, (uint32_t)t.epoch), t.leader);
+}
+// Reply (:220-227): a FetchResponse must be new; other responses increment
+template <int SPEC, int N>
+RMC_HD bool kr_reply(const PState<SPEC, N>& s, Delta& d, const KMsg& resp, int req_k) {
+  const uint32_t r1 = kr_encode(resp) | 1u;
+  const uint32_t req = s.msg(req_k);
+  if (!(msg_count(req) > 0)) return false;
+  const int k = s.find(r1);
+  if (k >= 0 && resp.cls >= KR_NOTOK) return false;
+  push_op(d, req_k, req - 1u);
+  if (k >= 0) {
+    const uint32_t w = s.msg(k);
+    if (msg_count(w) >= 7) { d.err = E_CAP_COUNT; return true; }
+    push_op(d, k, w + 1u);
+  } else {
+    push_op(d, -1, r1);
+  }
+  return true;
+}
+// EndOffsetForEpoch (:285-301) -> offset, epoch
+RMC_HD int kr_end_offset_for_epoch(uint32_t a, uint32_t b, int lfe, int& ep) {
+  int off = 0;
+  for (int x = 1; x <= a_len(a); x++)
+    if (e_term(b, x - 1) <= lfe) off = x;
+  ep = off ? e_term(b, off - 1) : 0;
+  return off;
+}
+
+template <int SPEC, int N>
+RMC_HD bool kr_fixed(const PState<SPEC, N>& s, const Model& M, int act, int i, int jv, Delta& d) {
+  const uint32_t a = s.A(i), b = s.B(i);
+  const int st = kr_st(a);
+  switch (act) {
+    case A_RESTART: {  // KRaft.tla:423-432
+      if (!(h_rctr(s.hdr()) < M.R)) return false;
+      begin_srv(s, d, i);
+      uint32_t x = kr_set_leader(kr_set_st(a, KS_FOLLOWER), -1);
+      x = setb(x, 18, 7, 0);   // votesGranted = {}
+      x = setb(x, 12, 3, 0);   // highWatermark = 0
+      d.w[0] = x;
+      d.w[2] = 0;              // pendingFetch = Nil
+      d.w[3] = 0;              // endOffset[i] = [j |-> 0]
+      d.hdr = setb(s.hdr(), 12, 4, (uint32_t)(h_rctr(s.hdr()) + 1));
+      return true;
+    }
+    case A_REQUESTVOTE: {  // :439-456
+      const int ec = h_ectr(s.hdr());
+      if (!(ec < M.E)) return false;
+      if (!(st == KS_FOLLOWER || st == KS_CANDIDATE || st == KS_UNATTACHED)) return false;
+      const int e1 = a_term(a) + 1;
+      if (e1 > 3) { d.err = E_CAP_TERM; return true; }
+      KMsg m = kmsg_zero();
+      m.cls = 2; m.granted = 1; m.epoch = e1; m.f1 = kr_last_epoch(a, b); m.f2 = a_len(a); m.src = i; m.count = 1;
+      for (int j = 0; j < N; j++) {
+        if (j == i) continue;
+        m.dst = j;
+        if (!op_send_once(s, d, kr_encode(m))) return false;  // SendMultipleOnce
+      }
+      begin_srv(s, d, i);
+      uint32_t x = kr_set_leader(kr_set_st(a, KS_CANDIDATE), -1);
+      x = setb(x, 0, 4, (uint32_t)e1);
+      x = setb(x, 15, 3, (uint32_t)i);     // votedFor = i
+      x = setb(x, 18, 7, 1u << i);         // votesGranted = {i}
+      d.w[0] = x;
+      d.w[2] = 0;                          // pendingFetch = Nil
+      d.hdr = setb(s.hdr(), 8, 4, (uint32_t)(ec + 1));
+      return true;
+    }
+    case A_BECOMELEADER: {  // :546-558
+      if (st != KS_CANDIDATE) return false;
+      if (!(popc7((uint32_t)a_votes(a)) * 2 > N)) return false;
+      KMsg m = kmsg_zero();
+      m.cls = 0; m.epoch = a_term(a); m.src = i; m.count = 1;
+      for (int j = 0; j < N; j++) {
+        if (j == i) continue;
+        m.dst = j;
+        if (!op_send_once(s, d, kr_encode(m))) return false;
+      }
+      begin_srv(s, d, i);
+      d.w[0] = kr_set_leader(kr_set_st(a, KS_LEADER), i);
+      d.w[3] = 0;  // endOffset[i] = [j |-> 0]
+      return true;
+    }
+    case A_CLIENT: {  // :594-603
+      if (st != KS_LEADER || h_acked(s.hdr(), jv) != 0) return false;
+      begin_srv(s, d, i);
+      log_append(d.w[0], d.w[1], a_term(a), jv, d.err);
+      d.hdr = setb(s.hdr(), 16 + 2 * jv, 2, 1);  // acked[v] = FALSE
+      return true;
+    }
+    case A_KSENDFETCH: {  // :607-624
+      if (i == jv || st != KS_FOLLOWER || kr_leader(a) != jv || (s.Cw(i) & 1u)) return false;
+      KMsg m = kmsg_zero();
+      m.cls = 2; m.granted = 0; m.epoch = a_term(a); m.f1 = a_len(a); m.f2 = kr_last_epoch(a, b);
+      m.src = i; m.dst = jv; m.count = 1;
+      op_send_any(s, d, kr_encode(m));  // Send: _SendNoRestriction for a FetchRequest
+      begin_srv(s, d, i);
+      d.w[2] = kr_pf(m.epoch, m.f1, m.f2, jv);
+      return true;
+    }
+  }
+  return false;
+}
+
+template <int SPEC, int N>
+RMC_HD bool kr_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
+  const uint32_t w = s.msg(k);
+  if (!(msg_count(w) > 0)) return false;  // ReceivableMessage (:230-235): messages[m] > 0
+  const KMsg m = kr_decode(w);
+  const int i = m.dst, j = m.src;
+  const uint32_t a = s.A(i), b = s.B(i);
+  const int cur = a_term(a), st = kr_st(a);
+  switch (m.cls) {
+    case 2: {
+      if (m.granted) {  // HandleRequestVoteRequest (:464-513)
+        d.act = A_HRVREQ;
+        KMsg r = kmsg_zero();
+        r.cls = 3; r.src = i; r.dst = j; r.count = 1;
+        if (m.epoch < cur) {  // error = FencedLeaderEpoch: reply, no state change
+          r.epoch = cur; r.leader = kr_leader(a); r.granted = 0; r.err = KE_FENCED;
+          return kr_reply(s, d, r, k);
+        }
+        const KTr s0 = m.epoch > cur ? KTr{KS_UNATTACHED, m.epoch, -1} : KTr{st, cur, kr_leader(a)};
+        const bool logOk = kr_cmp(m.f2, m.f1, a_len(a), kr_last_epoch(a, b)) >= 0;
+        const int vf = a_votedfor2(a);
+        const bool grant = (s0.st == KS_UNATTACHED || (s0.st == KS_VOTED && vf == j)) && logOk;
+        // TransitionToVoted (:335-339): state0 is Unattached here
+        const KTr fin = (grant && s0.st == KS_UNATTACHED) ? KTr{KS_VOTED, m.epoch, -1} : s0;
+        r.epoch = m.epoch; r.leader = fin.leader; r.granted = grant; r.err = KE_NIL;
+        if (!kr_reply(s, d, r, k)) return false;
+        begin_srv(s, d, i);
+        uint32_t x = kr_apply(a, fin);
+        if (grant) x = setb(x, 15, 3, (uint32_t)j);
+        d.w[0] = x;
+        if (fin.st != st) d.w[2] = 0;  // IF state # state' THEN pendingFetch' = Nil
+        return true;
+      }
+      // a FetchRequest: RejectFetchRequest (:631-651) / DivergingFetchRequest
+      // (:658-679) / AcceptFetchRequest (:703-736) -- exclusive per message
+      KMsg r = kmsg_zero();
+      r.src = i; r.dst = j; r.count = 1; r.cepoch = m.epoch; r.cfo = m.f1; r.clfe = m.f2;
+      r.leader = kr_leader(a); r.epoch = cur; r.hwm = a_commit(a);
+      int err = st != KS_LEADER ? KE_NOTLEADER : m.epoch < cur ? KE_FENCED : m.epoch > cur ? KE_UNKNOWN : KE_NIL;
+      if (err != KE_NIL) {
+        d.act = A_KREJFETCH;
+        r.cls = KR_NOTOK; r.err = err;
+        return kr_reply(s, d, r, k);
+      }
+      int ep = 0;
+      const int off = kr_end_offset_for_epoch(a, b, m.f2, ep);
+      const bool valid = (m.f1 == 0 && m.f2 == 0) || (m.f1 <= off && m.f2 == ep);  // ValidFetchPosition (:305-310)
+      if (!valid) {
+        d.act = A_KDIVFETCH;
+        r.cls = KR_DIV; r.divepoch = ep; r.divend = off;
+        return kr_reply(s, d, r, k);
+      }
+      d.act = A_KACCFETCH;
+      const int offset = m.f1 + 1;
+      const uint32_t ne = row_set(s.Dw(i), j, m.f1);  // newEndOffset
+      // NewHighwaterMark (:689-701)
+      int best = 0;
+      for (int o = 1; o <= a_len(a); o++) {
+        uint32_t set = 1u << i;
+        for (int q = 0; q < N; q++)
+          if (row_get(ne, q) >= o) set |= 1u << q;
+        if (popc7(set) * 2 > N) best = o;
+      }
+      const int hwm = a_commit(a);
+      const int nh = (best > 0 && e_term(b, best - 1) == cur) ? best : hwm;
+      uint32_t hdr = s.hdr();
+      for (int v = 0; v < M.V; v++) {
+        if (h_acked(hdr, v) != 1) continue;
+        bool in = false;
+        for (int x = hwm + 1; x <= nh; x++)
+          if (e_value(b, x - 1) == v) in = true;
+        hdr = setb(hdr, 16 + 2 * v, 2, in ? 2u : 1u);
+      }
+      r.cls = KR_OK;
+      if (offset <= a_len(a)) { r.elen = 1; r.eepoch = e_term(b, offset - 1); r.evalue = e_value(b, offset - 1); }
+      r.hwm = nh < offset ? nh : offset;
+      if (!kr_reply(s, d, r, k)) return false;
+      d.hdr = hdr;
+      begin_srv(s, d, i);
+      d.w[0] = setb(a, 12, 3, (uint32_t)nh);
+      d.w[3] = ne;
+      return true;
+    }
+    case 3: {  // HandleRequestVoteResponse (:519-541)
+      bool handled;
+      const KTr ns = kr_common_response(s, i, m.leader, m.epoch, m.err, handled);
+      d.act = A_HRVRESP;
+      if (handled) {
+        begin_srv(s, d, i);
+        d.w[0] = kr_apply(a, ns);
+      } else {
+        if (st != KS_CANDIDATE) return false;
+        if (m.granted) {
+          begin_srv(s, d, i);
+          d.w[0] = setb(a, 18 + j, 1, 1);
+        }
+      }
+      op_discard(s, d, k);
+      return true;
+    }
+    case 0: {  // HandleBeginQuorumRequest (:563-590)
+      d.act = A_KHBQ;
+      KMsg r = kmsg_zero();
+      r.cls = 1; r.src = i; r.dst = j; r.count = 1;
+      if (m.epoch < cur) {
+        r.epoch = cur; r.err = KE_FENCED;
+        return kr_reply(s, d, r, k);
+      }
+      const KTr ns = kr_maybe_transition(s, i, j, m.epoch);
+      r.epoch = m.epoch; r.err = KE_NIL;
+      if (!kr_reply(s, d, r, k)) return false;
+      begin_srv(s, d, i);
+      d.w[0] = kr_apply(a, ns);
+      d.w[2] = 0;  // pendingFetch = Nil
+      return true;
+    }
+    case 1: return false;  // BeginQuorumResponse: no action receives it
+    default: {  // a FetchResponse: HandleSuccess / HandleDiverging / HandleError (:742-801)
+      bool handled;
+      const KTr ns = kr_common_response(s, i, m.leader, m.epoch, m.err, handled);
+      if (s.Cw(i) != kr_pf(m.cepoch, m.cfo, m.clfe, j)) return false;  // pendingFetch[i] = m.correlation
+      begin_srv(s, d, i);
+      d.w[2] = 0;  // pendingFetch = Nil
+      if (handled) {
+        d.act = A_KHERR;
+        d.w[0] = kr_apply(a, ns);
+      } else if (m.cls == KR_OK) {
+        d.act = A_KHSUCC;
+        d.w[0] = setb(a, 12, 3, (uint32_t)m.hwm);
+        if (m.elen) log_append(d.w[0], d.w[1], m.eepoch, m.evalue, d.err);
+      } else if (m.cls == KR_DIV) {
+        d.act = A_KHDIV;
+        // TruncateLog / HighestCommonOffset (:255-282)
+        int o = 0;
+        for (int x = 1; x <= a_len(a); x++)
+          if (kr_cmp(x, e_term(b, x - 1), m.divend, m.divepoch) <= 0) o = x;
+        log_truncate(d.w[0], d.w[1], o);
+      } else {
+        return false;  // NotOk is always handled (merror # Nil)
+      }
+      op_discard(s, d, k);
+      return true;
+    }
+  }
+  return false;
 }
 
 // ---------------------------------------------------------------- actions
@@ -741,12 +1181,14 @@ RMC_HD bool act_sendpull(const PState<SPEC, N>& s, const Model& M, int i, int j,
 // ranges over all of DOMAIN messages, Raft.tla:349-350).
 template <int SPEC, int N>
 RMC_HD bool msg_live(const PState<SPEC, N>& s, uint32_t w) {
+  if (SPEC == KRAFT) return msg_count(w) > 0;  // every KRaft message action needs messages[m] > 0
   return !(msg_count(w) == 0 && msg_term<SPEC>(w) <= a_term(s.A(msg_dst<SPEC>(w))));
 }
 
 // ---- message-bound actions: exactly one can be enabled per DOMAIN element
 template <int SPEC, int N>
 RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
+  if (SPEC == KRAFT) return kr_message(s, M, k, d);
   uint32_t w = s.msg(k);
   if (!msg_live<SPEC, N>(s, w)) return false;  // fast reject before the full decode
   MsgF m = msg_decode<SPEC>(w);
@@ -923,6 +1365,7 @@ RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   d.act = act;
   d.ordinal = ordinal;
+  if (SPEC == KRAFT) return kr_fixed(s, M, act, i, jv, d);
   switch (act) {
     case A_RESTART: return act_restart(s, M, i, d);
     case A_REQUESTVOTE: return act_requestvote(s, M, i, d);
@@ -979,6 +1422,18 @@ RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
   const int i = (int)((desc >> 24) & 15u), jv = (int)(desc >> 28);
   const uint32_t a = s.A(i);
   const int st = a_st(a);
+  if (SPEC == KRAFT) {
+    const int ks = kr_st(a);
+    switch ((int)((desc >> 16) & 0xFFu)) {
+      case A_RESTART: return h_rctr(s.hdr()) < M.R;
+      case A_REQUESTVOTE:
+        return h_ectr(s.hdr()) < M.E && (ks == KS_FOLLOWER || ks == KS_CANDIDATE || ks == KS_UNATTACHED);
+      case A_BECOMELEADER: return ks == KS_CANDIDATE;
+      case A_CLIENT: return ks == KS_LEADER && h_acked(s.hdr(), jv) == 0;
+      case A_KSENDFETCH: return ks == KS_FOLLOWER && i != jv && kr_leader(a) == jv && !(s.Cw(i) & 1u);
+    }
+    return true;
+  }
   switch ((int)((desc >> 16) & 0xFFu)) {
     case A_RESTART: return h_rctr(s.hdr()) < M.R;
     case A_REQUESTVOTE:
@@ -1125,6 +1580,21 @@ RMC_HD bool inv_committed_majority(const PState<SPEC, N>& s, int& err) {  // Raf
   }
   return false;
 }
+template <int SPEC, int N>
+RMC_HD bool inv_never_two_leaders(const PState<SPEC, N>& s) {  // KRaft.tla:916-921
+  for (int i = 0; i < N; i++)
+    for (int j = 0; j < N; j++) {
+      const int li = a_voted(s.A(i)), lj = a_voted(s.A(j));
+      if (li != NILS && lj != NILS && li != lj && a_term(s.A(i)) == a_term(s.A(j))) return false;
+    }
+  return true;
+}
+template <int SPEC, int N>
+RMC_HD bool inv_no_illegal_state(const PState<SPEC, N>& s) {  // KRaft.tla:887-889
+  for (int i = 0; i < N; i++)
+    if (kr_st(s.A(i)) == KS_ILLEGAL) return false;
+  return true;
+}
 // returns -1 if all hold, else the position (in cfg order) of the violated one
 template <int SPEC, int N>
 RMC_HD int check_invariants(const PState<SPEC, N>& s, const Model& M, int& err) {
@@ -1134,6 +1604,8 @@ RMC_HD int check_invariants(const PState<SPEC, N>& s, const Model& M, int& err) 
       case 0: ok = inv_leader_has_all_acked(s, M); break;
       case 1: ok = inv_no_log_divergence(s, err); break;
       case 2: ok = inv_committed_majority(s, err); break;
+      case 3: ok = inv_never_two_leaders(s); break;
+      case 4: ok = inv_no_illegal_state(s); break;
     }
     if (err) return -2;
     if (!ok) return q;
@@ -1185,13 +1657,16 @@ RMC_HD void relabel_server(uint32_t P, int i, uint32_t a, uint32_t c, uint32_t d
                            uint32_t& d2) {
   int v = a_voted(a);
   a2 = setb(a, 6, 3, v == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v));
-  if (SPEC == PULL2) {
+  if (SPEC == PULL2 || SPEC == KRAFT) {
     int v2 = a_votedfor2(a);
     a2 = setb(a2, 15, 3, v2 == NILS ? (uint32_t)NILS : (uint32_t)perm_of(P, v2));
   }
   a2 = setb(a2, 18, 7, relabel_set<N>(a_votes(a), P));
-  a2 = setb(a2, 25, 7, relabel_set<N>(a_pending(a), P));
-  c2 = SPEC == PULL2 ? relabel_vle<N>(c, i, P) : relabel_row<N>(c, P);
+  if (SPEC != KRAFT) a2 = setb(a2, 25, 7, relabel_set<N>(a_pending(a), P));  // KRaft: bit 25 is state
+  // KRaft's C word is pendingFetch[i]: its mdest relabelled
+  c2 = SPEC == PULL2 ? relabel_vle<N>(c, i, P)
+       : SPEC == KRAFT ? ((c & 1u) ? setb(c, 7, 3, (uint32_t)perm_of(P, (int)getb(c, 7, 3))) : c)
+                       : relabel_row<N>(c, P);
   d2 = relabel_row<N>(dd, P);
 }
 template <int SPEC, int N>
@@ -1208,7 +1683,8 @@ RMC_HD uint64_t h_msg(uint32_t P, uint32_t w) {
   int sp, dp;
   msg_srcdst_pos<SPEC>(w, sp, dp);
   uint32_t s = (w >> sp) & 7u, d = (w >> dp) & 7u;
-  uint32_t w2 = (w & ~((7u << sp) | (7u << dp))) | ((uint32_t)perm_of(P, (int)s) << sp) | ((uint32_t)perm_of(P, (int)d) << dp);
+  uint32_t w2 = (SPEC == KRAFT ? kr_body(w, sp, dp) : (w & ~((7u << sp) | (7u << dp)))) |
+                ((uint32_t)perm_of(P, (int)s) << sp) | ((uint32_t)perm_of(P, (int)d) << dp);
   return mix64((uint64_t)w2 * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
 }
 RMC_HD uint64_t h_acked_view(uint32_t hdr) {  // PullRaft's view includes acked (PullRaft.tla:123)
@@ -1247,7 +1723,7 @@ template <int SPEC>
 RMC_HD uint32_t msg_rest(uint32_t w) {  // the message with msource/mdest masked out
   int sp, dp;
   msg_srcdst_pos<SPEC>(w, sp, dp);
-  return w & ~((7u << sp) | (7u << dp));
+  return SPEC == KRAFT ? kr_body(w, sp, dp) : w & ~((7u << sp) | (7u << dp));
 }
 template <int SPEC, int N>
 RMC_HD uint32_t server_sig_own(int i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -1256,6 +1732,15 @@ RMC_HD uint32_t server_sig_own(int i, uint32_t a, uint32_t b, uint32_t c, uint32
   uint32_t votes = (uint32_t)a_votes(a), pend = (uint32_t)a_pending(a);
   uint32_t x = (a & 0x0003FE3Fu);  // term | state | Len | commitIndex | fsyncIndex
   x ^= vcls << 6;
+  if (SPEC == KRAFT) {  // votedFor (bits 15-17) by class; state bit 25; pendingFetch's mdest by class
+    const int v2 = a_votedfor2(a);
+    x = (x & ~(7u << 15)) | ((v2 == NILS ? 0u : (v2 == i ? 1u : 2u)) << 15);
+    x ^= ((a >> 25) & 1u) << 26;
+    if (c & 1u) c = setb(c, 7, 3, getb(c, 7, 3) == (uint32_t)a_voted(a) ? 1u : 2u);
+    votes = 0;
+    pend = 0;
+    x ^= ((uint32_t)popc7((uint32_t)a_votes(a)) << 18) | (((uint32_t)(a_votes(a) >> i) & 1u) << 21);
+  }
   if (SPEC == PULL2) {  // bits 15-17 are votedFor: its class, not its value
     const int v2 = a_votedfor2(a);
     x = (x & ~(7u << 15)) | ((v2 == NILS ? 0u : (v2 == i ? 1u : 2u)) << 15);
@@ -1270,7 +1755,7 @@ RMC_HD uint32_t server_sig_own(int i, uint32_t a, uint32_t b, uint32_t c, uint32
        (((pend >> i) & 1u) << 25);
   uint32_t h = mix32(x + 0x9E3779B9u);
   h = mix32(h ^ b);
-  h = mix32(h ^ (SPEC == PULL2 ? c : row_multiset(c, N, i) + 0x85EBCA6Bu * (((c >> (3 * i)) & 7u) + 1u)));
+  h = mix32(h ^ ((SPEC == PULL2 || SPEC == KRAFT) ? c : row_multiset(c, N, i) + 0x85EBCA6Bu * (((c >> (3 * i)) & 7u) + 1u)));
   h = mix32(h ^ (row_multiset(d, N, i) + 0xC2B2AE35u * (((d >> (3 * i)) & 7u) + 1u)));
   return h;
 }
@@ -1281,7 +1766,7 @@ RMC_HD void msg_sig(uint32_t w, int& src, int& dst, uint32_t& hs, uint32_t& hd) 
   msg_srcdst_pos<SPEC>(w, sp, dp);
   src = (int)((w >> sp) & 7u);
   dst = (int)((w >> dp) & 7u);
-  uint32_t r = w & ~((7u << sp) | (7u << dp));
+  uint32_t r = SPEC == KRAFT ? kr_body(w, sp, dp) : w & ~((7u << sp) | (7u << dp));
   hs = mix32(r ^ 0x27d4eb2fU);
   hd = mix32(r ^ 0x165667b1U);
 }
@@ -1319,7 +1804,8 @@ RMC_HD uint64_t msg_u(uint32_t w, int& src, int& dst) {
   msg_srcdst_pos<SPEC>(w, sp, dp);
   src = (int)((w >> sp) & 7u);
   dst = (int)((w >> dp) & 7u);
-  return mix64((uint64_t)(w & ~((7u << sp) | (7u << dp))) * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
+  const uint32_t body = SPEC == KRAFT ? kr_body(w, sp, dp) : w & ~((7u << sp) | (7u << dp));
+  return mix64((uint64_t)body * 0xD6E8FEB86659FD93ULL + 0xA0761D6478BD642FULL);
 }
 template <int SPEC, int N>
 RMC_HD void msg_contrib(uint32_t w, bool neg, uint32_t (&sig)[N], uint64_t (&S)[N][N]) {
@@ -1382,7 +1868,7 @@ RMC_HD uint64_t canon_from_sums(const Model& M, const DeltaView<SPEC, N>& V, con
   bool ties;
   const uint32_t P0 = sig_perm<N>(sig, ties);
   if (P0_out) *P0_out = ties ? 0xFFFFFFFFu : P0;
-  const uint64_t aux = SPEC == PULL ? h_acked_view(V.d.hdr) : 0ULL;
+  const uint64_t aux = (SPEC == PULL || SPEC == KRAFT) ? h_acked_view(V.d.hdr) : 0ULL;  // KRaft.tla:154
   uint64_t best = ~0ULL;
   const int np = ties ? M.nperm : 1;
 #if defined(RMC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
@@ -1493,7 +1979,8 @@ template <int SPEC>
 RMC_HD uint64_t msg_u2(uint32_t w) {  // the second word's hash of a message body (servers masked)
   int sp, dp;
   msg_srcdst_pos<SPEC>(w, sp, dp);
-  return mix64b((uint64_t)(w & ~((7u << sp) | (7u << dp))) * 0x9FB21C651E98DF25ULL + 0x2545F4914F6CDD1DULL);
+  const uint32_t body = SPEC == KRAFT ? kr_body(w, sp, dp) : w & ~((7u << sp) | (7u << dp));
+  return mix64b((uint64_t)body * 0x9FB21C651E98DF25ULL + 0x2545F4914F6CDD1DULL);
 }
 template <int SPEC, int N>
 RMC_HD uint64_t h_server2(uint32_t P, int i, uint32_t a, uint32_t b, uint32_t c, uint32_t dd) {
@@ -1528,8 +2015,9 @@ RMC_HD Fp128 canon_from_sums2(const Model& M, const DeltaView<SPEC, N>& V, const
                               const uint64_t (&S)[N][N], const uint64_t (&S2)[N][N]) {
   bool ties;
   const uint32_t P0 = sig_perm<N>(sig, ties);
-  const uint64_t aux = SPEC == PULL ? h_acked_view(V.d.hdr) : 0ULL;
-  const uint64_t aux2 = SPEC == PULL ? mix64b(((uint64_t)(V.d.hdr >> 16) & 0xFFu) + 0x8CB92BA72F3D8DD7ULL) : 0ULL;
+  const uint64_t aux = (SPEC == PULL || SPEC == KRAFT) ? h_acked_view(V.d.hdr) : 0ULL;
+  const uint64_t aux2 =
+      (SPEC == PULL || SPEC == KRAFT) ? mix64b(((uint64_t)(V.d.hdr >> 16) & 0xFFu) + 0x8CB92BA72F3D8DD7ULL) : 0ULL;
   Fp128 best{~0ULL, ~0ULL};
   const int np = ties ? M.nperm : 1;
 #pragma unroll 1

@@ -91,6 +91,7 @@ def lib():
     L.rmc_selftest_random_trace.argtypes = [P, ctypes.c_uint64, c_int]
     L.rmc_selftest_set_hint_kmax.argtypes = [P, ctypes.c_uint32]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
+    L.rmc_selftest_encode_kmsg.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
     _lib = L
     return L
 
@@ -281,4 +282,15 @@ def encode_msg(spec, **f):
     arr = (ctypes.c_int * 19)(*[int(f.get(n, 0)) for n in names])
     out = ctypes.c_uint32()
     ok = lib().rmc_selftest_encode_msg(spec, arr, ctypes.byref(out))
+    return out.value, ok == 0
+
+
+def encode_kmsg(**f):
+    """TEST HOOK: the packed word of a KRaft record (rmc_spec.h kr_encode) + codec self-consistency flag."""
+    names = ["cls", "dst", "src", "epoch", "err", "leader", "granted", "f1", "f2", "cepoch", "cfo", "clfe",
+             "elen", "eepoch", "evalue", "hwm", "divend", "divepoch", "count"]
+    defaults = dict(err=1, leader=-1)
+    arr = (ctypes.c_int * 19)(*[int(f.get(n, defaults.get(n, 0))) for n in names])
+    out = ctypes.c_uint32()
+    ok = lib().rmc_selftest_encode_kmsg(arr, ctypes.byref(out))
     return out.value, ok == 0

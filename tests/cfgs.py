@@ -114,3 +114,38 @@ VARIANT2_MEDIUM = [
 VARIANT2_N5 = [
     ("pull2_n5v1e1", dict(n=5, v=1, E=1), 400000, 3000),
 ]
+
+
+def kraft_cfg_text(n=3, v=1, E=2, R=0, inv=("LeaderHasAllAckedValues", "NoLogDivergence",
+                                            "NeverTwoLeadersInSameEpoch", "NoIllegalState")):
+    """A cfg in KRaft.cfg's shape (pull-raft/KRaft.cfg:5-50): its model values
+    and invariants, with the given bounds."""
+    lines = ["CONSTANTS"]
+    lines += ["    n%d = n%d" % (i, i) for i in range(1, n + 1)]
+    lines += ["    v%d = v%d" % (i, i) for i in range(1, v + 1)]
+    lines.append("    Server = {%s}" % ", ".join("n%d" % i for i in range(1, n + 1)))
+    lines.append("    Value = {%s}" % ", ".join("v%d" % i for i in range(1, v + 1)))
+    for k in ("Follower", "Candidate", "Leader", "Unattached", "Voted", "Nil", "RequestVoteRequest",
+              "RequestVoteResponse", "BeginQuorumRequest", "BeginQuorumResponse", "EndQuorumRequest",
+              "FetchRequest", "FetchResponse", "Ok", "NotOk", "Diverging", "FencedLeaderEpoch", "NotLeader",
+              "UnknownLeader", "IllegalState", "EqualEpoch", "AnyEpoch"):
+        lines.append("    %s = %s" % (k, k))
+    lines.append("    MaxElections = %d" % E)
+    lines.append("    MaxRestarts = %d" % R)
+    lines += ["INIT Init", "NEXT Next", "VIEW view", "SYMMETRY symmServers", "INVARIANT"]
+    lines += list(inv)
+    return "\n".join(lines) + "\n"
+
+
+# KRaft (pull-raft/KRaft.tla, SURVEY 8f rank 3): (name, kwargs); the Python
+# oracle (oracle/pyoracle/kraft.py) pins them
+KRAFT = [
+    ("kraft_n2v1e1", dict(n=2, v=1, E=1)),
+    ("kraft_n2v1e2", dict(n=2, v=1, E=2)),
+    ("kraft_n3v1e1", dict(n=3, v=1, E=1)),
+    ("kraft_n2v2e2", dict(n=2, v=2, E=2)),
+    ("kraft_n2v1e2r1", dict(n=2, v=1, E=2, R=1)),
+    ("kraft_n3v1e1r1", dict(n=3, v=1, E=1, R=1)),
+    ("kraft_n2v2e1r1", dict(n=2, v=2, E=1, R=1)),
+    ("kraft_n3v2e1", dict(n=3, v=2, E=1)),
+]

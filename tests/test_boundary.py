@@ -15,7 +15,7 @@ import raftmc
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = "/root/reference/specifications"
 SPECS = {"Raft": "standard-raft", "FlexibleRaft": "flexible-raft", "PullRaft": "pull-raft",
-         "RaftFsync": "raft-and-fsync", "PullRaftVariant2": "pull-raft"}
+         "RaftFsync": "raft-and-fsync", "PullRaftVariant2": "pull-raft", "KRaft": "pull-raft"}
 SHIPPED = json.load(open(os.path.join(HERE, "golden", "shipped.json")))
 
 pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference not mounted")

@@ -1,0 +1,72 @@
+"""GPU: KRaft (pull-raft/KRaft.tla) through the C ABI
+against the oracle fixtures (tests/golden/kraft.json): every per-level count,
+the counts and invariant at a violation (IllegalState with restarts), over
+chunk sizes, 128-bit fingerprints and the fingerprint-sharded protocol; the
+shipped cfg's constants against the oracle's first levels and the CPU engine."""
+import json
+import os
+
+import pytest
+
+import raftmc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+KR = json.load(open(os.path.join(HERE, "golden", "kraft.json")))
+FULL = sorted(k for k in KR if KR[k]["status"] != "truncated")
+
+pytestmark = pytest.mark.gpu
+
+
+def same(r, g):
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == \
+        (g["generated"], g["distinct"], g["depth"], g["status"])
+    if g["status"] == "ok":
+        assert r["levels"] == g["levels"]
+        assert r["hidden_var_collisions"] == g["hidden_same_level"]
+    else:
+        assert r["violated"] == g["violated"]
+
+
+@pytest.mark.parametrize("name", FULL)
+@pytest.mark.parametrize("chunk", [0, 7, 1000])
+def test_kraft_matches_oracle(name, chunk):
+    g = KR[name]
+    same(raftmc.check_text("KRaft", g["cfg"], chunk_parents=chunk), g)
+
+
+@pytest.mark.parametrize("name", ["kraft_n3v2e1", "kraft_n2v2e2"])
+def test_kraft_fp128(name):
+    g = KR[name]
+    same(raftmc.check_text("KRaft", g["cfg"], fp_bits=128), g)
+
+
+@pytest.mark.parametrize("name", ["kraft_n3v2e1", "kraft_n3v1e1r1"])
+@pytest.mark.parametrize("shards,chunk", [(2, 0), (3, 55)])
+def test_kraft_logical_shards(name, shards, chunk):
+    g = KR[name]
+    same(raftmc.Model(module="KRaft", cfg_text=g["cfg"]).check_logical(shards, chunk_parents=chunk), g)
+
+
+def test_kraft_violation_trace():
+    """The IllegalState behaviour is rebuilt and ends in the violating state."""
+    g = KR["kraft_n2v1e2r1"]
+    m = raftmc.Model(module="KRaft", cfg_text=g["cfg"])
+    r = m.check()
+    assert r["status"] == "violation" and r["violated"] == "NoIllegalState"
+    tr = m.trace()
+    assert len(tr) == g["trace_len"]
+    assert "IllegalState" in tr[-1][1]
+
+
+def test_kraft_shipped_cfg():
+    """KRaft.cfg's constants: the oracle's first levels, and GPU == CPU engine
+    on the whole state space."""
+    g = KR["KRaft_cfg_prefix"]
+    m = raftmc.Model(os.path.join(ROOT, "configs", "KRaft.tla"), os.path.join(ROOT, "configs", "KRaft.cfg"))
+    r = m.check()
+    n = len(g["levels"])
+    assert r["levels"][:n] == g["levels"]
+    c = m.check_cpu(workers=16)
+    assert (r["generated"], r["distinct"], r["depth"], r["status"], r["levels"]) == \
+        (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"])

@@ -10,7 +10,7 @@ import sys
 
 SPECS = {"Raft": "standard-raft/Raft.tla", "FlexibleRaft": "flexible-raft/FlexibleRaft.tla",
          "PullRaft": "pull-raft/PullRaft.tla", "RaftFsync": "raft-and-fsync/RaftFsync.tla",
-         "PullRaftVariant2": "pull-raft/PullRaftVariant2.tla"}
+         "PullRaftVariant2": "pull-raft/PullRaftVariant2.tla", "KRaft": "pull-raft/KRaft.tla"}
 
 
 def normalise(t):
