@@ -45,7 +45,12 @@ def test_kraft_fp128(name):
 @pytest.mark.parametrize("shards,chunk", [(2, 0), (3, 55)])
 def test_kraft_logical_shards(name, shards, chunk):
     g = KR[name]
-    same(raftmc.Model(module="KRaft", cfg_text=g["cfg"]).check_logical(shards, chunk_parents=chunk), g)
+    r = raftmc.Model(module="KRaft", cfg_text=g["cfg"]).check_logical(shards, chunk_parents=chunk)
+    if g["status"] == "ok":
+        same(r, g)
+    else:  # the sharded protocol stops at the violating round: TLC's trace, not its counts at the stop
+        assert r["status"] == "violation" and r["violated"] == g["violated"]
+        assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]
 
 
 def test_kraft_violation_trace():
@@ -60,8 +65,9 @@ def test_kraft_violation_trace():
 
 
 def test_kraft_shipped_cfg():
-    """KRaft.cfg's constants: the oracle's first levels, and GPU == CPU engine
-    on the whole state space."""
+    """KRaft.cfg's constants (19,841,847 distinct, 57,806,118 generated, depth
+    52): the oracle's first levels, and GPU == CPU engine on the whole state
+    space."""
     g = KR["KRaft_cfg_prefix"]
     m = raftmc.Model(os.path.join(ROOT, "configs", "KRaft.tla"), os.path.join(ROOT, "configs", "KRaft.cfg"))
     r = m.check()
