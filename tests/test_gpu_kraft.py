@@ -76,3 +76,26 @@ def test_kraft_shipped_cfg():
     c = m.check_cpu(workers=16)
     assert (r["generated"], r["distinct"], r["depth"], r["status"], r["levels"]) == \
         (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"])
+
+
+def test_kraft_simulation():
+    """TLC -simulate on KRaft: restarts reach IllegalState (the replayed behaviour
+    ends there); KRaft.cfg's constants (safe: exhausted above) find nothing."""
+    g = KR["kraft_n3v1e1r1"]
+    r = raftmc.Model(module="KRaft", cfg_text=g["cfg"]).simulate(walkers=1 << 14, depth=60, seed=3,
+                                                                behaviors=1 << 20, seconds=60)
+    assert r["status"] == "violation" and r["violated"] == "NoIllegalState"
+    assert r["trace"][0][0] == "Initial predicate" and len(r["trace"]) >= g["trace_len"]
+    assert "IllegalState" in r["trace"][-1][1]
+    s = raftmc.Model(os.path.join(ROOT, "configs", "KRaft.tla"), os.path.join(ROOT, "configs", "KRaft.cfg")).simulate(
+        walkers=1 << 14, depth=80, seed=5, behaviors=1 << 18)
+    assert s["status"] == "ok" and s["behaviors"] == 1 << 18
+
+
+def test_kraft_dump_trace_module():
+    """TLC -dumpTrace tla: the IllegalState behaviour as a module over KRaft's variables."""
+    g = KR["kraft_n2v1e2r1"]
+    m = raftmc.Model(module="KRaft", cfg_text=g["cfg"])
+    m.check()
+    tla, cfg = m.trace_module("KRaftTrace")
+    assert "EXTENDS KRaft" in tla and "pendingFetch |->" in tla and "IllegalState" in tla
