@@ -4,8 +4,8 @@ tests/golden/make_kraft.py), the lowered actions replayed on the host
 (rmc_spec.h kr_*, the code the kernels run), the CPU engine (same layout and
 first-in-TLC-order rule as the GPU path) and the packed record order.
 
-Parity: pinned by the Python oracle alone (the C oracle does not restate
-KRaft); the lowering is an independent restatement of the same spec."""
+Parity: pinned by two independent restatements, the Python oracle and the
+C++ oracle (oracle/cengine/kraft_oracle.cpp); the lowering is a third."""
 import json
 import os
 
@@ -153,3 +153,15 @@ def test_kraft_packed_order_is_tlc_order():
     by_tlc = sorted(recs, key=tlc_key)
     words = [recs[r] for r in by_tlc]
     assert words == sorted(words) and len(set(words)) == len(words)
+
+
+@pytest.mark.parametrize("name", sorted(KR))
+def test_c_oracle_reproduces_fixture(name):
+    """The independent C++ restatement (oracle/cengine/kraft_oracle.cpp) agrees."""
+    from oracle import run_c
+    g = KR[name]
+    cfg = parse_cfg(g["cfg"])
+    c = run_c.run_kraft(cfg["constants"], cfg["invariants"], max_states=g.get("max_states", 0))
+    assert (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"], c["hidden_same_level"],
+            c["action_counts"]) == (g["generated"], g["distinct"], g["depth"], g["status"], g["levels"],
+                                    g["hidden_same_level"], g["action_counts"])
