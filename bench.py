@@ -41,6 +41,10 @@ WORKLOADS = {
                     "standard-raft: 3 servers, Value={v1}, MaxElections=3 (terms <= 4), MaxRestarts=0"),
     "raft_n3v2e3": ("Raft", "configs/Raft_n3v2e3.cfg", "2",
                     "standard-raft: 3 servers, Value={v1,v2}, MaxElections=3 (terms <= 4), MaxRestarts=0"),
+    "kraft_cfg": ("KRaft", "configs/KRaft.cfg", "SURVEY 8f rank 3 (KRaft)",
+                  "KRaft.cfg (pull-raft/KRaft.cfg): 3 servers, Value={v1}, MaxElections=2, MaxRestarts=0"),
+    "kraft_n3v2e2": ("KRaft", "configs/KRaft_n3v2e2.cfg", "SURVEY 8f rank 3 (KRaft)",
+                     "KRaft: 3 servers, Value={v1,v2}, MaxElections=2, MaxRestarts=0"),
 }
 DEFAULT_WORKLOAD = "raft_n3v2e2"
 HBM_PEAK = 8.0e12  # MI355X HBM3E, bytes/s (MI355X_MICROARCH.md chip table)
@@ -183,7 +187,8 @@ def main():
                       "frac": ach / HBM_PEAK, "traffic": kpmc.get(name)}
     if rank == 0:
         line = {
-            "metric": "distinct states/sec + time-to-exhaust, standard-raft",
+            "metric": "distinct states/sec + time-to-exhaust, " +
+                      {"Raft": "standard-raft", "KRaft": "KRaft"}.get(module, module),
             "value": value,
             "unit": "distinct states/s",
             "n_gpus": world,
