@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol():
 
 def test_load_errors_are_reported():
     with pytest.raises(raftmc.RaftmcError, match="unsupported module"):
-        raftmc.Model(module="KRaft", cfg_text="CONSTANTS\n")
+        raftmc.Model(module="KRaftWithReconfig", cfg_text="CONSTANTS\n")
     with pytest.raises(raftmc.RaftmcError, match="MaxElections"):
         raftmc.Model(module="Raft", cfg_text="CONSTANTS Server = {n1, n2} Value = {v1}\nINIT Init NEXT Next VIEW view")
     with pytest.raises(raftmc.RaftmcError, match="cfg"):
