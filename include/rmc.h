@@ -119,6 +119,13 @@ int rmc_comm_unique_id(unsigned char* id128);
 int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, int device, const unsigned char* id128,
                       rmc_result* out);
 int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result* out);
+/* The same multi-process protocol as rmc_check_sharded with POSIX shared
+ * memory (segment `shm_name`, created by the ranks) as the transport instead
+ * of RCCL: one process per shard on one host, any GPUs -- including several
+ * processes on ONE GPU, which RCCL refuses.  For testing the multi-rank path
+ * and for hosts without xGMI peers; world <= 16. */
+int rmc_check_sharded_shm(rmc_model* m, const rmc_options* o, int rank, int world, int device, const char* shm_name,
+                          rmc_result* out);
 /* TLC's random simulation mode (-simulate): rounds of `walkers` random
  * behaviours in parallel on the GPU, each from Init for at most `depth` steps
  * (a uniformly random enabled successor per step), invariants checked on every

@@ -32,6 +32,9 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <rccl/rccl.h>
 #include "rmc_internal.h"
 #include "rmc_fpset.h"
@@ -122,6 +125,120 @@ struct RcclComm : Comm {
       }
     }
     NCCLCHK(ncclGroupEnd());
+  }
+};
+
+// One shard per process, host shared memory as the transport: the same
+// multi-process protocol as RcclComm (rank-local shards, allgathered counts,
+// point-to-point transfers) where RCCL cannot run, e.g. several processes on
+// one GPU (RCCL refuses two ranks per device).  Transfers are staged through
+// per-(source, destination) slots of a POSIX shared-memory segment, in rounds
+// of the slot size, with a process-shared barrier between the write and read
+// halves of every round.
+struct ShmComm : Comm {
+  struct Hdr {
+    int ready;
+    int count;  // arrivals at the current barrier
+    int sense;  // flips when the last rank arrives
+  };
+  static constexpr size_t SLOT = 8u << 20;   // bytes per (src, dst) slot and round
+  static constexpr int GATHER_MAX = 64;      // values per rank in one allgather
+  std::string name;
+  int rank = 0;
+  size_t bytes = 0;
+  unsigned char* base = nullptr;
+  Hdr* hdr() { return reinterpret_cast<Hdr*>(base); }
+  uint64_t* gather() { return reinterpret_cast<uint64_t*>(base + 256); }
+  unsigned char* slot(int src, int dst) {
+    return base + 256 + (size_t)world * GATHER_MAX * 8 + ((size_t)src * world + dst) * SLOT;
+  }
+  ShmComm(int r, int W, const std::string& nm, hipStream_t s) : name(nm), rank(r) {
+    world = W;
+    local = {r};
+    stream = s;
+    bytes = 256 + (size_t)W * GATHER_MAX * 8 + (size_t)W * W * SLOT;
+    int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+    if (fd < 0) throw std::runtime_error("shm_open " + name + " failed");
+    if (ftruncate(fd, (off_t)bytes) != 0) { close(fd); throw std::runtime_error("ftruncate of the shm segment failed"); }
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw std::runtime_error("mmap of the shm segment failed");
+    base = (unsigned char*)p;
+    if (rank == 0) {
+      __atomic_store_n(&hdr()->count, 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&hdr()->sense, 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&hdr()->ready, 1, __ATOMIC_RELEASE);
+    } else {
+      for (int t = 0; !__atomic_load_n(&hdr()->ready, __ATOMIC_ACQUIRE); t++) {
+        if (t > 600000) throw std::runtime_error("shm transport: rank 0 never initialised " + name);
+        usleep(100);
+      }
+    }
+    barrier();
+  }
+  ~ShmComm() override {
+    if (!base) return;
+    try { barrier(); } catch (...) {}
+    munmap(base, bytes);
+    if (rank == 0) shm_unlink(name.c_str());
+  }
+  // sense-reversing barrier in the segment; a rank that waits 120 s (a peer
+  // failed or died) throws instead of hanging
+  int my_sense = 0;
+  bool dead = false;
+  void barrier() {
+    if (dead) return;
+    my_sense ^= 1;
+    if (__atomic_add_fetch(&hdr()->count, 1, __ATOMIC_ACQ_REL) == world) {
+      __atomic_store_n(&hdr()->count, 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&hdr()->sense, my_sense, __ATOMIC_RELEASE);
+      return;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    for (long k = 0; __atomic_load_n(&hdr()->sense, __ATOMIC_ACQUIRE) != my_sense; k++) {
+      if (k > 1000) usleep(50);
+      if ((k & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+        dead = true;
+        throw std::runtime_error("shm transport: a peer rank did not arrive within 120 s");
+      }
+    }
+  }
+  void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) override {
+    if (k > GATHER_MAX) throw std::runtime_error("shm transport: allgather too wide");
+    memcpy(gather() + (size_t)rank * k, in[0].data(), (size_t)k * 8);
+    barrier();
+    out.assign(gather(), gather() + (size_t)world * k);
+    barrier();
+  }
+  // x is the round's global transfer list, identical on every rank (the
+  // protocol builds it from allgathered counts), so every rank walks the same
+  // transfers and rounds: each transfer goes through its pair's slot in
+  // SLOT-sized pieces.  Copies go on the check's stream and are waited for
+  // before each barrier (a pageable host-to-device copy may return before its
+  // DMA lands, and the stream does not order with the null stream).
+  void alltoallv(const std::vector<Xfer>& x) override {
+    HIPCHK(hipStreamSynchronize(stream));  // the send buffers are ready
+    for (auto& t : x) {
+      if (!t.bytes || (t.src == t.dst)) {
+        if (t.bytes && t.src == rank)
+          HIPCHK(hipMemcpyAsync(t.rbuf, t.sbuf, t.bytes, hipMemcpyDeviceToDevice, stream));
+        continue;
+      }
+      for (size_t off = 0; off < t.bytes; off += SLOT) {
+        const size_t n = std::min(SLOT, t.bytes - off);
+        if (t.src == rank) {
+          HIPCHK(hipMemcpyAsync(slot(t.src, t.dst), (const char*)t.sbuf + off, n, hipMemcpyDeviceToHost, stream));
+          HIPCHK(hipStreamSynchronize(stream));
+        }
+        barrier();
+        if (t.dst == rank) {
+          HIPCHK(hipMemcpyAsync((char*)t.rbuf + off, slot(t.src, t.dst), n, hipMemcpyHostToDevice, stream));
+          HIPCHK(hipStreamSynchronize(stream));
+        }
+        barrier();
+      }
+    }
+    HIPCHK(hipStreamSynchronize(stream));
   }
 };
 
@@ -834,6 +951,38 @@ int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, i
       comm = c;
     }
     return run_with_regrow(m, o, *comm, out);
+  } catch (std::exception& e) {
+    set_last_error(e.what());
+    return -5;
+  }
+}
+
+int rmc_check_sharded_shm(rmc_model* m, const rmc_options* o, int rank, int world, int device, const char* shm_name,
+                          rmc_result* out) {
+  if (!m || !out || !shm_name || world < 1 || world > 16 || rank < 0 || rank >= world) {
+    set_last_error("bad argument");
+    return -1;
+  }
+  rmc_options def;
+  rmc_options_default(&def);
+  if (!o) o = &def;
+  memset(out, 0, sizeof *out);
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+      set_last_error("no HIP device available: the raftmc GPU path requires an MI355X (gfx950)");
+      return -4;
+    }
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int rc;
+    {
+      ShmComm comm(rank, world, std::string("/") + shm_name, s);
+      rc = run_with_regrow(m, o, comm, out);
+    }
+    HIPCHK(hipStreamDestroy(s));
+    return rc;
   } catch (std::exception& e) {
     set_last_error(e.what());
     return -5;

@@ -51,7 +51,7 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
-           "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu"]
+           "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm"]
 
 _lib = None
 
@@ -81,6 +81,8 @@ def lib():
     L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                     ctypes.POINTER(Result)]
     L.rmc_check_logical.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(Result)]
+    L.rmc_check_sharded_shm.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
+                                        ctypes.POINTER(Result)]
     L.rmc_check_cpu.argtypes = [P, ctypes.POINTER(Options), ctypes.POINTER(Result)]
     L.rmc_simulate.argtypes = [P, ctypes.POINTER(Options), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                ctypes.c_uint64, ctypes.c_double, ctypes.POINTER(Result)]
@@ -179,6 +181,14 @@ class Model:
         o, r = self._options(**kw), Result()
         rc = lib().rmc_check_sharded(self._h, ctypes.byref(o), int(rank), int(world), int(device),
                                      bytes(unique_id), ctypes.byref(r))
+        return self._result(rc, r)
+
+    def check_sharded_shm(self, rank, world, device, shm_name, **kw):
+        """One shard of a multi-process check with shared memory as the transport
+        (several processes may share one GPU; see rmc_check_sharded_shm)."""
+        o, r = self._options(**kw), Result()
+        rc = lib().rmc_check_sharded_shm(self._h, ctypes.byref(o), int(rank), int(world), int(device),
+                                         shm_name.encode(), ctypes.byref(r))
         return self._result(rc, r)
 
     def simulate(self, walkers=1 << 16, depth=100, seed=0, behaviors=None, seconds=0.0, **kw):

@@ -1,0 +1,22 @@
+"""One rank of a multi-process fingerprint-sharded check over the shared-memory
+transport (rmc_check_sharded_shm); launched by tests/test_gpu_sharded_mp.py.
+argv: rank world shm_name fixture_file fixture_name chunk -> prints one JSON line."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "raft-tlaplus_amd"))
+import raftmc  # noqa: E402
+
+rank, world, name, fx, key, chunk = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5], sys.argv[6]
+g = json.load(open(os.path.join(HERE, "golden", fx)))[key]
+m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+try:
+    r = m.check_sharded_shm(int(rank), int(world), 0, name, chunk_parents=int(chunk))
+except raftmc.RaftmcError as e:
+    print(json.dumps(dict(rank=int(rank), error=str(e))), flush=True)
+    sys.exit(3)
+r.pop("trace", None)
+print(json.dumps(dict(rank=int(rank), **{k: r[k] for k in ("generated", "distinct", "depth", "status", "violated",
+                                                             "levels", "hidden_var_collisions")})), flush=True)

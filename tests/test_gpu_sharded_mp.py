@@ -1,0 +1,58 @@
+"""GPU: the fingerprint-sharded protocol (raft-tlaplus_amd/csrc/rmc_sharded.cpp)
+run by SEVERAL PROCESSES, one shard each, as on a multi-GPU node -- here all on
+one GPU, with shared memory as the transport (rmc_check_sharded_shm) because
+RCCL refuses two ranks per device.  Every rank must report the oracle's global
+result.  (The gloo test, tests/test_sharded_gloo.py, runs a Python restatement
+of the protocol; this runs the product's own C++.)"""
+import json
+import os
+import subprocess
+import sys
+import uuid
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(world, fx, key, chunk=0):
+    name = "rmc_test_" + uuid.uuid4().hex[:12]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "sharded_shm_rank.py"), str(r), str(world), name,
+                               fx, key, str(chunk)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            tails = [q.communicate()[1][-1500:] for q in procs]
+            raise AssertionError("ranks hung; stderr tails:\n" + "\n----\n".join(tails))
+        assert p.returncode == 0, e[-2000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    return outs
+
+
+@pytest.mark.parametrize("world,fx,key,chunk", [
+    (2, "small.json", "raft_n3v1e1", 0),
+    (3, "small.json", "pull_n3v2e1", 97),
+    (2, "variant2.json", "pull2_n3v2e1", 0),
+    (4, "kraft.json", "kraft_n3v2e1", 1000),
+    (2, "small.json", "raft_n2v2e2", 7),
+    (5, "small.json", "raft_n3v1e1", 33),
+])
+def test_multiprocess_shards_match_oracle(world, fx, key, chunk):
+    g = json.load(open(os.path.join(HERE, "golden", fx)))[key]
+    for r in run_ranks(world, fx, key, chunk):
+        assert (r["generated"], r["distinct"], r["depth"], r["status"]) == \
+            (g["generated"], g["distinct"], g["depth"], g["status"])
+        assert r["levels"] == g["levels"]
+        assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+def test_multiprocess_shards_violation():
+    g = json.load(open(os.path.join(HERE, "golden", "kraft.json")))["kraft_n3v1e1r1"]
+    for r in run_ranks(2, "kraft.json", "kraft_n3v1e1r1"):
+        assert r["status"] == "violation" and r["violated"] == g["violated"] and r["depth"] == g["depth"]
