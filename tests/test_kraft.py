@@ -165,3 +165,19 @@ def test_c_oracle_reproduces_fixture(name):
     assert (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"], c["hidden_same_level"],
             c["action_counts"]) == (g["generated"], g["distinct"], g["depth"], g["status"], g["levels"],
                                     g["hidden_same_level"], g["action_counts"])
+
+
+def test_kraft_hand_derived_first_levels():
+    """Known answers derived by hand from KRaft.tla for KRaft.cfg's constants
+    (N=3, V={v1}, MaxElections=2), independent of every restatement:
+    level 1 = Init (:397-415), 1 state.
+    level 2: only RequestVote(i) is enabled (all Unattached, :441; no messages,
+      no leader): 3 successors, one orbit under symmServers -> [3, 1].
+    level 3, from n1 Candidate at epoch 2 with RVReqs to n2, n3: RequestVote(n1)
+      again (Candidate, electionCtr 1 < 2), RequestVote(n2), RequestVote(n3),
+      HandleRequestVoteRequest on each RVReq (epoch 2 > 1: Unattached -> Voted,
+      grant) -> 5 successors; n2/n3 are symmetric, so 3 distinct -> [5, 3]."""
+    g = KR["KRaft_cfg_prefix"]
+    assert g["levels"][:3] == [[1, 1], [3, 1], [5, 3]]
+    r = raftmc.Model(module="KRaft", cfg_text=g["cfg"]).selftest_host_bfs(max_distinct=5)
+    assert r["levels"][:3] == [[1, 1], [3, 1], [5, 3]]
