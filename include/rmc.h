@@ -19,6 +19,8 @@
  *                       (State k: /\ var = value) after an invariant violation
  *                       (invariants Raft.tla:588-620, listed at Raft.cfg:34-36)
  *   rmc_model_free   <- end of run
+ * Modules: Raft, FlexibleRaft, RaftFsync, PullRaft, PullRaftVariant2 and KRaft
+ * (specifications/pull-raft/KRaft.tla, e.g. with pull-raft/KRaft.cfg:5-50).
  * Plain pointers and sizes only; no torch or HIP types cross this boundary.
  *
  * Ownership: the caller owns rmc_options, rmc_result and text buffers; the
