@@ -11,7 +11,11 @@ import raftmc  # noqa: E402
 
 rank, world, name, fx, key, chunk = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5], sys.argv[6]
 g = json.load(open(os.path.join(HERE, "golden", fx)))[key]
-m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+if "cfg" in g:
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+else:  # shipped.json: the restated reference cfg under configs/
+    root = os.path.dirname(HERE)
+    m = raftmc.Model(os.path.join(root, "configs", g["module"] + ".tla"), os.path.join(root, g["cfg_path"]))
 try:
     r = m.check_sharded_shm(int(rank), int(world), 0, name, chunk_parents=int(chunk))
 except raftmc.RaftmcError as e:

@@ -42,6 +42,8 @@ def run_ranks(world, fx, key, chunk=0):
     (4, "kraft.json", "kraft_n3v2e1", 1000),
     (2, "small.json", "raft_n2v2e2", 7),
     (5, "small.json", "raft_n3v1e1", 33),
+    (2, "shipped.json", "Raft_cfg", 100000),   # Raft.cfg: 8,664,032 distinct, levels of up to 10 rounds
+    (3, "shipped.json", "PullRaftVariant2_cfg", 0),  # 891 same-level hidden-variable collisions
 ])
 def test_multiprocess_shards_match_oracle(world, fx, key, chunk):
     g = json.load(open(os.path.join(HERE, "golden", fx)))[key]
