@@ -553,6 +553,90 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
   if (coll) atomicAdd(&st->hidden_coll, (unsigned long long)coll);
 }
 
+// The same marking, a wave per k_expand tile (64 parents): a tile's
+// candidates are one contiguous range, so the wave reads them coalesced, 64
+// at a time, and ranks the winners inside each parent's segment with ballots
+// (the parents' running counts carried in LDS from one 64-candidate step to
+// the next).  The table reads stay random (only candidates k_expand did not
+// already find in an earlier level).
+#ifndef RMC_MARK_WPB
+#define RMC_MARK_WPB 4
+#endif
+constexpr int MARK_WPB = RMC_MARK_WPB;  // waves (tiles) per k_mark_tiles block
+__global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long long nparents, unsigned long long pbase,
+                                                    unsigned long long floor, int ew,
+                                                    const unsigned long long* __restrict__ table,
+                                                    const unsigned long long* __restrict__ cand_slot,
+                                                    const uint32_t* __restrict__ cand_ob,
+                                                    const uint32_t* __restrict__ par_off,
+                                                    const uint32_t* __restrict__ par_n, uint16_t* __restrict__ cand_win,
+                                                    uint32_t* __restrict__ par_win, DevStatus* st) {
+  __shared__ uint32_t sOff[MARK_WPB][WAVE + 1], sCarry[MARK_WPB][WAVE];
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const unsigned long long p0 = ((unsigned long long)blockIdx.x * MARK_WPB + w) * WAVE;
+  const bool active = p0 < nparents;
+  const int np = active ? (int)((nparents - p0) < WAVE ? (nparents - p0) : WAVE) : 0;
+  const uint32_t off0 = active ? par_off[p0] : 0u;
+  if (lane < np) {
+    sOff[w][lane] = par_off[p0 + lane] - off0;
+    sCarry[w][lane] = 0;
+    if (lane == np - 1) sOff[w][np] = par_off[p0 + lane] + par_n[p0 + lane] - off0;
+  }
+  __syncthreads();
+  const int total = active ? (int)sOff[w][np] : 0;
+  int steps = 0;  // block-uniform trip count (the loop holds a barrier)
+  for (int q = 0; q < MARK_WPB; ++q) {
+    const bool qa = ((unsigned long long)blockIdx.x * MARK_WPB + q) * WAVE < nparents;
+    if (qa) {
+      const unsigned long long qp = ((unsigned long long)blockIdx.x * MARK_WPB + q) * WAVE;
+      const int qn = (int)((nparents - qp) < WAVE ? (nparents - qp) : WAVE);
+      const int qt = (int)sOff[q][qn];
+      steps = steps > qt ? steps : qt;
+    }
+  }
+  uint32_t coll = 0;
+  const unsigned long long base0 = pbase + p0 + 1;  // ranks count parents from 1
+  for (int i0 = 0; i0 < steps; i0 += WAVE) {
+    const int idx = i0 + lane;
+    bool win = false;
+    int p = 0;
+    if (idx < total) {
+      int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)sOff[w][mid] <= idx) lo = mid; else hi = mid - 1;
+      }
+      p = lo;
+      const unsigned long long t = (unsigned long long)off0 + idx;
+      const uint32_t ob = cand_ob[t];
+      const unsigned long long sl = (ob & OB_ERR) ? CAND_DUP : cand_slot[t];
+      if (!(sl & CAND_DUP)) {
+        const unsigned long long v = table[ew * (sl & CAND_SLOT_MASK) + (ew >> 1)];
+        bool c = false;
+        win = fpset_won(v, ((base0 + p) << 10) | (ob >> 16), floor, sl >> 47, c);
+        coll += c ? 1u : 0u;
+      }
+    }
+    const unsigned long long m = __ballot(win);
+    if (idx < total) {
+      const int first = (int)sOff[w][p] - i0;  // parent p's first lane in this step (may be < 0)
+      const int endl = (int)sOff[w][p + 1] - i0;  // one past its last lane (may be > 64)
+      const unsigned long long from = first > 0 ? ~((1ULL << first) - 1ULL) : ~0ULL;
+      const uint32_t r = sCarry[w][p] + (uint32_t)__popcll(m & lanemask_lt() & from);
+      cand_win[(unsigned long long)off0 + idx] = win ? (uint16_t)(r + 1u) : (uint16_t)0;
+      if (lane == (endl < WAVE ? endl : WAVE) - 1) {  // p's last lane in this step carries its count on
+        const unsigned long long to = endl < WAVE ? ((1ULL << endl) - 1ULL) : ~0ULL;
+        sCarry[w][p] += (uint32_t)__popcll(m & from & to);
+      }
+    }
+    __syncthreads();  // the carries are read by other lanes in the next step
+  }
+  if (lane < np) par_win[p0 + lane] = sCarry[w][lane];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) coll += __shfl_xor(coll, o, WAVE);
+  if (lane == 0 && coll) atomicAdd(&st->hidden_coll, (unsigned long long)coll);
+}
+
 // Materialize the level's new states, tile by tile (same tiling as k_expand,
 // so a tile's candidates are one contiguous range).  Winners are compacted
 // into an LDS list and processed lane-per-winner: regenerate the successor
@@ -924,10 +1008,17 @@ static void dispatch(int spec, int N, bool expand, const LevelArgs& a, hipStream
 void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, true, a, s); }
 void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, false, a, s); }
 void launch_mark(const LevelArgs& a, hipStream_t s) {
+#ifdef RMC_MARK_THREADS
   unsigned long long blocks = (a.nparents + 255) / 256;
   hipLaunchKernelGGL(k_mark, dim3((unsigned)blocks), dim3(256), 0, s, a.nparents, a.pbase, a.floor,
                      a.model->fpw == 2 ? 4 : 2, a.table,
                      a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.cand_win, a.par_win, a.st);
+#else
+  unsigned long long blocks = (a.nparents + MARK_WPB * WAVE - 1) / (MARK_WPB * WAVE);
+  hipLaunchKernelGGL(k_mark_tiles, dim3((unsigned)blocks), dim3(MARK_WPB * WAVE), 0, s, a.nparents, a.pbase, a.floor,
+                     a.model->fpw == 2 ? 4 : 2, a.table,
+                     a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.cand_win, a.par_win, a.st);
+#endif
 }
 // Move every entry of the fingerprint set into a larger one (values kept).
 // Grid-stride: a table of 2^32 slots or more would need a grid of 2^32
