@@ -563,6 +563,10 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
 #define RMC_MARK_WPB 4
 #endif
 constexpr int MARK_WPB = RMC_MARK_WPB;  // waves (tiles) per k_mark_tiles block
+#ifndef RMC_MARK_U
+#define RMC_MARK_U 4
+#endif
+constexpr int MARK_U = RMC_MARK_U;  // 64-candidate steps whose loads are issued together
 __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long long nparents, unsigned long long pbase,
                                                     unsigned long long floor, int ew,
                                                     const unsigned long long* __restrict__ table,
@@ -596,40 +600,57 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
   }
   uint32_t coll = 0;
   const unsigned long long base0 = pbase + p0 + 1;  // ranks count parents from 1
-  for (int i0 = 0; i0 < steps; i0 += WAVE) {
-    const int idx = i0 + lane;
-    bool win = false;
-    int p = 0;
-    if (idx < total) {
-      int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int)sOff[w][mid] <= idx) lo = mid; else hi = mid - 1;
+  // MARK_U steps per round: their candidate and table loads are all issued
+  // before the first ballot (the kernel waits on those random reads)
+  for (int i0 = 0; i0 < steps; i0 += MARK_U * WAVE) {
+    uint32_t obv[MARK_U];
+    unsigned long long slv[MARK_U], vv[MARK_U];
+    int pv[MARK_U];
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int idx = i0 + u * WAVE + lane;
+      pv[u] = 0;
+      obv[u] = OB_ERR;
+      slv[u] = CAND_DUP;
+      if (idx < total) {
+        int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if ((int)sOff[w][mid] <= idx) lo = mid; else hi = mid - 1;
+        }
+        pv[u] = lo;
+        const unsigned long long t = (unsigned long long)off0 + idx;
+        obv[u] = cand_ob[t];
+        const unsigned long long s0 = cand_slot[t];  // read beside ob, used only without OB_ERR
+        slv[u] = (obv[u] & OB_ERR) ? CAND_DUP : s0;
       }
-      p = lo;
-      const unsigned long long t = (unsigned long long)off0 + idx;
-      const uint32_t ob = cand_ob[t];
-      const unsigned long long sl = (ob & OB_ERR) ? CAND_DUP : cand_slot[t];
-      if (!(sl & CAND_DUP)) {
-        const unsigned long long v = table[ew * (sl & CAND_SLOT_MASK) + (ew >> 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u)
+      vv[u] = (slv[u] & CAND_DUP) ? ~0ULL : table[ew * (slv[u] & CAND_SLOT_MASK) + (ew >> 1)];
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int iu = i0 + u * WAVE, idx = iu + lane, p = pv[u];
+      bool win = false;
+      if (idx < total && !(slv[u] & CAND_DUP)) {
         bool c = false;
-        win = fpset_won(v, ((base0 + p) << 10) | (ob >> 16), floor, sl >> 47, c);
+        win = fpset_won(vv[u], ((base0 + p) << 10) | (obv[u] >> 16), floor, slv[u] >> 47, c);
         coll += c ? 1u : 0u;
       }
-    }
-    const unsigned long long m = __ballot(win);
-    if (idx < total) {
-      const int first = (int)sOff[w][p] - i0;  // parent p's first lane in this step (may be < 0)
-      const int endl = (int)sOff[w][p + 1] - i0;  // one past its last lane (may be > 64)
-      const unsigned long long from = first > 0 ? ~((1ULL << first) - 1ULL) : ~0ULL;
-      const uint32_t r = sCarry[w][p] + (uint32_t)__popcll(m & lanemask_lt() & from);
-      cand_win[(unsigned long long)off0 + idx] = win ? (uint16_t)(r + 1u) : (uint16_t)0;
-      if (lane == (endl < WAVE ? endl : WAVE) - 1) {  // p's last lane in this step carries its count on
-        const unsigned long long to = endl < WAVE ? ((1ULL << endl) - 1ULL) : ~0ULL;
-        sCarry[w][p] += (uint32_t)__popcll(m & from & to);
+      const unsigned long long m = __ballot(win);
+      if (idx < total) {
+        const int first = (int)sOff[w][p] - iu;  // parent p's first lane in this step (may be < 0)
+        const int endl = (int)sOff[w][p + 1] - iu;  // one past its last lane (may be > 64)
+        const unsigned long long from = first > 0 ? ~((1ULL << first) - 1ULL) : ~0ULL;
+        const uint32_t r = sCarry[w][p] + (uint32_t)__popcll(m & lanemask_lt() & from);
+        cand_win[(unsigned long long)off0 + idx] = win ? (uint16_t)(r + 1u) : (uint16_t)0;
+        if (lane == (endl < WAVE ? endl : WAVE) - 1) {  // p's last lane in this step carries its count on
+          const unsigned long long to = endl < WAVE ? ((1ULL << endl) - 1ULL) : ~0ULL;
+          sCarry[w][p] += (uint32_t)__popcll(m & from & to);
+        }
       }
+      __syncthreads();  // the carries are read by other lanes in the next step
     }
-    __syncthreads();  // the carries are read by other lanes in the next step
   }
   if (lane < np) par_win[p0 + lane] = sCarry[w][lane];
 #pragma unroll
