@@ -95,7 +95,7 @@ def cpu_baseline(module, cfg_path, seconds=15.0):
     it); rate = distinct states / seconds of the levels it completed."""
     import raftmc
     cores, model = host_cores()
-    m = raftmc.Model(os.path.join(ROOT, "configs", module + ".tla"), os.path.join(ROOT, cfg_path))
+    m = raftmc.Model(module=module, cfg_path=os.path.join(ROOT, cfg_path))
     r = m.check_cpu(workers=cores, time_limit=seconds)
     return dict(value=r["distinct"] / max(r["seconds"], 1e-9), unit="distinct states/s", cores=cores,
                 kind="port", cpu_model=model,
@@ -131,7 +131,7 @@ def main():
     import raftmc
 
     module, cfg_rel, bcfg, desc = WORKLOADS[args.workload]
-    model = raftmc.Model(os.path.join(ROOT, "configs", module + ".tla"), os.path.join(ROOT, cfg_rel))
+    model = raftmc.Model(module=module, cfg_path=os.path.join(ROOT, cfg_rel))
     if world > 1:
         uid = [raftmc.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)

@@ -62,12 +62,17 @@ typedef struct {
   const char* checkpoint_dir;
   double checkpoint_minutes;
   const char* recover_dir;
+  /* BFS levels in pinned host memory (SURVEY.md §7 hard part 5): the current and next level's packed states
+   * live in host RAM and stream through HBM in chunk-sized windows, so the fingerprint set may take the
+   * whole device.  0 = auto (when a level would not fit beside the set in HBM), 1 = always, -1 = never
+   * (rmc_check only). */
+  int host_frontier;
 } rmc_options;
 
 typedef struct {
   uint64_t generated, distinct, left_on_queue;
   uint32_t depth;
-  int status; /* 0 ok, 1 invariant violated, 2 evaluation error, 3 capacity overflow, 4 stopped (max_depth) */
+  int status; /* 0 ok, 1 invariant violated, 2 evaluation error, 3 capacity overflow, 4 stopped (max_depth, time_limit) */
   char violated[64];
   char message[256];
   uint64_t hidden_var_collisions; /* same-level duplicates whose VIEW-hidden variables (acked, electionCtr,
@@ -82,10 +87,13 @@ typedef struct {
   uint64_t hash_capacity;
 } rmc_result;
 
-/* Load M.tla + M.cfg.  tla_path may name a file that does not exist; the module
- * is then taken from its basename (M.tla -> M).  Returns 0 or a negative error. */
+/* Load M.tla + M.cfg, as TLC reads them (`tlc2.TLC -config M.cfg M.tla`; a
+ * path without ".tla" gets it appended).  The .tla must exist and be the
+ * reference's text of a supported module (verified by a normalised hash); the
+ * module is its basename.  cfg_path NULL = M.cfg beside it.  Returns 0, or -3
+ * when a file cannot be read, -2 when the spec or cfg is rejected. */
 int rmc_model_load(const char* tla_path, const char* cfg_path, rmc_model** out, char* err, size_t errlen);
-/* Same, from in-memory cfg text and a module name. */
+/* The built-in lowering of `module` bound to in-memory cfg text (no .tla needed). */
 int rmc_model_load_text(const char* module, const char* cfg_text, rmc_model** out, char* err, size_t errlen);
 void rmc_options_default(rmc_options* o);
 int rmc_check(rmc_model* m, const rmc_options* o, rmc_result* out); /* blocking */
@@ -146,6 +154,10 @@ int rmc_simulate(rmc_model* m, const rmc_options* o, uint64_t walkers, uint32_t 
 int rmc_check_cpu(rmc_model* m, const rmc_options* o, rmc_result* out);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
 int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
+/* ABI self-description for binding checks (ctypes, JNA): fills up to cap values -- sizeof(rmc_options),
+ * the offset of each of its fields in declaration order, then sizeof(rmc_result) and its field offsets --
+ * and returns how many there are. */
+int rmc_abi_layout(uint64_t* out, int cap);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,10 @@
 // raftmc — TLC-compatible command line over librmc:
 //   raftmc [-deadlock] [-workers N] [-config M.cfg] [-json] [-v] M.tla
 // mirrors `java tlc2.TLC -deadlock [-workers N] [-config M.cfg] M.tla`
-// (reference README.md:6) and prints TLC's result lines.
+// (reference README.md:6) and prints TLC's result lines.  As TLC, it reads
+// M.tla (which must be the reference's text of a supported module);
+//   raftmc -module M -config X.cfg ...
+// checks the built-in lowering of module M against X.cfg without the .tla.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,7 +46,7 @@ int main(int argc, char** argv) {
   rmc_options o;
   rmc_options_default(&o);
   o.deadlock_check = 1;  // TLC default; the reference always passes -deadlock
-  std::string tla, cfg;
+  std::string tla, cfg, module;
   bool json = false, simulate = false, cpu = false;
   int shards = 0;  // > 0: the fingerprint-sharded protocol with this many logical shards on one GPU
   std::string metadir, recover;
@@ -60,6 +63,7 @@ int main(int argc, char** argv) {
     if (k == "-deadlock") o.deadlock_check = 0;
     else if (k == "-workers") o.cpu_workers = atoi(val().c_str());
     else if (k == "-config") cfg = val();
+    else if (k == "-module") module = val();
     else if (k == "-gpus") o.n_gpus = atoi(val().c_str());
     else if (k == "-msgcap") o.msg_cap_K = (uint32_t)atoi(val().c_str());
     else if (k == "-hashslots") o.hash_slots = strtoull(val().c_str(), nullptr, 10);
@@ -87,14 +91,27 @@ int main(int argc, char** argv) {
     else if (!k.empty() && k[0] == '-') { fprintf(stderr, "raftmc: unknown option %s\n", k.c_str()); return 2; }
     else tla = k;
   }
-  if (tla.empty()) {
+  if (tla.empty() == module.empty() || (!module.empty() && cfg.empty())) {
     fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-checkpoint MIN] [-metadir DIR] [-recover DIR] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
+                    "       raftmc [options] -module M -config X.cfg   (the built-in lowering of module M, no .tla)\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }
   char err[512];
   rmc_model* m = nullptr;
-  if (rmc_model_load(tla.c_str(), cfg.empty() ? nullptr : cfg.c_str(), &m, err, sizeof err) != 0) {
+  if (!module.empty()) {
+    FILE* f = fopen(cfg.c_str(), "rb");
+    if (!f) { fprintf(stderr, "raftmc: cannot read cfg file %s\n", cfg.c_str()); return 1; }
+    std::string text;
+    char b[4096];
+    for (size_t n; (n = fread(b, 1, sizeof b, f)) > 0;) text.append(b, n);
+    fclose(f);
+    if (rmc_model_load_text(module.c_str(), text.c_str(), &m, err, sizeof err) != 0) {
+      fprintf(stderr, "raftmc: %s\n", err);
+      return 1;
+    }
+    tla = module + " (built-in lowering)";
+  } else if (rmc_model_load(tla.c_str(), cfg.empty() ? nullptr : cfg.c_str(), &m, err, sizeof err) != 0) {
     fprintf(stderr, "raftmc: %s\n", err);
     return 1;
   }

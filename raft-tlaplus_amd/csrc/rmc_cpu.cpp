@@ -27,6 +27,11 @@
 
 using namespace rmc;
 
+#ifdef RMC_TILESTATS
+#include <cstdio>
+#include <unordered_set>
+static std::atomic<uint64_t> g_tile_intra{0}, g_tile_early{0};
+#endif
 namespace rmcx {
 namespace {
 
@@ -169,7 +174,16 @@ int check_cpu_t(rmc_model* m, const rmc_options* opt, int T, rmc_result* res) {
       parallel_for(T, n, [&](int w, uint64_t lo, uint64_t hi) {
         std::vector<Cand>& out = cands[w];
         std::vector<std::pair<int, Cand>> succ;
+#ifdef RMC_TILESTATS
+        // diagnostic: successors whose fingerprint another successor of the same
+        // 64-parent tile (k_expand's tile) produced first; earlier-level duplicates
+        std::unordered_set<uint64_t> tile_fps;
+        uint64_t t_intra = 0, t_early = 0;
+#endif
         for (uint64_t q = lo; q < hi; q++) {
+#ifdef RMC_TILESTATS
+          if (q == lo || q % 64 == 0) tile_fps.clear();
+#endif
           const uint64_t pg = cur_base + c0 + q;
           PState<SPEC, N> s{cur.data() + (c0 + q) * W};
           MsgSums<N> ms{};
@@ -207,6 +221,10 @@ int check_cpu_t(rmc_model* m, const rmc_options* opt, int T, rmc_result* res) {
               uint64_t val = ((((pg + 1) << 10) | (uint64_t)d.ordinal) << RANK_SHIFT) | c.hidden;
               c.slot = set.insert(fp, val, floor);
               if (c.slot == EMPTY64) capf |= 1u << E_CAP_TABLE;
+#ifdef RMC_TILESTATS
+              if (!tile_fps.insert(fp).second) t_intra++;
+              else if (c.slot != EMPTY64 && __atomic_load_n(&set.T[2 * c.slot + 1], __ATOMIC_RELAXED) < floor) t_early++;
+#endif
             }
             succ.push_back({d.ordinal, c});
           }
@@ -215,6 +233,10 @@ int check_cpu_t(rmc_model* m, const rmc_options* opt, int T, rmc_result* res) {
           par_off[q] = out.size();  // worker-local; rebased below
           for (auto& sc : succ) out.push_back(sc.second);
         }
+#ifdef RMC_TILESTATS
+        g_tile_intra += t_intra;
+        g_tile_early += t_early;
+#endif
       });
       if (capf.load()) {
         int e = 0;
@@ -365,6 +387,11 @@ int check_cpu_t(rmc_model* m, const rmc_options* opt, int T, rmc_result* res) {
   res->status = status;
   snprintf(res->message, sizeof res->message, "%s", message.c_str());
   res->seconds = elapsed();
+#ifdef RMC_TILESTATS
+  fprintf(stderr, "[rmc-cpu] successors %llu: new %llu, same-tile duplicates %llu, earlier-level duplicates %llu\n",
+          (unsigned long long)generated, (unsigned long long)distinct, (unsigned long long)g_tile_intra.load(),
+          (unsigned long long)g_tile_early.load());
+#endif
   res->hash_capacity = set.mask + 1;
   res->max_msgs = max_msgs;
   res->hidden_var_collisions = hidden_coll;

@@ -1139,6 +1139,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   try {
   while (status == 0 && cur_n > 0) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
+    if (opt->time_limit > 0 && secs(t0, now()) >= opt->time_limit) { status = 4; message = "time limit"; break; }
     unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     if (cur_base + cur_n + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
@@ -1161,6 +1162,26 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       }
       return hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL;
     };
+    if (m->profile_level && level == m->profile_level) {
+      // test hook (RMC_DIAG builds): k_expand on this level's first chunk,
+      // stopped after each phase in turn; none of these launches inserts
+      const unsigned long long n = std::min(chunk, cur_n);
+      for (int dg : {4, 3, 2, 1})
+        for (int rep = 0; rep < 3; rep++) {
+          LevelArgs a;
+          fill_args(a, 0, n, level);
+          a.diag = dg;
+          HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
+          HIPCHK(hipEventRecord(te.a, stream));
+          launch_expand(M.spec, M.N, a, stream);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipEventRecord(te.b, stream));
+          HIPCHK(hipStreamSynchronize(stream));
+          float ms = 0;
+          HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
+          m->profile_ms.push_back({dg, ms});
+        }
+    }
     unsigned long long c0 = 0;
     while (c0 < cur_n) {
       unsigned long long n = std::min(chunk, cur_n - c0);
@@ -1201,6 +1222,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
       expand_ms += ms;
       expand_launches++;
+      if (m->profile_level && level == m->profile_level && c0 == 0) m->profile_ms.push_back({0, ms});
       HIPCHK(hipEventElapsedTime(&ms, te.b, tm.b));
       mark_ms += ms;
       if (hst.cap_flags == (1u << E_RETRY)) {
@@ -1484,6 +1506,15 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     if (stp[8])
       fprintf(stderr, "[rmc] phase B fixed bindings: %.2f (parent, binding) pairs per parent pass may_enable; "
               "%.2f wave chunks per 64 parents\n", (double)stp[13] / stp[8], 64.0 * stp[14] / stp[8]);
+    {
+      unsigned long long fs[8];
+      read_fpstats(fs);
+      if (fs[FPS_INSERT])
+        fprintf(stderr, "[rmc] fingerprint-set inserts: %llu, 4-entry load groups %llu (%.3f per insert), CAS %llu "
+                "(%.3f per insert, %llu won), atomicMin %llu (%.3f per insert)\n", fs[FPS_INSERT], fs[FPS_GROUP],
+                (double)fs[FPS_GROUP] / fs[FPS_INSERT], fs[FPS_CAS], (double)fs[FPS_CAS] / fs[FPS_INSERT],
+                fs[FPS_CAS_WON], fs[FPS_MIN], (double)fs[FPS_MIN] / fs[FPS_INSERT]);
+    }
     fprintf(stderr, "[rmc] fingerprint set: 2^%d slots, load %.3f, %llu growths, %llu chunk redos\n",
             __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);
   }
@@ -1504,7 +1535,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   res->expand_launches = expand_launches;
   res->hash_capacity = slots;
   res->max_msgs = hst.max_msgs;
-  if (status == 0 && !opt->max_depth && !opt->msg_cap_K) m->hint_kmax = std::max(1u, hst.max_msgs);
+  // the next check's row packing: the peak |DOMAIN messages| of a complete
+  // check (a resumed one saw only the levels after its snapshot)
+  if (status == 0 && !opt->max_depth && !opt->msg_cap_K && !recovering) m->hint_kmax = std::max(1u, hst.max_msgs);
   return 0;
 }
 
@@ -1528,6 +1561,28 @@ void set_err(char* err, size_t len, const std::string& msg) {
 extern "C" {
 
 const char* rmc_version(void) { return "raftmc 0.1 (gfx950)"; }
+
+// ABI self-description for binding checks: sizeof and every field offset of
+// rmc_options then rmc_result, in declaration order (see include/rmc.h).
+int rmc_abi_layout(uint64_t* out, int cap) {
+  const uint64_t v[] = {
+      sizeof(rmc_options), offsetof(rmc_options, n_gpus), offsetof(rmc_options, cpu_workers),
+      offsetof(rmc_options, deadlock_check), offsetof(rmc_options, fp_bits), offsetof(rmc_options, tlc_order),
+      offsetof(rmc_options, hash_slots), offsetof(rmc_options, msg_cap_K), offsetof(rmc_options, frontier_cap),
+      offsetof(rmc_options, chunk_parents), offsetof(rmc_options, verbose), offsetof(rmc_options, max_depth),
+      offsetof(rmc_options, grow_on_overflow), offsetof(rmc_options, time_limit),
+      offsetof(rmc_options, checkpoint_dir), offsetof(rmc_options, checkpoint_minutes),
+      offsetof(rmc_options, recover_dir), offsetof(rmc_options, host_frontier),
+      sizeof(rmc_result), offsetof(rmc_result, generated), offsetof(rmc_result, distinct),
+      offsetof(rmc_result, left_on_queue), offsetof(rmc_result, depth), offsetof(rmc_result, status),
+      offsetof(rmc_result, violated), offsetof(rmc_result, message), offsetof(rmc_result, hidden_var_collisions),
+      offsetof(rmc_result, seconds), offsetof(rmc_result, expand_ms), offsetof(rmc_result, mark_ms),
+      offsetof(rmc_result, materialize_ms), offsetof(rmc_result, expand_launches), offsetof(rmc_result, state_bytes),
+      offsetof(rmc_result, max_msgs), offsetof(rmc_result, hash_capacity)};
+  const int n = (int)(sizeof v / sizeof v[0]);
+  for (int k = 0; k < n && k < cap; k++) out[k] = v[k];
+  return n;
+}
 const char* rmc_last_error(void) { return g_last_error.c_str(); }
 
 void rmc_options_default(rmc_options* o) {
@@ -1553,14 +1608,21 @@ int rmc_model_load(const char* tla_path, const char* cfg_path, rmc_model** out, 
   std::string tp = tla_path;
   std::string base = tp.substr(tp.find_last_of('/') == std::string::npos ? 0 : tp.find_last_of('/') + 1);
   std::string module = base.size() > 4 && base.substr(base.size() - 4) == ".tla" ? base.substr(0, base.size() - 4) : base;
+  if (base.size() <= 4 || base.substr(base.size() - 4) != ".tla") tp += ".tla";  // TLC: `tlc2.TLC Raft` reads Raft.tla
   bool ok = false;
   std::string tla = read_file(tp, ok);
+  if (!ok) {
+    // as TLC: the module file must exist (rmc_model_load_text checks the
+    // built-in lowering of a module from its cfg alone)
+    set_err(err, errlen, "cannot read module file " + tp + " (file not found)");
+    return -3;
+  }
   std::string cp = cfg_path ? std::string(cfg_path) : (tp.size() > 4 && tp.substr(tp.size() - 4) == ".tla" ? tp.substr(0, tp.size() - 4) : tp) + ".cfg";
   bool cok = false;
   std::string cfg = read_file(cp, cok);
   if (!cok) { set_err(err, errlen, "cannot read cfg file " + cp); return -3; }
   try {
-    *out = load_model(module, cfg, ok ? tla : "");
+    *out = load_model(module, cfg, tla);
     return 0;
   } catch (std::exception& e) {
     set_err(err, errlen, e.what());
@@ -1751,6 +1813,27 @@ void rmc_release_device_memory(void) {
     if (hipSetDevice(kv.first) == hipSuccess) kv.second->release();
   }
   (void)hipSetDevice(cur);
+}
+
+// Test hook only (RMC_DIAG builds): check up to `level`, timing k_expand on
+// that level's first chunk stopped after each phase (diag 4: staging, 3:
+// bindings, 2: successor deltas, 1: fingerprints, no insert; 0: the real
+// launch).  Fills (diag, ms) pairs; returns how many.
+int rmc_selftest_profile_expand(rmc_model* m, const rmc_options* o, int level, double* out, int cap) {
+  if (!m || !o || level < 2) { g_last_error = "bad argument"; return -1; }
+  if (!diag_build()) { g_last_error = "librmc was not built with -DRMC_DIAG"; return -1; }
+  rmc_options oo = *o;
+  oo.max_depth = level;
+  m->profile_level = (unsigned)level;
+  m->profile_ms.clear();
+  rmc_result r;
+  const int rc = rmc_check(m, &oo, &r);
+  m->profile_level = 0;
+  if (rc != 0) return rc;
+  int n = 0;
+  for (auto& pr : m->profile_ms)
+    if (n + 1 < cap) { out[n] = pr.first; out[n + 1] = pr.second; n += 2; }
+  return n / 2;
 }
 
 // Test hook only: the row packing the next check of m starts from (as if its

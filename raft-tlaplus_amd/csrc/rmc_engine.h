@@ -51,6 +51,7 @@ struct LevelArgs {
   unsigned long long* tr_parent;
   uint16_t* tr_bind;
   DevStatus* st;
+  int diag;  // RMC_DIAG builds: k_expand stops after a phase (rmc_selftest_profile_expand); 0 = the real kernel
 };
 
 void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s);
@@ -86,6 +87,8 @@ void launch_mark_gen(const LevelArgs& a, int moved, const uint32_t* perm, const 
                      unsigned long long* newcount, hipStream_t s);
 int host_fp_owner(unsigned long long fp, int W);
 void read_stamps(unsigned long long* out);  // -DRMC_STAMPS diagnostic builds
+void read_fpstats(unsigned long long* out);
+bool diag_build();  // compiled with -DRMC_DIAG (k_expand phase cutoffs)  // -DRMC_FPSTATS diagnostic builds (8 counters, rmc_fpset.h)
 void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long walkers, unsigned depth,
                      unsigned long long seed, uint16_t* binds, unsigned long long* counters, SimStatus* ss,
                      DevStatus* st, int words, hipStream_t s);

@@ -52,20 +52,95 @@ __host__ __device__ __forceinline__ int fp_owner(unsigned long long fp, int W) {
   return (int)(((fp >> 32) * (unsigned long long)W) >> 32);
 }
 
+// Diagnostic build only (-DRMC_FPSTATS): exact counts of what the inserts do
+// (inserts, 4-entry group loads, CAS issued / won, atomicMin issued), read
+// back with read_fpstats(); the product build compiles them away.
+#ifdef RMC_FPSTATS
+static __device__ unsigned long long g_fpstats[8];
+#define FPSTAT(i) atomicAdd(&g_fpstats[i], 1ULL)
+#else
+#define FPSTAT(i) ((void)0)
+#endif
+enum { FPS_INSERT = 0, FPS_GROUP = 1, FPS_CAS = 2, FPS_CAS_WON = 3, FPS_MIN = 4 };
+
 // Insert fp with value val; returns the slot, or EMPTY when the probe run is
 // too long (the table is too full: the driver grows it and redoes the chunk,
 // whose inserts are idempotent).
 //
-// Fast path: the first 4 entries of the probe run are read with plain 16 B
-// loads (issued together: one memory round trip).  Keys are never removed or
-// moved while a level is expanded, so a key seen there is really there: an
-// earlier level's copy of fp is final (no atomic, no write -- most
-// successors), and a same-level copy only needs its atomicMin.  A slot seen
-// empty may have been claimed since (the load can be stale), so the run goes
-// on from there with the CAS protocol, one returning atomic per probe.
+// The probe run is READ, four entries (64 B) per group of plain 16 B loads
+// issued together, up to the first entry that is fp or EMPTY.  Keys are never
+// removed or moved while a level is expanded, so a key read with a plain load
+// is really there -- an earlier level's copy of fp is final (no atomic, no
+// write), a same-level copy only needs its atomicMin, and another key means
+// "go on".  A slot seen EMPTY may have been claimed since (the XCD's L2 is not
+// coherent with the other XCDs' atomics), so it takes ONE CAS, whose returned
+// key decides; a CAS lost to another key resumes the READ probe after it.  So
+// a wave issues at most one CAS instruction per probe step.  (On gfx950 every
+// device-scope atomic executes at the memory side, MI355X_MICROARCH.md
+// 'Global float atomics': the r02 protocol's CAS per slot past the first
+// four entries was a memory round trip and a WRITE_SIZE transaction per
+// occupied slot passed.)
+#ifndef RMC_FP_LEGACY
 __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T, unsigned long long mask,
                                                            unsigned long long fp, unsigned long long val,
                                                            unsigned long long floor, DevStatus* st) {
+  FPSTAT(FPS_INSERT);
+  unsigned long long slot = fp_slot(fp, mask);
+  const unsigned long long limit = mask < 4096 ? mask : 4096;
+  const ulonglong2* E = reinterpret_cast<const ulonglong2*>(T);
+  for (unsigned long long probe = 0; probe <= limit;) {
+    FPSTAT(FPS_GROUP);
+    ulonglong2 e[4];
+    if (slot + 3 <= mask) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) e[q] = E[slot + q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) e[q] = E[(slot + q) & mask];
+    }
+    int k = 4;
+    unsigned long long kv = 0;
+    bool found = false;
+#pragma unroll
+    for (int q = 3; q >= 0; q--)
+      if (e[q].x == fp || e[q].x == EMPTY) { k = q; kv = e[q].y; found = e[q].x == fp; }
+    slot = (slot + (unsigned long long)k) & mask;
+    probe += (unsigned long long)k;
+    if (k == 4) continue;  // four other keys: read on
+    if (found) {
+      // same level (or its claimer's min in flight): values only decrease, so
+      // a snapshot already below val means this successor lost -- no atomic
+      if (kv >= floor && val < kv) { FPSTAT(FPS_MIN); atomicMin(T + 2 * slot + 1, val); }
+      return slot;
+    }
+    FPSTAT(FPS_CAS);
+    const unsigned long long prev = atomicCAS(T + 2 * slot, EMPTY, fp);
+    if (prev == EMPTY) {
+      FPSTAT(FPS_CAS_WON);
+      FPSTAT(FPS_MIN);
+      atomicMin(T + 2 * slot + 1, val);
+      return slot;
+    }
+    if (prev == fp) {
+      // claimed by another lane this level (a value of ~0: its claimer's
+      // atomicMin is still in flight, >= floor, so this one takes part)
+      const unsigned long long cur = __hip_atomic_load(T + 2 * slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur >= floor && val < cur) { FPSTAT(FPS_MIN); atomicMin(T + 2 * slot + 1, val); }
+      return slot;
+    }
+    slot = (slot + 1) & mask;  // another key took it since the load
+    probe++;
+  }
+  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+  return EMPTY;
+}
+#else
+// r02 protocol (kept for A/B measurement): four entries read, then a CAS per probe
+__device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T, unsigned long long mask,
+                                                           unsigned long long fp, unsigned long long val,
+                                                           unsigned long long floor, DevStatus* st) {
+  FPSTAT(FPS_INSERT);
+  FPSTAT(FPS_GROUP);
   unsigned long long slot = fp_slot(fp, mask);
 #ifndef RMC_FP_FAST
 #define RMC_FP_FAST 4
@@ -83,26 +158,24 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
       if (e[q].x == fp || e[q].x == EMPTY) { k = q; kv = e[q].y; found = e[q].x == fp; }
     slot = (slot + (unsigned long long)k) & mask;  // k == RMC_FP_FAST may step past the last slot: wrap
     if (found) {
-      // same level (or its claimer's min in flight): values only decrease, so
-      // a snapshot already below val means this successor lost -- no atomic
-      if (kv >= floor && val < kv) atomicMin(T + 2 * slot + 1, val);
+      if (kv >= floor && val < kv) { FPSTAT(FPS_MIN); atomicMin(T + 2 * slot + 1, val); }
       return slot;
     }
   }
   const unsigned long long limit = mask < 4096 ? mask : 4096;
   for (unsigned long long probe = 0; probe <= limit; probe++) {
     unsigned long long* e = T + 2 * slot;
+    FPSTAT(FPS_CAS);
     const unsigned long long prev = atomicCAS(e, EMPTY, fp);
     if (prev == EMPTY) {
+      FPSTAT(FPS_CAS_WON);
+      FPSTAT(FPS_MIN);
       atomicMin(e + 1, val);
       return slot;
     }
     if (prev == fp) {
-      // an earlier level's entry is final: leave its line clean.  (A value of
-      // ~0 is an entry being claimed this level, whose claimer's atomicMin is
-      // still in flight: >= floor, so this one takes part.)
       const unsigned long long cur = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur >= floor && val < cur) atomicMin(e + 1, val);
+      if (cur >= floor && val < cur) { FPSTAT(FPS_MIN); atomicMin(e + 1, val); }
       return slot;
     }
     slot = (slot + 1) & mask;
@@ -110,6 +183,7 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
   atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
   return EMPTY;
 }
+#endif
 
 // The value of fp's entry (~0 if absent): read-only probe.
 __device__ __forceinline__ unsigned long long fpset_value(const unsigned long long* T, unsigned long long mask,

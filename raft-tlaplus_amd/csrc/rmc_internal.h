@@ -38,6 +38,10 @@ struct rmc_model {
   // this model packs rows to exactly that many message slots (an overflow
   // still re-runs with a larger capacity, so the hint is never unsafe)
   uint32_t hint_kmax = 0;
+  // test hook (rmc_selftest_profile_expand): time k_expand's phases on the
+  // first chunk of this level; (diag, ms) pairs of the last check
+  unsigned profile_level = 0;
+  std::vector<std::pair<int, double>> profile_ms;
 };
 
 

@@ -72,6 +72,21 @@ void read_stamps(unsigned long long* out) {
 #endif
 }
 
+bool diag_build() {
+#ifdef RMC_DIAG
+  return true;
+#else
+  return false;
+#endif
+}
+void read_fpstats(unsigned long long* out) {
+#ifdef RMC_FPSTATS
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fpstats), 8 * sizeof(unsigned long long));
+#else
+  for (int i = 0; i < 8; i++) out[i] = 0;
+#endif
+}
+
 // Parents per expand/materialize tile: one per lane of a wave in phase B.
 template <int N>
 struct Tile {
@@ -80,8 +95,9 @@ struct Tile {
 
 // Dynamic LDS layout of k_expand (bytes; the launch computes the same).
 constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
+constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-successor round
 struct ExpandLds {
-  int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, bytes;
+  int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, bytes;
 };
 __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes, int nfixed, int nord) {
   ExpandLds L;
@@ -89,16 +105,10 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
   int o = (PB * L.Wp * 4 + 7) & ~7;
   L.off_Ms = o;  // per-parent message sums (MsgSums<N>, 8 B aligned)
   o += PB * msbytes;
-  L.off_Mask = o;  // per fixed binding: the tile's parents that pass may_enable (64-bit masks)
-  o += nfixed * 8;
-  L.off_BOff = o;  // exclusive prefix over fixed bindings of the passing pairs
-  o += (nfixed + 1) * 4;
   L.off_Ord = o;  // per parent: bitmask over TLC ordinals of its enabled bindings
   o += PB * ordw * 4;
   L.off_Base = o;  // exclusive prefix over the tile's parents of their successor counts
   o += (PB + 1) * 4;
-  L.off_Live = o;  // per parent: bitmask over DOMAIN messages that can enable an action (msg_live)
-  o += PB * LIVE_WORDS * 4;
   // the model's binding tables, staged once per block: a lane's own binding
   // then costs LDS reads instead of dependent vector loads of __constant__ data
   L.off_Desc = o;  // fixed binding -> descriptor (Model::fb_desc)
@@ -107,7 +117,17 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
   o += ((nord + 1) & ~1) * 2;
   L.off_MOff = o;  // message action id -> its first ordinal
   o += ((A_NUM + 1) & ~1) * 2;
-  L.bytes = o;
+  o = (o + 7) & ~7;
+  // phase B only (dead in phase C, where the dedup table reuses the bytes)
+  L.off_Mask = o;  // per fixed binding: the tile's parents that pass may_enable (64-bit masks)
+  L.off_Hash = o;  // phase C: DEDUP fingerprints (8 B) + DEDUP representatives (4 B)
+  o += nfixed * 8;
+  L.off_BOff = o;  // exclusive prefix over fixed bindings of the passing pairs
+  o += (nfixed + 1) * 4;
+  L.off_Live = o;  // per parent: bitmask over DOMAIN messages that can enable an action (msg_live)
+  o += PB * LIVE_WORDS * 4;
+  const int hash_end = L.off_Hash + DEDUP * 12;
+  L.bytes = o > hash_end ? o : hash_end;
   return L;
 }
 
@@ -179,7 +199,15 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
                                                 uint32_t* __restrict__ cand_ob, uint32_t* __restrict__ par_off,
                                                 uint32_t* __restrict__ par_n,
                                                 unsigned long long* __restrict__ counters, unsigned long long cand_cap,
-                                                DevStatus* st, unsigned long long* __restrict__ cand_val) {
+                                                DevStatus* st, unsigned long long* __restrict__ cand_val
+#ifdef RMC_DIAG
+                                                , int diag
+#endif
+                                                ) {
+#ifndef RMC_DIAG
+  constexpr int diag = 0;  // RMC_DIAG builds: stop after a phase (4: staging, 3: bindings, 2: + successor
+                           // deltas, 1: + fingerprints and tile dedup, no global insert)
+#endif
   constexpr int PB = Tile<N>::PB;
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG, sSeg;
@@ -217,6 +245,12 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
   __syncthreads();
   STAMP(0);
+  if (diag == 4) {  // staging only (a checksum keeps it live)
+    uint32_t x = 0;
+    for (int q = tid; q < np * words; q += 256) x ^= sS[(q / words) * L.Wp + q % words];
+    if (tid < np) par_n[p0 + tid] = x;
+    return;
+  }
   // ---- B: enabled bindings, lane per parent
   {
     const int p = tid % PB, bstride = 256 / PB;
@@ -421,6 +455,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     if (tid == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
     return;
   }
+  if (diag == 3) return;  // bindings only
 #ifdef RMC_STAMPS
   // diagnostic: phase C without the fingerprint-set inserts (stamp 7), so the
   // inserts' share is the difference from the real phase C (stamp 3)
@@ -460,6 +495,83 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   //      candidate gbase + idx, so a wave's candidate stores are contiguous
   //      (binding-major enumeration scattered them: one 32 B write request per
   //      8 B store, ~0.7 GB of extra HBM writes per launch on the bench cfg).
+#ifndef RMC_NO_DEDUP
+  if constexpr (FPW == 1) {
+    if (!sharded) {
+      // Tile-local dedup first.  A BFS level's duplicates are same-level ones
+      // (0.7% of the bench workload's successors are of an earlier level),
+      // and 37% of all successors repeat a fingerprint another successor of
+      // the SAME 64-parent tile produced (commuting actions of sibling
+      // parents; CPU census).  Per round of 256 successors
+      // an LDS table keeps each fingerprint's first successor in TLC order
+      // (the lowest idx: candidates are in TLC order), and only that
+      // representative touches the HBM set -- it carries the tile's lowest
+      // rank, so the others could never lower the entry's min.  They share
+      // its slot: k_mark's win test and hidden-variable collision count read
+      // the entry exactly as if they had inserted.
+      unsigned long long* sHK = (unsigned long long*)(lds + L.off_Hash);
+      uint32_t* sHR = (uint32_t*)(lds + L.off_Hash + DEDUP * 8);
+      for (int r0 = 0; r0 < total; r0 += 256) {
+        sHK[tid] = EMPTY;
+        sHR[tid] = 0xFFFFFFFFu;
+        __syncthreads();
+        const int idx = r0 + tid;
+        const bool act = idx < total;
+        uint32_t obw = OB_ERR;  // the candidate's ordinal/binding word (the Delta is dead after the fp)
+        unsigned long long fp = 0, val = 0;
+        if (act) {
+          int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
+          while (lo < hi) {
+            int mid = (lo + hi + 1) >> 1;
+            if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
+          }
+          const int p = lo;
+          const int ord = select_bit(sOrd + p * ordw, idx - (int)sBase[p]);
+          const int b = sO2b[ord];
+          PState<SPEC, N> s{sS + p * L.Wp};
+          Delta d;
+          eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
+          obw = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : 0u);
+          if (diag == 2) fp = (unsigned long long)d.hdr ^ d.w[0] ^ d.opc[0];  // the delta only
+          else if (!d.err) {
+            const unsigned long long pg = pbase + p0 + p;
+            val = ((((pg + 1) << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
+                  (unsigned long long)hidden_of<SPEC>(d.hdr);
+            fp = delta_fp_sums<SPEC, N>(s, cM, d, sums1<N>(sMS[p]));
+          }
+        }
+        const bool ok = act && !(obw & OB_ERR) && diag != 2;
+        int h = 0;
+        if (ok) {
+          h = (int)((fp ^ (fp >> 32)) & (DEDUP - 1));
+          for (;;) {  // at most 256 keys in DEDUP slots: a slot is always found
+            const unsigned long long prev = atomicCAS(&sHK[h], EMPTY, fp);
+            if (prev == EMPTY || prev == fp) break;
+            h = (h + 1) & (DEDUP - 1);
+          }
+          atomicMin(&sHR[h], (uint32_t)tid);
+        }
+        __syncthreads();
+        const bool rep = ok && sHR[h] == (uint32_t)tid;
+        unsigned long long raw = EMPTY;
+        if (rep) {
+          raw = diag == 1 ? (fp & CAND_SLOT_MASK) : fpset_insert(table, mask, fp, val, floor, st);
+          sHK[h] = raw;  // keys are not read again this round: the slot in their place
+        }
+        __syncthreads();
+        if (ok && !rep) raw = sHK[h];
+        if (act) {
+          const unsigned long long t = gbase + (unsigned long long)idx;
+          cand_slot[t] = diag == 2 ? fp : ok ? cand_word(raw, val) : CAND_DUP;
+          cand_ob[t] = obw;
+        }
+        __syncthreads();  // the next round resets the table
+      }
+      STAMP(3);
+      return;
+    }
+  }
+#endif
   for (int idx = tid; idx < total; idx += 256) {
     int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
     while (lo < hi) {
@@ -484,8 +596,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
         const Fp128 fp = delta_fp_sums2<SPEC, N>(s, cM, d, sMS[p]);
         slot = cand_word(fpset_insert128(table, mask, fp, val, floor, st), val);
       } else {
-        unsigned long long fp = delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
-        if (sharded) {  // the fp's owner inserts it: here when that is this shard, else k_insert_recv
+        unsigned long long fp = diag == 2 ? (unsigned long long)d.hdr ^ d.w[0] ^ d.opc[0]
+                                          : delta_fp_sums<SPEC, N>(s, cM, d, sMS[p]);
+        if (diag) {
+          slot = fp;
+        } else if (sharded) {  // the fp's owner inserts it: here when that is this shard, else k_insert_recv
           if (fp_owner(fp, sharded) == shard_self) {
             // as the single-shard search (a full table flags E_CAP_TABLE: the
             // round is redone), plus the fp: the table may grow before k_mark_gen
@@ -990,7 +1105,11 @@ struct Launch {
                              M.ordinal_limit);
     hipLaunchKernelGGL((k_expand<SPEC, N, FPW>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.floor, a.sharded, a.shard_self, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
-                       a.st, a.cand_val);
+                       a.st, a.cand_val
+#ifdef RMC_DIAG
+                       , a.diag
+#endif
+                       );
   }
   template <int SPEC, int N>
   static void materialize(const LevelArgs& a, hipStream_t s) {
@@ -1054,11 +1173,15 @@ __global__ __launch_bounds__(256) void k_rehash(const unsigned long long* __rest
     if (k == EMPTY) continue;
     unsigned long long slot = fp_slot(k, mask);
     unsigned long long probe = 0;
+    // read the run, CAS only a slot seen empty (an atomic is a memory-side
+    // round trip on gfx950; an occupied slot read with a plain load is final)
     for (; probe <= mask; probe++) {
-      unsigned long long prev = atomicCAS(nt + ew * slot, EMPTY, k);
-      if (prev == EMPTY) {
-        for (int w = 1; w < ew; w++) nt[ew * slot + w] = old[ew * e + w];
-        break;
+      if (nt[ew * slot] == EMPTY) {
+        unsigned long long prev = atomicCAS(nt + ew * slot, EMPTY, k);
+        if (prev == EMPTY) {
+          for (int w = 1; w < ew; w++) nt[ew * slot + w] = old[ew * e + w];
+          break;
+        }
       }
       slot = (slot + 1) & mask;
     }

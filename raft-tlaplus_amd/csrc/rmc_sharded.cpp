@@ -471,6 +471,17 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   };
   while (status == 0 && P > 0 && !stop) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
+    if (opt->time_limit > 0) {
+      // every rank must stop at the same level boundary: the slowest clock decides
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      for (int i = 0; i < NL; i++) rows[i] = {(uint64_t)(el * 1e6)};
+      comm.allgather(rows, all, 1);
+      if ((double)*std::max_element(all.begin(), all.end()) >= opt->time_limit * 1e6) {
+        status = 4;
+        message = "time limit";
+        break;
+      }
+    }
     const unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     const unsigned long long rounds = (P + W * CH - 1) / (W * CH);

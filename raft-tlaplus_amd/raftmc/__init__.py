@@ -31,7 +31,8 @@ class Options(ctypes.Structure):
                 ("chunk_parents", ctypes.c_uint32), ("verbose", ctypes.c_int),
                 ("max_depth", ctypes.c_int), ("grow_on_overflow", ctypes.c_int),
                 ("time_limit", ctypes.c_double), ("checkpoint_dir", ctypes.c_char_p),
-                ("checkpoint_minutes", ctypes.c_double), ("recover_dir", ctypes.c_char_p)]
+                ("checkpoint_minutes", ctypes.c_double), ("recover_dir", ctypes.c_char_p),
+                ("host_frontier", ctypes.c_int)]
 
 
 class Result(ctypes.Structure):
@@ -51,7 +52,8 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_trace_len", "rmc_trace_state", "rmc_trace_action", "rmc_format_report",
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
-           "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm"]
+           "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm",
+           "rmc_abi_layout"]
 
 _lib = None
 
@@ -77,6 +79,7 @@ def lib():
     L.rmc_last_error.restype = ctypes.c_char_p
     L.rmc_version.restype = ctypes.c_char_p
     L.rmc_levels.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), c_int]
+    L.rmc_abi_layout.argtypes = [ctypes.POINTER(ctypes.c_uint64), c_int]
     L.rmc_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                     ctypes.POINTER(Result)]
@@ -92,6 +95,7 @@ def lib():
     L.rmc_trace_json.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_selftest_random_trace.argtypes = [P, ctypes.c_uint64, c_int]
     L.rmc_selftest_set_hint_kmax.argtypes = [P, ctypes.c_uint32]
+    L.rmc_selftest_profile_expand.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(ctypes.c_double), c_int]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
     L.rmc_selftest_encode_kmsg.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
     _lib = L
@@ -102,9 +106,19 @@ class Model:
     """A spec + cfg loaded into librmc (TLC's parse/bind step)."""
 
     def __init__(self, tla_path=None, cfg_path=None, module=None, cfg_text=None):
+        """Model("M.tla", "M.cfg") reads both files, as TLC does (the .tla must be
+        the reference's text of a supported module).  Model(module="M",
+        cfg_text=...) or Model(module="M", cfg_path="X.cfg") binds the built-in
+        lowering of module M to a cfg without a .tla."""
         L = lib()
         err = ctypes.create_string_buffer(512)
         h = ctypes.c_void_p()
+        if tla_path is None and cfg_text is None and module is not None and cfg_path is not None:
+            try:
+                with open(cfg_path) as f:
+                    cfg_text = f.read()
+            except OSError as e:
+                raise RaftmcError("cannot read cfg file %s (%s)" % (cfg_path, e.strerror))
         if cfg_text is not None:
             rc = L.rmc_model_load_text(module.encode(), cfg_text.encode(), ctypes.byref(h), err, 512)
         else:
@@ -121,7 +135,8 @@ class Model:
 
     def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
                  chunk_parents=0, verbose=False, max_depth=0, workers=0, grow_on_overflow=False,
-                 time_limit=0.0, fp_bits=64, checkpoint_dir=None, checkpoint_minutes=0.0, recover_dir=None):
+                 time_limit=0.0, fp_bits=64, checkpoint_dir=None, checkpoint_minutes=0.0, recover_dir=None,
+                 host_frontier=0):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
@@ -139,6 +154,7 @@ class Model:
         o.grow_on_overflow = int(grow_on_overflow)
         o.time_limit = float(time_limit)
         o.fp_bits = int(fp_bits)
+        o.host_frontier = int(host_frontier)
         return o
 
     def _result(self, rc, r):
@@ -249,6 +265,16 @@ class Model:
         L.rmc_format_report(self._h, ctypes.byref(self._last), buf, len(buf))
         return buf.value.decode()
 
+    def selftest_profile_expand(self, level, **kw):
+        """TEST HOOK (RMC_DIAG builds): k_expand phase times on `level`'s first chunk:
+        [(diag, ms)], diag 4 staging .. 1 no insert, 0 the real launch."""
+        o = self._options(**kw)
+        buf = (ctypes.c_double * 64)()
+        n = lib().rmc_selftest_profile_expand(self._h, ctypes.byref(o), int(level), buf, 64)
+        if n < 0:
+            raise RaftmcError(lib().rmc_last_error().decode())
+        return [(int(buf[2 * k]), buf[2 * k + 1]) for k in range(n)]
+
     def selftest_set_hint_kmax(self, k):
         """TEST HOOK: pretend the last check saw at most k messages per state, so the
         next check packs rows to k slots (an overflow must take the re-run path)."""
@@ -283,6 +309,13 @@ def comm_unique_id():
 
 def check_text(module, cfg_text, **kw):
     return Model(module=module, cfg_text=cfg_text).check(**kw)
+
+
+def abi_layout():
+    """librmc's own sizeof/offsetof of rmc_options and rmc_result (rmc_abi_layout)."""
+    buf = (ctypes.c_uint64 * 64)()
+    n = lib().rmc_abi_layout(buf, 64)
+    return [buf[k] for k in range(n)]
 
 
 def encode_msg(spec, **f):

@@ -15,7 +15,7 @@ if "cfg" in g:
     m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
 else:  # shipped.json: the restated reference cfg under configs/
     root = os.path.dirname(HERE)
-    m = raftmc.Model(os.path.join(root, "configs", g["module"] + ".tla"), os.path.join(root, g["cfg_path"]))
+    m = raftmc.Model(module=g["module"], cfg_path=os.path.join(root, g["cfg_path"]))
 try:
     r = m.check_sharded_shm(int(rank), int(world), 0, name, chunk_parents=int(chunk))
 except raftmc.RaftmcError as e:

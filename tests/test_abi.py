@@ -1,5 +1,6 @@
 """The C ABI boundary: librmc.so loads, exports every entry point include/rmc.h
 declares, rejects bad input with a message, and fails loudly without a GPU."""
+import ctypes
 import os
 import re
 
@@ -30,16 +31,66 @@ def test_load_errors_are_reported():
     with pytest.raises(raftmc.RaftmcError, match="MaxElections"):
         raftmc.Model(module="Raft", cfg_text="CONSTANTS Server = {n1, n2} Value = {v1}\nINIT Init NEXT Next VIEW view")
     with pytest.raises(raftmc.RaftmcError, match="cfg"):
-        raftmc.Model(os.path.join(ROOT, "configs", "Raft.tla"), os.path.join(ROOT, "configs", "missing.cfg"))
+        raftmc.Model(module="Raft", cfg_path=os.path.join(ROOT, "configs", "missing.cfg"))
+
+
+def test_missing_tla_is_refused(tmp_path):
+    """TLC fails on a module file that does not exist; so does rmc_model_load
+    (the built-in lowering without a .tla is rmc_model_load_text)."""
+    cfg = tmp_path / "Raft.cfg"
+    cfg.write_text(open(os.path.join(ROOT, "configs", "Raft.cfg")).read())
+    with pytest.raises(raftmc.RaftmcError, match="cannot read module file"):
+        raftmc.Model(str(tmp_path / "Raft.tla"), str(cfg))
+    with pytest.raises(raftmc.RaftmcError, match="cannot read module file"):
+        raftmc.Model(str(tmp_path / "Raft"), str(cfg))  # TLC appends .tla
+
+
+def test_abi_layout_matches_ctypes():
+    """librmc's own sizeof/offsetof of rmc_options and rmc_result equal the
+    ctypes structures' (a binding that drifts from include/rmc.h would write
+    past the struct or read the wrong fields)."""
+    lay = raftmc.abi_layout()
+    no, nr = len(raftmc.Options._fields_), len(raftmc.Result._fields_)
+    assert len(lay) == 2 + no + nr
+    assert lay[0] == ctypes.sizeof(raftmc.Options)
+    assert lay[1:1 + no] == [getattr(raftmc.Options, f).offset for f, _ in raftmc.Options._fields_]
+    assert lay[1 + no] == ctypes.sizeof(raftmc.Result)
+    assert lay[2 + no:] == [getattr(raftmc.Result, f).offset for f, _ in raftmc.Result._fields_]
+
+
+def test_header_fields_match_bindings():
+    """The field lists of include/rmc.h, the ctypes structures and the JNA
+    stub in INTEGRATION.md are the same, in the same order."""
+    h = open(os.path.join(ROOT, "include", "rmc.h")).read()
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+
+    def header_fields(name):
+        body = dict((n, b) for b, n in re.findall(r"typedef struct \{([^{}]*)\} (\w+);", h))[name]
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        out = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            decl = re.sub(r"\[\d+\]", "", decl)
+            names = [x.strip().split()[-1].lstrip("*") for x in decl.split(",")]
+            out += names
+        return out
+
+    jna = re.findall(r"@Structure\.FieldOrder\(\{(.*?)\}\)", integ, re.S)
+    assert len(jna) == 2
+    jna = [[x.strip().strip('"') for x in j.split(",")] for j in jna]
+    assert header_fields("rmc_options") == [f for f, _ in raftmc.Options._fields_] == jna[0]
+    assert header_fields("rmc_result") == [f for f, _ in raftmc.Result._fields_] == jna[1]
 
 
 def test_loads_shipped_cfgs():
     for mod in ("Raft", "PullRaft", "RaftFsync", "FlexibleRaft"):
-        raftmc.Model(os.path.join(ROOT, "configs", mod + ".tla"), os.path.join(ROOT, "configs", mod + ".cfg"))
+        raftmc.Model(module=mod, cfg_path=os.path.join(ROOT, "configs", mod + ".cfg"))
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
 def test_check_without_gpu_fails_loudly():
-    m = raftmc.Model(os.path.join(ROOT, "configs", "Raft.tla"), os.path.join(ROOT, "configs", "Raft.cfg"))
+    m = raftmc.Model(module="Raft", cfg_path=os.path.join(ROOT, "configs", "Raft.cfg"))
     with pytest.raises(raftmc.RaftmcError, match="HIP device|no HIP"):
         m.check()

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 def model(g):
     if "cfg_path" in g:
-        return raftmc.Model(os.path.join(ROOT, "configs", g["module"] + ".tla"), os.path.join(ROOT, g["cfg_path"]))
+        return raftmc.Model(module=g["module"], cfg_path=os.path.join(ROOT, g["cfg_path"]))
     return raftmc.Model(module=g["module"], cfg_text=g["cfg"])
 
 

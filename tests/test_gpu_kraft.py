@@ -68,7 +68,7 @@ def test_kraft_shipped_cfg():
     """KRaft.cfg's constants (19,841,847 distinct, 57,806,118 generated, depth
     52): every level equal to the C++ oracle's, and GPU == CPU engine."""
     g = KR["KRaft_cfg"]  # C++ oracle, exhaustive (its first 16 levels also the Python oracle's)
-    m = raftmc.Model(os.path.join(ROOT, "configs", "KRaft.tla"), os.path.join(ROOT, "configs", "KRaft.cfg"))
+    m = raftmc.Model(module="KRaft", cfg_path=os.path.join(ROOT, "configs", "KRaft.cfg"))
     r = m.check()
     assert (r["generated"], r["distinct"], r["depth"], r["status"], r["levels"]) == \
         (g["generated"], g["distinct"], g["depth"], g["status"], g["levels"])
@@ -87,7 +87,7 @@ def test_kraft_simulation():
     assert r["status"] == "violation" and r["violated"] == "NoIllegalState"
     assert r["trace"][0][0] == "Initial predicate" and len(r["trace"]) >= g["trace_len"]
     assert "IllegalState" in r["trace"][-1][1]
-    s = raftmc.Model(os.path.join(ROOT, "configs", "KRaft.tla"), os.path.join(ROOT, "configs", "KRaft.cfg")).simulate(
+    s = raftmc.Model(module="KRaft", cfg_path=os.path.join(ROOT, "configs", "KRaft.cfg")).simulate(
         walkers=1 << 14, depth=80, seed=5, behaviors=1 << 18)
     assert s["status"] == "ok" and s["behaviors"] == 1 << 18
 

@@ -43,7 +43,7 @@ def test_tiny_chunks_and_table_growth(name):
 @pytest.mark.parametrize("name", sorted(SHIPPED))
 def test_shipped_configs_match_oracle(name):
     g = SHIPPED[name]
-    r = raftmc.check(os.path.join(ROOT, "configs", g["module"] + ".tla"), os.path.join(ROOT, g["cfg_path"]))
+    r = raftmc.Model(module=g["module"], cfg_path=os.path.join(ROOT, g["cfg_path"])).check()
     assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
     assert r["levels"] == g["levels"]
     assert r["status"] == "ok"
@@ -56,7 +56,7 @@ def test_tight_rows_from_the_previous_check(name):
     a second check of the same model packs rows to exactly that many message
     slots (smaller rows) and must reproduce every count."""
     g = SHIPPED[name]
-    m = raftmc.Model(os.path.join(ROOT, "configs", g["module"] + ".tla"), os.path.join(ROOT, g["cfg_path"]))
+    m = raftmc.Model(module=g["module"], cfg_path=os.path.join(ROOT, g["cfg_path"]))
     r1 = m.check()
     assert r1["max_msgs"] == g["max_msgs"]
     r2 = m.check()

@@ -46,7 +46,7 @@ def test_logical_shards_medium(name):
 
 def test_logical_shards_shipped_raft_cfg():
     g = SHIPPED["Raft_cfg"]
-    m = raftmc.Model(os.path.join(ROOT, "configs", "Raft.tla"), os.path.join(ROOT, g["cfg_path"]))
+    m = raftmc.Model(module="Raft", cfg_path=os.path.join(ROOT, g["cfg_path"]))
     same(m.check_logical(8), dict(g, status="ok"))
 
 

@@ -58,7 +58,7 @@ def test_cli_dump_trace(tmp_path):
     cfgp.write_text(g["cfg"])
     out = tmp_path / "Unsafe_TTrace.tla"
     exe = os.path.join(ROOT, "raft-tlaplus_amd", "build", "raftmc")
-    p = subprocess.run([exe, "-deadlock", "-config", str(cfgp), "-dumpTrace", "tla", str(out), g["module"] + ".tla"],
+    p = subprocess.run([exe, "-deadlock", "-config", str(cfgp), "-dumpTrace", "tla", str(out), "-module", g["module"]],
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 12, p.stdout + p.stderr  # 12 = invariant violated (TLC's exit code)
     assert "Error: Invariant %s is violated." % g["violated"] in p.stdout
@@ -66,7 +66,7 @@ def test_cli_dump_trace(tmp_path):
     assert len(parse_trace_states(out.read_text())) == g["trace_len"]
     assert "INIT TraceInit" in (tmp_path / "Unsafe_TTrace.cfg").read_text()
     pj = tmp_path / "t.json"
-    p = subprocess.run([exe, "-deadlock", "-config", str(cfgp), "-dumpTrace", "json", str(pj), g["module"] + ".tla"],
+    p = subprocess.run([exe, "-deadlock", "-config", str(cfgp), "-dumpTrace", "json", str(pj), "-module", g["module"]],
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 12
     assert len(json.loads(pj.read_text())["states"]) == g["trace_len"]

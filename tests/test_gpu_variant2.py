@@ -49,7 +49,7 @@ def test_variant2_shipped_cfg():
     """PullRaftVariant2.cfg's constants: 891 same-level hidden-variable collisions
     in TLC order (2,615 if the last successor won)."""
     g = SHIPPED["PullRaftVariant2_cfg"]
-    m = raftmc.Model(os.path.join(ROOT, "configs", "PullRaftVariant2.tla"), os.path.join(ROOT, g["cfg_path"]))
+    m = raftmc.Model(module="PullRaftVariant2", cfg_path=os.path.join(ROOT, g["cfg_path"]))
     for kw in (dict(), dict(chunk_parents=10000)):
         r = m.check(**kw)
         assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \

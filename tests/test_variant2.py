@@ -75,7 +75,7 @@ def test_cpu_engine_shipped_cfg_first_wins():
     count (891; the reverse-order probe counts 2,615)."""
     g = SHIPPED["PullRaftVariant2_cfg"]
     ROOT = os.path.dirname(HERE)
-    m = raftmc.Model(os.path.join(ROOT, "configs", "PullRaftVariant2.tla"), os.path.join(ROOT, g["cfg_path"]))
+    m = raftmc.Model(module="PullRaftVariant2", cfg_path=os.path.join(ROOT, g["cfg_path"]))
     r = m.check_cpu(workers=8)
     assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == \
         (g["generated"], g["distinct"], g["depth"], g["levels"])

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 CFG=${CFG:-Raft_n3v2e2}
 for i in 1 2; do
   for v in ${BUILDS:-build build_b}; do
-    timeout -k 10 120 ./raft-tlaplus_amd/$v/raftmc -deadlock -json configs/Raft.tla -config configs/$CFG.cfg > gpurun_out/ab_$v.txt 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab_$v.txt; exit 1; }
+    timeout -k 10 120 ./raft-tlaplus_amd/$v/raftmc -deadlock -json -module Raft -config configs/$CFG.cfg > gpurun_out/ab_$v.txt 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab_$v.txt; exit 1; }
     echo "$v $(tail -1 gpurun_out/ab_$v.txt)"
   done
 done

@@ -8,5 +8,5 @@ timeout -k 10 180 python -u __graft_entry__.py > gpurun_out/smoke.log 2>&1; rc=$
 ok $rc || exit $rc
 timeout -k 10 420 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc" | tee -a gpurun_out/pytest_gpu.log
 ok $rc || exit $rc
-timeout -k 10 120 ./raft-tlaplus_amd/build/raftmc -deadlock -json -v configs/Raft.tla -config configs/Raft.cfg > gpurun_out/raft_cfg.txt 2>&1; rc=$?; echo "raftmc rc=$rc" | tee -a gpurun_out/raft_cfg.txt
+timeout -k 10 120 ./raft-tlaplus_amd/build/raftmc -deadlock -json -v -module Raft -config configs/Raft.cfg > gpurun_out/raft_cfg.txt 2>&1; rc=$?; echo "raftmc rc=$rc" | tee -a gpurun_out/raft_cfg.txt
 exit 0

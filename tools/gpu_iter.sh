@@ -19,7 +19,7 @@ if [ "${BENCH:-1}" = 1 ]; then
 fi
 for cfg in $RUNS; do
   mod=$cfg; case $cfg in Raft_*) mod=Raft;; PullRaft_*) mod=PullRaft;; RaftFsync_*) mod=RaftFsync;; FlexibleRaft_*) mod=FlexibleRaft;; KRaft_*) mod=KRaft;; esac
-  timeout -k 10 ${RUN_LIMIT:-240} ./raft-tlaplus_amd/build/raftmc -deadlock -json -v $RUN_ARGS configs/$mod.tla -config configs/$cfg.cfg > gpurun_out/run_${TAG}_$cfg.txt 2>&1; rc=$?
+  timeout -k 10 ${RUN_LIMIT:-240} ./raft-tlaplus_amd/build/raftmc -deadlock -json -v $RUN_ARGS -module $mod -config configs/$cfg.cfg > gpurun_out/run_${TAG}_$cfg.txt 2>&1; rc=$?
   echo "$cfg rc=$rc"; tail -2 gpurun_out/run_${TAG}_$cfg.txt
   [ $rc -eq 0 ] || [ $rc -eq 12 ] || [ $rc -eq 13 ] || exit $rc
 done

@@ -15,7 +15,7 @@ timeout -k 10 420 python -u bench.py --workload $WL $BENCH_ARGS > $O/bench.json 
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 $R/bench.py --workload $WL --no-cpu-baseline --steps 2 --warmup 1 > $O/kt.log 2>&1 || { echo "kernel-trace failed"; exit 1; }
-CLI="$R/raft-tlaplus_amd/build/raftmc -deadlock -json $R/configs/Raft.tla -config $R/configs/$CFG.cfg"
+CLI="$R/raft-tlaplus_amd/build/raftmc -deadlock -json -module Raft -config $R/configs/$CFG.cfg"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc1 -o run --output-format csv -- $CLI > $O/pmc1.log 2>&1 || { echo "pmc1 failed"; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc2 -o run --output-format csv -- $CLI > $O/pmc2.log 2>&1 || { echo "pmc2 failed"; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $O/pmc3 -o run --output-format csv -- $CLI > $O/pmc3.log 2>&1 || { echo "pmc3 failed"; exit 1; }

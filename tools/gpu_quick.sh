@@ -9,7 +9,7 @@ echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 for cfg in ${CFGS:-Raft_n3v2e2}; do
   mod=$cfg; case $cfg in Raft_*) mod=Raft;; esac
-  timeout -k 10 ${RUN_LIMIT:-200} ./raft-tlaplus_amd/build/raftmc -deadlock -json configs/$mod.tla -config configs/$cfg.cfg > gpurun_out/run_${TAG}_$cfg.txt 2>&1; rc=$?
+  timeout -k 10 ${RUN_LIMIT:-200} ./raft-tlaplus_amd/build/raftmc -deadlock -json -module $mod -config configs/$cfg.cfg > gpurun_out/run_${TAG}_$cfg.txt 2>&1; rc=$?
   echo "$cfg rc=$rc"; tail -1 gpurun_out/run_${TAG}_$cfg.txt
   [ $rc -eq 0 ] || [ $rc -eq 12 ] || exit $rc
 done

@@ -9,6 +9,6 @@ if [ -z "$NOTEST" ]; then
   tail -1 gpurun_out/pytest_gpu.log
 fi
 for i in 1 2 3; do
-  timeout -k 10 120 ./raft-tlaplus_amd/build/raftmc -deadlock -json configs/Raft.tla -config configs/$CFG.cfg > gpurun_out/ab.txt 2>&1 || { echo "raftmc failed"; tail -5 gpurun_out/ab.txt; exit 1; }
+  timeout -k 10 120 ./raft-tlaplus_amd/build/raftmc -deadlock -json -module Raft -config configs/$CFG.cfg > gpurun_out/ab.txt 2>&1 || { echo "raftmc failed"; tail -5 gpurun_out/ab.txt; exit 1; }
   tail -1 gpurun_out/ab.txt
 done

@@ -10,7 +10,7 @@ echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_r02a.log
 [ $rc -eq 0 ] || exit $rc
 for cfg in ${RUNGS:-FlexibleRaft Raft_n3v2e3}; do
   mod=$cfg; case $cfg in Raft_*) mod=Raft;; esac
-  timeout -k 10 ${RUNG_LIMIT:-200} ./raft-tlaplus_amd/build/raftmc -deadlock -json -v configs/$mod.tla -config configs/$cfg.cfg > gpurun_out/ladder_r02_$cfg.txt 2>&1
+  timeout -k 10 ${RUNG_LIMIT:-200} ./raft-tlaplus_amd/build/raftmc -deadlock -json -v -module $mod -config configs/$cfg.cfg > gpurun_out/ladder_r02_$cfg.txt 2>&1
   rc=$?; echo "rc=$rc" >> gpurun_out/ladder_r02_$cfg.txt
   echo "$cfg rc=$rc"; tail -4 gpurun_out/ladder_r02_$cfg.txt
   [ $rc -eq 0 ] || [ $rc -eq 12 ] || [ $rc -eq 13 ] || [ $rc -eq 124 ] || exit $rc

@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 CFG=${CFG:-Raft_n3v2e2}
 for w in ${SHARDS:-1 8}; do
   timeout -k 10 ${LIMIT:-240} rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/shprof_$w -o run -- \
-    ./raft-tlaplus_amd/build/raftmc -deadlock -json -shards $w configs/Raft.tla -config configs/$CFG.cfg > gpurun_out/shprof_$w.txt 2>&1; rc=$?
+    ./raft-tlaplus_amd/build/raftmc -deadlock -json -shards $w -module Raft -config configs/$CFG.cfg > gpurun_out/shprof_$w.txt 2>&1; rc=$?
   echo "W=$w rc=$rc"; tail -1 gpurun_out/shprof_$w.txt
   [ $rc -eq 0 ] || exit $rc
 done
