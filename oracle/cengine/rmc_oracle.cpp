@@ -823,8 +823,50 @@ bool CommittedEntriesReachMajority(const State& s) {  // Raft.tla:625-636
   }
   return false;
 }
+// The classic Raft properties, opt-in (not defined by the reference's specs);
+// restated from their TLA+ text in INTEGRATION.md.
+bool ElectionSafety(const State& s) {
+  for (int a = 0; a < C.N; a++)
+    for (int b = 0; b < C.N; b++)
+      if (a != b && s.st[a] == LEADER && s.st[b] == LEADER && s.term[a] == s.term[b]) return false;
+  return true;
+}
+bool LogMatching(const State& s) {
+  for (int a = 0; a < C.N; a++)
+    for (int b = 0; b < C.N; b++)
+      for (int i = 1; i <= std::min(s.loglen[a], s.loglen[b]); i++)
+        if (log_at(s, a, i).term == log_at(s, b, i).term)
+          for (int k = 1; k <= i; k++)
+            if (!entry_eq(log_at(s, a, k), log_at(s, b, k))) return false;
+  return true;
+}
+bool LeaderCompleteness(const State& s) {
+  for (int l = 0; l < C.N; l++) {
+    if (s.st[l] != LEADER) continue;
+    bool newest = true;
+    for (int k = 0; k < C.N; k++) if (s.term[k] > s.term[l]) newest = false;
+    if (!newest) continue;
+    for (int k = 0; k < C.N; k++)
+      for (int i = 1; i <= std::min(s.commit[k], s.loglen[k]); i++)
+        if (!(i <= s.loglen[l] && entry_eq(log_at(s, l, i), log_at(s, k, i)))) return false;
+  }
+  return true;
+}
+bool StateMachineSafety(const State& s) {
+  for (int a = 0; a < C.N; a++)
+    for (int b = 0; b < C.N; b++) {
+      const int c = std::min(std::min(s.commit[a], s.commit[b]), std::min(s.loglen[a], s.loglen[b]));
+      for (int i = 1; i <= c; i++)
+        if (!entry_eq(log_at(s, a, i), log_at(s, b, i))) return false;
+    }
+  return true;
+}
 const char* check_invariants(const State& s) {
   for (auto& n : C.inv_order) {
+    if (n == "ElectionSafety" && !ElectionSafety(s)) return "ElectionSafety";
+    if (n == "LogMatching" && !LogMatching(s)) return "LogMatching";
+    if (n == "LeaderCompleteness" && !LeaderCompleteness(s)) return "LeaderCompleteness";
+    if (n == "StateMachineSafety" && !StateMachineSafety(s)) return "StateMachineSafety";
     if (n == "LeaderHasAllAckedValues" && !LeaderHasAllAckedValues(s)) return "LeaderHasAllAckedValues";
     if (n == "NoLogDivergence" && !NoLogDivergence(s)) return "NoLogDivergence";
     if (n == "CommittedEntriesReachMajority" && !CommittedEntriesReachMajority(s)) return "CommittedEntriesReachMajority";

@@ -43,7 +43,9 @@ class RaftSpec:
         self.perms = permutations(self.N)
         table = {"LeaderHasAllAckedValues": self.LeaderHasAllAckedValues,
                  "NoLogDivergence": self.NoLogDivergence,
-                 "CommittedEntriesReachMajority": self.CommittedEntriesReachMajority}
+                 "CommittedEntriesReachMajority": self.CommittedEntriesReachMajority,
+                 "ElectionSafety": self.ElectionSafety, "LogMatching": self.LogMatching,
+                 "LeaderCompleteness": self.LeaderCompleteness, "StateMachineSafety": self.StateMachineSafety}
         self.invariants = [(n, table[n]) for n in invariants]
 
     def setup(self, consts):
@@ -484,6 +486,47 @@ class RaftSpec:
                        seq_get(s["log"][j], ci) == seq_get(s["log"][i], ci) for j in q):
                     return True
         return False
+
+    # The classic Raft safety properties (Ongaro, Fig. 3.2), opt-in extras: the
+    # reference's specs do not define them.  Restated from the
+    # TLA+ text given in INTEGRATION.md, literally (sets of servers, SubSeq).
+    def ElectionSafety(self, s):
+        # \A s1, s2 : s1 # s2 /\ both Leader => currentTerm[s1] # currentTerm[s2]
+        return not any(s1 != s2 and s["state"][s1] == LEADER and s["state"][s2] == LEADER and
+                       s["currentTerm"][s1] == s["currentTerm"][s2]
+                       for s1 in self.Server for s2 in self.Server)
+
+    def LogMatching(self, s):
+        # \A s1, s2, i \in 1..Min(Len, Len) : same term at i => SubSeq(.., 1, i) equal
+        lg = s["log"]
+        for s1 in self.Server:
+            for s2 in self.Server:
+                for i in range(1, min(len(lg[s1]), len(lg[s2])) + 1):
+                    if seq_get(lg[s1], i).term == seq_get(lg[s2], i).term and lg[s1][:i] != lg[s2][:i]:
+                        return False
+        return True
+
+    def LeaderCompleteness(self, s):
+        # a leader whose term no server exceeds holds every committed entry
+        lg, ci = s["log"], s["commitIndex"]
+        for l in self.Server:
+            if s["state"][l] != LEADER or any(s["currentTerm"][k] > s["currentTerm"][l] for k in self.Server):
+                continue
+            for k in self.Server:
+                for i in range(1, min(ci[k], len(lg[k])) + 1):
+                    if not (i <= len(lg[l]) and seq_get(lg[l], i) == seq_get(lg[k], i)):
+                        return False
+        return True
+
+    def StateMachineSafety(self, s):
+        # committed prefixes (bounded by Len) agree
+        lg, ci = s["log"], s["commitIndex"]
+        for s1 in self.Server:
+            for s2 in self.Server:
+                for i in range(1, min(ci[s1], ci[s2], len(lg[s1]), len(lg[s2])) + 1):
+                    if seq_get(lg[s1], i) != seq_get(lg[s2], i):
+                        return False
+        return True
 
     # ----------------------------------------------------- VIEW and SYMMETRY
     def view_vars(self):

@@ -67,6 +67,7 @@ int main(int argc, char** argv) {
     else if (k == "-gpus") o.n_gpus = atoi(val().c_str());
     else if (k == "-msgcap") o.msg_cap_K = (uint32_t)atoi(val().c_str());
     else if (k == "-hashslots") o.hash_slots = strtoull(val().c_str(), nullptr, 10);
+    else if (k == "-hostfrontier") o.host_frontier = atoi(val().c_str());  // -1 never, 0 auto, 1 always
     else if (k == "-maxdepth") o.max_depth = atoi(val().c_str());
     else if (k == "-chunk") o.chunk_parents = (uint32_t)atoi(val().c_str());
     else if (k == "-simulate") simulate = true;
@@ -92,7 +93,7 @@ int main(int argc, char** argv) {
     else tla = k;
   }
   if (tla.empty() == module.empty() || (!module.empty() && cfg.empty())) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-checkpoint MIN] [-metadir DIR] [-recover DIR] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-hostfrontier -1|0|1] [-checkpoint MIN] [-metadir DIR] [-recover DIR] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
                     "       raftmc [options] -module M -config X.cfg   (the built-in lowering of module M, no .tla)\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;

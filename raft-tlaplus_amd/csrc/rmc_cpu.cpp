@@ -432,6 +432,7 @@ extern "C" int rmc_check_cpu(rmc_model* m, const rmc_options* o, rmc_result* out
     if (o->fp_bits && o->fp_bits != 64) throw std::runtime_error("fp_bits 128 is offered by the single-GPU search (rmc_check) only");
     if ((o->checkpoint_dir && *o->checkpoint_dir) || (o->recover_dir && *o->recover_dir))
       throw std::runtime_error("checkpoint / recover are offered by the single-GPU search (rmc_check) only");
+    if (o->host_frontier == 1) throw std::runtime_error("host_frontier = 1 is offered by the single-GPU search (rmc_check) only");
     m->kmax_user = 0;
     int rc;
     while ((rc = rmcx::check_cpu(m, o, out)) == 1) memset(out, 0, sizeof *out);

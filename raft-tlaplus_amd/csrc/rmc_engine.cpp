@@ -16,6 +16,9 @@
 #include <set>
 #include <sstream>
 #include <sys/stat.h>
+#include <dirent.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include <cerrno>
 #include <string>
 #include <vector>
@@ -415,9 +418,14 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
                                                : n == "TestInv" ? -2 : -1;
       if (spec == KRAFT && n == "NeverTwoLeadersInSameEpoch") id = 3;  // KRaft.tla:916-921
       if (spec == KRAFT && n == "NoIllegalState") id = 4;              // KRaft.tla:887-889
+      // the classic Raft properties, opt-in (rmc_spec.h)
+      if (spec != KRAFT && n == "ElectionSafety") id = 5;
+      if (spec != KRAFT && n == "LogMatching") id = 6;
+      if (spec != KRAFT && n == "LeaderCompleteness") id = 7;
+      if (spec != KRAFT && n == "StateMachineSafety") id = 8;
       if (id == -2) continue;  // TestInv == TRUE
       if (id < 0) throw std::runtime_error("unsupported invariant " + n);
-      if (M.ninv >= 5) throw std::runtime_error("too many invariants");
+      if (M.ninv >= 9) throw std::runtime_error("too many invariants");
       M.inv[M.ninv++] = id;
       m->inv_names.push_back(n);
     }
@@ -756,12 +764,14 @@ struct HostReadback {
 struct Arena {
   // table/table2: the fingerprint set and its growth target
   DevBuf table, table2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
+  DevBuf hwin_in[2], hwin_out[2];  // host-frontier windows: parents in, new rows out (double-buffered)
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   HostReadback* hrb = nullptr;
   void release() {
     if (hrb) (void)hipHostFree(hrb);
     hrb = nullptr;
-    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
+    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp,
+                      &hwin_in[0], &hwin_in[1], &hwin_out[0], &hwin_out[1]})
       b->release();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
@@ -778,6 +788,17 @@ Arena& arena_for_current_device() {
 }
 
 void set_last_error(const std::string& s) { g_last_error = s; }
+
+// The single-GPU search's cached buffers on the current device.  The sharded
+// entry points call this (and rmc_check calls release_shard_buffers): a
+// process that alternates the two must not have one's cache starve the other.
+void release_single_buffers() {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  auto it = g_arenas.find(dev);
+  if (it != g_arenas.end()) it->second->release();
+}
 
 void replay_trace(rmc_model* m, const std::vector<int>& binds, int last_b, int status, std::string& message,
                   rmc_result* res) {
@@ -813,16 +834,39 @@ void replay_trace(rmc_model* m, const std::vector<int>& binds, int last_b, int s
 // ---- checkpoint / recover (TLC -checkpoint / -recover, its states/ directory)
 // A snapshot is taken at a level boundary: the fingerprint set (raw entries),
 // the next level's frontier (packed rows), the trace records of every state
-// so far, and the counts.  checkpoint.meta is written last (after the binary
-// files are complete), so a directory without it holds no snapshot.
+// so far, and the counts.  Each snapshot goes into a fresh subdirectory
+// (snap-<seq>); its files are fsync'd, then checkpoint.meta is replaced
+// atomically (written to a temporary, fsync'd, renamed, directory fsync'd) to
+// name it, and only then is the previous snapshot's subdirectory removed -- as
+// TLC keeps its previous checkpoint valid until the new one is complete, a
+// crash, kill or full disk at any point leaves one complete snapshot.
 struct Ckpt {
   unsigned long long sig = 0, slots = 0, generated = 0, distinct = 0, cur_base = 0, cur_n = 0, hidden = 0;
   unsigned depth = 0;
   uint32_t kmax = 0;
   int fpw = 1;
   double rate = 4.0;
+  unsigned long long seq = 0;  // snapshot sequence number; files in snap-<seq>/
   std::vector<std::pair<unsigned long long, unsigned long long>> levels;
 };
+static std::string ckpt_subdir(unsigned long long seq) { return "snap-" + std::to_string(seq); }
+static void fsync_dir(const std::string& dir) {
+  int fd = open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (fd < 0) throw std::runtime_error("checkpoint: cannot open " + dir);
+  int rc = fsync(fd);
+  close(fd);
+  if (rc != 0) throw std::runtime_error("checkpoint: cannot sync " + dir);
+}
+static void remove_tree(const std::string& dir) {
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) {
+      std::string n = e->d_name;
+      if (n != "." && n != "..") (void)unlink((dir + "/" + n).c_str());
+    }
+    closedir(d);
+  }
+  (void)rmdir(dir.c_str());
+}
 unsigned long long model_signature(const rmc_model* m) {
   const Model& M = m->M;
   char b[320];
@@ -843,6 +887,7 @@ static void ckpt_write(const std::string& path, const void* dev, size_t bytes, v
     HIPCHK(hipMemcpy(stage, (const char*)dev + o, n, hipMemcpyDeviceToHost));
     if (fwrite(stage, 1, n, f) != n) { fclose(f); throw std::runtime_error("checkpoint: short write to " + tmp); }
   }
+  if (fflush(f) != 0 || fsync(fileno(f)) != 0) { fclose(f); throw std::runtime_error("checkpoint: cannot sync " + tmp); }
   if (fclose(f) != 0 || rename(tmp.c_str(), path.c_str()) != 0)
     throw std::runtime_error("checkpoint: cannot finish " + path);
 }
@@ -859,16 +904,45 @@ static void ckpt_read(const std::string& path, void* dev, size_t bytes, void* st
   }
   fclose(f);
 }
+// The frontier file of a snapshot taken with w0-word rows, loaded as w-word rows
+// (w >= w0: a resumed check that overflowed the snapshot's message capacity
+// re-runs with more slots; the extra slots are empty -- the message count is in
+// the header word -- and fingerprints, ranks and bindings do not depend on it).
+static void ckpt_read_rows(const std::string& path, uint32_t* dev, size_t n, size_t w0, size_t w, void* stage,
+                           size_t stage_bytes) {
+  if (w == w0) return ckpt_read(path, dev, n * w * 4, stage, stage_bytes);
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("recover: cannot read " + path);
+  fseek(f, 0, SEEK_END);
+  if ((size_t)ftell(f) != n * w0 * 4) { fclose(f); throw std::runtime_error("recover: " + path + " has the wrong size"); }
+  fseek(f, 0, SEEK_SET);
+  const size_t rows = stage_bytes / (w * 4);
+  std::vector<uint32_t> in(rows * w0);
+  uint32_t* out = (uint32_t*)stage;
+  for (size_t r0 = 0; r0 < n; r0 += rows) {
+    const size_t k = std::min(rows, n - r0);
+    if (fread(in.data(), 4, k * w0, f) != k * w0) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
+    for (size_t r = 0; r < k; r++) {
+      memcpy(out + r * w, in.data() + r * w0, w0 * 4);
+      memset(out + r * w + w0, 0, (w - w0) * 4);
+    }
+    HIPCHK(hipMemcpy(dev + r0 * w, out, k * w * 4, hipMemcpyHostToDevice));
+  }
+  fclose(f);
+}
 static void ckpt_write_meta(const std::string& dir, const rmc_model* m, const Ckpt& c) {
   const std::string path = dir + "/checkpoint.meta", tmp = path + ".tmp";
   FILE* f = fopen(tmp.c_str(), "w");
   if (!f) throw std::runtime_error("checkpoint: cannot write " + tmp);
-  fprintf(f, "raftmc-checkpoint 1\nmodule %s\nsignature %016llx\nkmax %u\nfpw %d\nslots %llu\ngenerated %llu\n"
-             "distinct %llu\ndepth %u\ncur_base %llu\ncur_n %llu\nhidden %llu\nrate %.17g\nlevels %zu\n",
-          m->module.c_str(), c.sig, c.kmax, c.fpw, c.slots, c.generated, c.distinct, c.depth, c.cur_base, c.cur_n,
-          c.hidden, c.rate, c.levels.size());
+  fprintf(f, "raftmc-checkpoint 2\nmodule %s\nsnapshot %llu\nsignature %016llx\nkmax %u\nfpw %d\nslots %llu\n"
+             "generated %llu\ndistinct %llu\ndepth %u\ncur_base %llu\ncur_n %llu\nhidden %llu\nrate %.17g\n"
+             "levels %zu\n",
+          m->module.c_str(), c.seq, c.sig, c.kmax, c.fpw, c.slots, c.generated, c.distinct, c.depth, c.cur_base,
+          c.cur_n, c.hidden, c.rate, c.levels.size());
   for (auto& l : c.levels) fprintf(f, "%llu %llu\n", l.first, l.second);
+  if (fflush(f) != 0 || fsync(fileno(f)) != 0) { fclose(f); throw std::runtime_error("checkpoint: cannot sync " + tmp); }
   if (fclose(f) != 0 || rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("checkpoint: cannot finish " + path);
+  fsync_dir(dir);
 }
 static Ckpt ckpt_read_meta(const std::string& dir, const rmc_model* m) {
   const std::string path = dir + "/checkpoint.meta";
@@ -878,11 +952,11 @@ static Ckpt ckpt_read_meta(const std::string& dir, const rmc_model* m) {
   char module[128] = {0};
   int ver = 0;
   size_t nl = 0;
-  int ok = fscanf(f, "raftmc-checkpoint %d module %127s signature %llx kmax %u fpw %d slots %llu generated %llu "
-                     "distinct %llu depth %u cur_base %llu cur_n %llu hidden %llu rate %lg levels %zu",
-                  &ver, module, &c.sig, &c.kmax, &c.fpw, &c.slots, &c.generated, &c.distinct, &c.depth, &c.cur_base,
-                  &c.cur_n, &c.hidden, &c.rate, &nl);
-  if (ok != 14 || ver != 1) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
+  int ok = fscanf(f, "raftmc-checkpoint %d module %127s snapshot %llu signature %llx kmax %u fpw %d slots %llu "
+                     "generated %llu distinct %llu depth %u cur_base %llu cur_n %llu hidden %llu rate %lg levels %zu",
+                  &ver, module, &c.seq, &c.sig, &c.kmax, &c.fpw, &c.slots, &c.generated, &c.distinct, &c.depth,
+                  &c.cur_base, &c.cur_n, &c.hidden, &c.rate, &nl);
+  if (ok != 15 || ver != 2) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
   for (size_t k = 0; k < nl; k++) {
     unsigned long long g = 0, d = 0;
     if (fscanf(f, "%llu %llu", &g, &d) != 2) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
@@ -892,6 +966,47 @@ static Ckpt ckpt_read_meta(const std::string& dir, const rmc_model* m) {
   if (m->module != module) throw std::runtime_error(std::string("recover: the checkpoint is of module ") + module);
   return c;
 }
+
+size_t host_frontier_limit() {
+  if (const char* e = getenv("RMC_HOST_FRONTIER_GIB")) return (size_t)(atof(e) * 1073741824.0);
+  unsigned long long avail_kb = 0;
+  if (FILE* f = fopen("/proc/meminfo", "r")) {
+    char line[256];
+    while (fgets(line, sizeof line, f))
+      if (sscanf(line, "MemAvailable: %llu kB", &avail_kb) == 1) break;
+    fclose(f);
+  }
+  const size_t avail = (size_t)avail_kb * 1024;
+  return std::min<size_t>(avail / 5 * 4, 200ULL << 30);
+}
+
+// The copy stream and events of the host frontier, created on first use.
+struct HostFrontierStreams {
+  hipStream_t cs = nullptr;
+  hipEvent_t in[2], mat[2], out[2];
+  void init(hipStream_t compute) {
+    if (cs) return;
+    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++) {
+      HIPCHK(hipEventCreateWithFlags(&in[k], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&mat[k], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&out[k], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(in[k], compute));
+      HIPCHK(hipEventRecord(mat[k], compute));
+      HIPCHK(hipEventRecord(out[k], compute));
+    }
+  }
+  ~HostFrontierStreams() {
+    if (!cs) return;
+    (void)hipStreamSynchronize(cs);
+    for (int k = 0; k < 2; k++) {
+      (void)hipEventDestroy(in[k]);
+      (void)hipEventDestroy(mat[k]);
+      (void)hipEventDestroy(out[k]);
+    }
+    (void)hipStreamDestroy(cs);
+  }
+};
 
 int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   auto t0 = std::chrono::steady_clock::now();
@@ -903,23 +1018,28 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   if (kmax > 120) kmax = 120;
   const bool recovering = opt->recover_dir && *opt->recover_dir;
   Ckpt rc;
-  if (recovering) {  // the snapshot's row layout
+  size_t snap_words = 0;  // row width of the snapshot's frontier file
+  if (recovering) {  // verified against the snapshot's own row layout
     rc = ckpt_read_meta(opt->recover_dir, m);
-    kmax = rc.kmax;
+    finalize_model(m, rc.kmax);
+    M.fpw = opt->fp_bits == 128 ? 2 : 1;
+    if (M.kmax != (int)rc.kmax || M.fpw != rc.fpw || model_signature(m) != rc.sig)
+      throw std::runtime_error(std::string("recover: the checkpoint in ") + opt->recover_dir +
+                               " is of a different model, constants or fingerprint width");
+    snap_words = (size_t)M.words;
+    // a resumed level that overflowed the snapshot's message capacity re-runs
+    // from the same snapshot with more slots (its rows are widened on load)
+    kmax = std::max(kmax, rc.kmax);
   }
   finalize_model(m, kmax);
   M.fpw = opt->fp_bits == 128 ? 2 : 1;
-  if (recovering) {
-    if (M.kmax != rc.kmax || M.fpw != rc.fpw || model_signature(m) != rc.sig)
-      throw std::runtime_error(std::string("recover: the checkpoint in ") + opt->recover_dir +
-                               " is of a different model, constants or fingerprint width");
-  }
   const int ew = 2 * M.fpw;  // fingerprint-set entry width in 64-bit words
   HIPCHK(upload_model(M));
   hipStream_t stream;
   HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   const size_t W = (size_t)M.words;
   res->state_bytes = (uint32_t)(W * 4);
+  const auto t_model = std::chrono::steady_clock::now();
 
   // ---- sizing
   // Fingerprint set: starts at hash_slots (or at the size the last check of
@@ -952,8 +1072,12 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   GrowBuf &fa = A.fa, &fb = A.fb, &trp = A.trp, &trb = A.trb;
   table.ensure(slots * ew * 8);
   HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * ew * 8, stream));
-  fa.ensure(fcap * W * 4);
-  fb.ensure(fcap * W * 4);
+  if (opt->host_frontier != 1) {
+    fa.ensure(fcap * W * 4);
+    fb.ensure(fcap * W * 4);
+  } else {  // always host: only Init (or a recovered level) passes through the device
+    fa.ensure((recovering ? std::max(1ULL, rc.cur_n) : 1ULL) * W * 4);
+  }
   cslot.ensure(cand_cap * 8);
   cob.ensure(cand_cap * 4);
   cwin.ensure(cand_cap * 2);
@@ -981,6 +1105,11 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     HIPCHK(hipMemcpyAsync(stbuf.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
   };
   reset_status();
+  HIPCHK(hipStreamSynchronize(stream));
+  if (opt->verbose)
+    fprintf(stderr, "[rmc] setup: runtime + model upload %.3fs, buffers %.3fs (fingerprint set 2^%d slots)\n",
+            std::chrono::duration<double>(t_model - t0).count(),
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_model).count(), __builtin_ctzll(slots));
 
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -1015,17 +1144,6 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     if (opt->verbose)
       fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs)\n", __builtin_ctzll(slots), secs(tr0, now()));
     return true;
-  };
-  auto t_fit = [&](unsigned long long need) {
-    if (need * 4 <= slots * 3) return;
-    if (!full_ok) {
-      unsigned long long nslots = slots;
-      while (need * 2 > nslots) nslots <<= 1;  // to <= 0.5 after growing
-      if (t_grow(nslots)) return;
-      full_ok = true;
-      if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(slots));
-    }
-    if (need * 10 > slots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
   };
 
   // ---- level 1: Init (Raft.tla:213-218)
@@ -1073,9 +1191,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     return ck_stage;
   };
   if (recovering) {  // resume from the snapshot instead of Init
-    const std::string dir = opt->recover_dir;
+    const std::string dir = std::string(opt->recover_dir) + "/" + ckpt_subdir(rc.seq);
     ckpt_read(dir + "/fpset.bin", table.p, slots * ew * 8, stage(), ck_stage_bytes);
-    ckpt_read(dir + "/frontier.bin", fa.p, rc.cur_n * W * 4, stage(), ck_stage_bytes);
+    ckpt_read_rows(dir + "/frontier.bin", fa.as<uint32_t>(), rc.cur_n, snap_words, W, stage(), ck_stage_bytes);
     ckpt_read(dir + "/trace_parent.bin", trp.p, rc.distinct * 8, stage(), ck_stage_bytes);
     ckpt_read(dir + "/trace_bind.bin", trb.p, rc.distinct * 2, stage(), ck_stage_bytes);
     generated = rc.generated;
@@ -1107,6 +1225,81 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   };
   uint32_t* cur = fa.as<uint32_t>();
   uint32_t* nxt = fb.as<uint32_t>();
+  // ---- host frontier (rmc_options.host_frontier: -1 never, 0 when HBM runs
+  // out, 1 always): the current and next level live in pinned host pages and
+  // stream through two input and two output windows in HBM; the fingerprint
+  // set and the trace records stay on the device.
+  const int hf_opt = opt->host_frontier;
+  bool hf = false;
+  HostPagePool pool;
+  const size_t row_bytes = W * 4;
+  size_t page_rows = std::max<size_t>(1, (256ULL << 20) / row_bytes);
+  // test hooks: RMC_HOST_PAGE_ROWS (small pages: rows straddle many), and
+  // RMC_HOST_FRONTIER_AT=L (auto mode moves to the host before level L's
+  // second chunk) or L:grow (as if the next-level buffer's growth ran out of
+  // HBM in that chunk)
+  if (const char* e = getenv("RMC_HOST_PAGE_ROWS")) page_rows = std::max<long long>(1, atoll(e));
+  unsigned hf_force_level = 0;
+  bool hf_force_grow = false;
+  if (const char* e = getenv("RMC_HOST_FRONTIER_AT")) {
+    hf_force_level = (unsigned)atoi(e);
+    hf_force_grow = strstr(e, ":grow") != nullptr;
+  }
+  pool.page_bytes = page_rows * row_bytes;
+  pool.limit = host_frontier_limit();
+  HostLevel hcur, hnxt;
+  hcur.init(page_rows, row_bytes);
+  hnxt.init(page_rows, row_bytes);
+  struct LevelPagesGuard {  // every exit path returns the levels' pages to the pool (freed with it)
+    HostLevel &a, &b;
+    HostPagePool& pool;
+    ~LevelPagesGuard() { a.clear(pool); b.clear(pool); }
+  } level_pages_guard{hcur, hnxt, pool};
+  HostFrontierStreams hs;
+  unsigned long long hwin_c0[2] = {~0ULL, ~0ULL};  // first row of the chunk each input window holds
+  unsigned long long lvl_c0 = 0, lvl_next_n = 0;   // chunk-loop position (for a switch to the host frontier)
+  double hf_copy_s = 0;
+  // Move the current level (all of it) and the next level so far to host
+  // pages, free the device frontiers, and continue in host-frontier mode.
+  auto enter_hf = [&]() {
+    auto th0 = std::chrono::steady_clock::now();
+    HIPCHK(hipStreamSynchronize(stream));
+    hs.init(stream);
+    hcur.init(page_rows, row_bytes);
+    hnxt.init(page_rows, row_bytes);
+    hcur.reserve(cur_n, pool);
+    hcur.d2h_append(cur, cur_n, hs.cs);
+    hnxt.reserve(lvl_next_n, pool);
+    hnxt.d2h_append(nxt, lvl_next_n, hs.cs);
+    HIPCHK(hipStreamSynchronize(hs.cs));
+    if (lvl_c0 > chunk) hcur.recycle_below(lvl_c0 - chunk, pool);
+    fa.release();
+    fb.release();
+    cur = nxt = nullptr;
+    hf = true;
+    hwin_c0[0] = hwin_c0[1] = ~0ULL;
+    A.hwin_in[0].ensure(chunk * W * 4);
+    A.hwin_in[1].ensure(chunk * W * 4);
+    hf_copy_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - th0).count();
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] frontier moved to host memory at depth %u (%.1f GiB of pinned pages, limit %.1f GiB)\n",
+              depth, pool.allocated / 1073741824.0, pool.limit / 1073741824.0);
+  };
+  auto t_fit = [&](unsigned long long need) {
+    if (need * 4 <= slots * 3) return;
+    if (!full_ok) {
+      unsigned long long nslots = slots;
+      while (need * 2 > nslots) nslots <<= 1;  // to <= 0.5 after growing
+      if (t_grow(nslots)) return;
+      if (!hf && hf_opt == 0) {  // the device frontiers give their HBM to the set
+        enter_hf();
+        if (t_grow(nslots)) return;
+      }
+      full_ok = true;
+      if (opt->verbose) fprintf(stderr, "[rmc] fingerprint set stays at 2^%d slots (HBM full)\n", __builtin_ctzll(slots));
+    }
+    if (need * 10 > slots * 9) throw OutOfDeviceMemory("fingerprint set full (0.9 load) and HBM exhausted");
+  };
   double rate = recovering ? rc.rate : 4.0;  // new states per parent of the previous level (pre-sizes the table per chunk)
   auto last_ckpt = now();
   // the level that stopped the search (exact counts at the failing state, below)
@@ -1114,11 +1307,13 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   std::vector<ChunkLog> chunk_log;
   unsigned long long stop_level_base = 0, stop_level_n = 0, stop_gen_before = 0, stop_dist_before = 0;
   const uint32_t* stop_front = nullptr;
+  bool stop_hf = false;
   unsigned stop_level = 0;
-  auto fill_args = [&](LevelArgs& a, unsigned long long c0, unsigned long long n, unsigned level) {
+  auto fill_args = [&](LevelArgs& a, unsigned long long c0, unsigned long long n, unsigned level,
+                       const uint32_t* rows = nullptr) {
     memset(&a, 0, sizeof a);
     a.model = &M;
-    a.frontier = cur + c0 * W;
+    a.frontier = rows ? rows : cur + c0 * W;
     a.nparents = n;
     a.pbase = cur_base + c0;
     a.level = level;
@@ -1137,6 +1332,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     a.st = stbuf.as<DevStatus>();
   };
   try {
+  if (hf_opt == 1 && !hf) enter_hf();
   while (status == 0 && cur_n > 0) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     if (opt->time_limit > 0 && secs(t0, now()) >= opt->time_limit) { status = 4; message = "time limit"; break; }
@@ -1145,6 +1341,9 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     if (cur_base + cur_n + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
     unsigned long long next_n = 0, gen_lvl = 0;
     chunk_log.clear();
+    hwin_c0[0] = hwin_c0[1] = ~0ULL;
+    unsigned ck = 0;                       // chunk number within the level (host-frontier window parity)
+    unsigned long long prev_c0 = 0;        // first row of the previous chunk (kept for the recount)
     // the last k_materialize's snapshot (hrb->mat) is not examined yet; call
     // after a stream sync.  True when it ended the search (status 3 set, or
     // hst holds the error/violation keys).
@@ -1162,7 +1361,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       }
       return hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL;
     };
-    if (m->profile_level && level == m->profile_level) {
+    if (m->profile_level && level == m->profile_level && !hf) {
       // test hook (RMC_DIAG builds): k_expand on this level's first chunk,
       // stopped after each phase in turn; none of these launches inserts
       const unsigned long long n = std::min(chunk, cur_n);
@@ -1185,6 +1384,15 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     unsigned long long c0 = 0;
     while (c0 < cur_n) {
       unsigned long long n = std::min(chunk, cur_n - c0);
+      lvl_c0 = c0;
+      lvl_next_n = next_n;
+      if (!hf && hf_opt == 0 && !hf_force_grow && level == hf_force_level && c0 > 0) {
+        if (mat_pending) {
+          HIPCHK(hipStreamSynchronize(stream));
+          if (finish_mat()) break;
+        }
+        enter_hf();
+      }
       if (!opt->grow_on_overflow) {  // room for this chunk's new states (at the highest rate seen)
         const double r = std::max(rate, c0 ? (double)next_n / (double)c0 : 0.0);
         const unsigned long long need = distinct + next_n + (unsigned long long)((double)n * r * 1.25) + 1024;
@@ -1196,8 +1404,16 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
           t_fit(need);
         }
       }
+      const int hs_k = ck & 1;  // host frontier: this chunk's windows
+      if (hf && hwin_c0[hs_k] != c0) {  // parents not prefetched: copy them in (window free after chunk ck-2)
+        HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k], 0));
+        hcur.h2d(c0, n, A.hwin_in[hs_k].p, hs.cs);
+        HIPCHK(hipEventRecord(hs.in[hs_k], hs.cs));
+        hwin_c0[hs_k] = c0;
+      }
+      if (hf) HIPCHK(hipStreamWaitEvent(stream, hs.in[hs_k], 0));
       LevelArgs a;
-      fill_args(a, c0, n, level);
+      fill_args(a, c0, n, level, hf ? A.hwin_in[hs_k].as<uint32_t>() : nullptr);
       HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
       HIPCHK(hipEventRecord(te.a, stream));
       launch_expand(M.spec, M.N, a, stream);
@@ -1208,6 +1424,14 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       launch_scan(scantmp.p, scantmp.bytes, a.par_win, a.par_pos, n, stream);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(tm.b, stream));
+      if (hf && c0 + n < cur_n && hwin_c0[hs_k ^ 1] != c0 + n) {
+        // prefetch the next chunk's parents into the other window once chunk
+        // ck-1's k_materialize (which re-reads that window) is done
+        HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k ^ 1], 0));
+        hcur.h2d(c0 + n, std::min(chunk, cur_n - c0 - n), A.hwin_in[hs_k ^ 1].p, hs.cs);
+        HIPCHK(hipEventRecord(hs.in[hs_k ^ 1], hs.cs));
+        hwin_c0[hs_k ^ 1] = c0 + n;
+      }
       unsigned long long ncand = 0;
       HIPCHK(hipMemcpyAsync(hrb->segc, counters.p, 1024, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&hrb->lastpos, a.par_pos + (n - 1), 4, hipMemcpyDeviceToHost, stream));
@@ -1238,7 +1462,12 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       if ((hst.cap_flags & ~(1u << E_RETRY)) == (1u << E_CAP_TABLE) && !full_ok) {
         // the table filled up under this chunk: grow it and redo the chunk
         // (its inserts are idempotent; the next frontier was not touched)
-        if (!t_grow(slots * 2)) {
+        bool grown = t_grow(slots * 2);
+        if (!grown && !hf && hf_opt == 0) {  // the device frontiers give their HBM to the set
+          enter_hf();
+          grown = t_grow(slots * 2);
+        }
+        if (!grown) {
           full_ok = true;
           status = 3;
           message = "capacity overflow: fingerprint set full and HBM exhausted";
@@ -1273,31 +1502,59 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       unsigned long long W_chunk = (unsigned long long)hrb->lastpos + hrb->lastwin;
       for (int sg = 0; sg < 8; sg++) ncand += hrb->segc[16 * sg];
       gen_lvl += ncand;
-      {
-        // the next-level buffer grows in place to exactly what this chunk needs
-        bool cur_is_a = cur == fa.as<uint32_t>();
-        GrowBuf& nb = cur_is_a ? fb : fa;
-        const size_t need = (size_t)(next_n + W_chunk) * W * 4;
-        if (nb.bytes < need) {
-          auto tg0 = now();
-          HIPCHK(hipStreamSynchronize(stream));
-          nb.ensure(need);
-          cur = (cur_is_a ? fa : fb).as<uint32_t>();
-          nxt = nb.as<uint32_t>();
-          a.frontier = cur + c0 * W;
-          grow_s += secs(tg0, now());
+      for (int attempt = 0;; attempt++) {
+        try {
+          if (!hf && hf_opt == 0 && hf_force_grow && level == hf_force_level && c0 > 0 && !attempt)
+            throw OutOfDeviceMemory("test: RMC_HOST_FRONTIER_AT");
+          if (!hf) {
+            // the next-level buffer grows in place to exactly what this chunk needs
+            bool cur_is_a = cur == fa.as<uint32_t>();
+            GrowBuf& nb = cur_is_a ? fb : fa;
+            const size_t need = (size_t)(next_n + W_chunk) * W * 4;
+            if (nb.bytes < need) {
+              auto tg0 = now();
+              HIPCHK(hipStreamSynchronize(stream));
+              nb.ensure(need);
+              cur = (cur_is_a ? fa : fb).as<uint32_t>();
+              nxt = nb.as<uint32_t>();
+              a.frontier = cur + c0 * W;
+              grow_s += secs(tg0, now());
+            }
+            fcap = std::max(fcap, next_n + W_chunk);
+          }
+          if (distinct + next_n + W_chunk > trcap) {
+            auto tg0 = now();
+            HIPCHK(hipStreamSynchronize(stream));
+            trcap = (distinct + next_n + W_chunk) + (distinct + next_n + W_chunk) / 4;
+            trp.ensure(trcap * 8);
+            trb.ensure(trcap * 2);
+            grow_s += secs(tg0, now());
+          }
+          break;
+        } catch (OutOfDeviceMemory&) {
+          if (hf || hf_opt != 0 || attempt) throw;
+          // HBM is full: the frontiers move to host memory; this chunk's
+          // parents (k_materialize re-reads them) go to its input window
+          lvl_next_n = next_n;
+          enter_hf();
+          hcur.h2d(c0, n, A.hwin_in[hs_k].p, hs.cs);
+          HIPCHK(hipStreamSynchronize(hs.cs));
+          hwin_c0[hs_k] = c0;
+          a.frontier = A.hwin_in[hs_k].as<uint32_t>();
         }
-        fcap = std::max(fcap, next_n + W_chunk);
       }
-      if (distinct + next_n + W_chunk > trcap) {
-        auto tg0 = now();
-        HIPCHK(hipStreamSynchronize(stream));
-        trcap = (distinct + next_n + W_chunk) + (distinct + next_n + W_chunk) / 4;
-        trp.ensure(trcap * 8);
-        trb.ensure(trcap * 2);
-        grow_s += secs(tg0, now());
+      if (hf) {
+        // output window hs_k: free once chunk ck-2's rows have left it
+        const size_t need = (size_t)W_chunk * W * 4;
+        if (A.hwin_out[hs_k].bytes < need) {
+          HIPCHK(hipEventSynchronize(hs.out[hs_k]));
+          A.hwin_out[hs_k].ensure(need + need / 4);
+        }
+        HIPCHK(hipStreamWaitEvent(stream, hs.out[hs_k], 0));
+        a.out = A.hwin_out[hs_k].as<uint32_t>();
+      } else {
+        a.out = nxt + next_n * W;
       }
-      a.out = nxt + next_n * W;
       a.out_base_global = distinct + next_n;
       a.tr_parent = trp.as<unsigned long long>();
       a.tr_bind = trb.as<uint16_t>();
@@ -1307,9 +1564,21 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(tz.b, stream));
       HIPCHK(hipMemcpyAsync(&hrb->mat, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
+      if (hf) {  // the new rows go to host pages (copy stream), after this k_materialize
+        HIPCHK(hipEventRecord(hs.mat[hs_k], stream));
+        hnxt.reserve(W_chunk, pool);
+        HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k], 0));
+        hnxt.d2h_append(A.hwin_out[hs_k].p, W_chunk, hs.cs);
+        HIPCHK(hipEventRecord(hs.out[hs_k], hs.cs));
+        // rows below the previous chunk are consumed (the last two chunks stay
+        // for the recount at a violation)
+        hcur.recycle_below(prev_c0, pool);
+      }
       mat_pending = true;
       next_n += W_chunk;
+      prev_c0 = c0;
       c0 += n;
+      ck++;
       if (hst.err_key != ~0ULL) {  // this chunk's expand hit an evaluation error: the search stops here
         HIPCHK(hipStreamSynchronize(stream));
         finish_mat();
@@ -1320,6 +1589,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       HIPCHK(hipStreamSynchronize(stream));
       finish_mat();
     }
+    if (hf) HIPCHK(hipStreamSynchronize(hs.cs));  // every new row is in its host page
     const unsigned long long gen_before = generated, dist_before = distinct;
     generated += gen_lvl;
     distinct += next_n;
@@ -1342,27 +1612,34 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       stop_level = level;
       stop_level_base = cur_base;
       stop_level_n = cur_n;
-      stop_front = cur;
+      stop_front = hf ? nullptr : cur;
+      stop_hf = hf;
       stop_gen_before = gen_before;
       stop_dist_before = dist_before;
       cur_base += cur_n;
       cur_n = next_n;
       std::swap(cur, nxt);
+      std::swap(hcur, hnxt);  // host frontier: hnxt keeps the stopped level for the recount
       break;
     }
     rate = (double)next_n / (double)cur_n;
     cur_base += cur_n;
     cur_n = next_n;
     std::swap(cur, nxt);
+    if (hf) {
+      hcur.clear(pool);
+      std::swap(hcur, hnxt);
+    }
     if (opt->verbose) {
       size_t fr = 0, tot = 0;
       (void)hipMemGetInfo(&fr, &tot);
       fprintf(stderr,
               "[rmc] depth %u: %llu new, %llu distinct, %llu generated, t=%.3fs (rehash %.3fs, grow %.3fs) "
-              "HBM GiB: fp-set %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f\n",
+              "HBM GiB: fp-set %.1f+%.1f frontiers %.1f+%.1f trace %.1f+%.1f free %.1f%s\n",
               depth, next_n, distinct, generated, secs(t0, now()), rehash_s, grow_s, table.bytes / 1073741824.0,
               A.table2.bytes / 1073741824.0, fa.bytes / 1073741824.0, fb.bytes / 1073741824.0, trp.bytes / 1073741824.0, trb.bytes / 1073741824.0,
-              fr / 1073741824.0);
+              fr / 1073741824.0,
+              hf ? (" | host frontier: " + std::to_string(pool.allocated >> 20) + " MiB pinned").c_str() : "");
     }
     // ---- snapshot at this level boundary (TLC -checkpoint)
     if (opt->checkpoint_dir && *opt->checkpoint_dir && cur_n > 0 &&
@@ -1371,12 +1648,36 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       HIPCHK(hipStreamSynchronize(stream));
       const std::string dir = opt->checkpoint_dir;
       if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) throw std::runtime_error("checkpoint: cannot create " + dir);
-      (void)remove((dir + "/checkpoint.meta").c_str());  // the old snapshot is void from here on
-      ckpt_write(dir + "/fpset.bin", table.p, slots * ew * 8, stage(), ck_stage_bytes);
-      ckpt_write(dir + "/frontier.bin", cur, cur_n * W * 4, stage(), ck_stage_bytes);
-      ckpt_write(dir + "/trace_parent.bin", trp.p, distinct * 8, stage(), ck_stage_bytes);
-      ckpt_write(dir + "/trace_bind.bin", trb.p, distinct * 2, stage(), ck_stage_bytes);
+      // the snapshot the directory holds now (if any) stays valid until the new one is durable
+      unsigned long long prev_seq = 0;
+      bool have_prev = false;
+      try {
+        prev_seq = ckpt_read_meta(dir, m).seq;
+        have_prev = true;
+      } catch (std::exception&) {
+      }
       Ckpt c;
+      c.seq = have_prev ? prev_seq + 1 : 0;
+      const std::string sub = dir + "/" + ckpt_subdir(c.seq);
+      remove_tree(sub);  // debris of an interrupted snapshot with this number
+      if (mkdir(sub.c_str(), 0755) != 0) throw std::runtime_error("checkpoint: cannot create " + sub);
+      ckpt_write(sub + "/fpset.bin", table.p, slots * ew * 8, stage(), ck_stage_bytes);
+      if (hf) {
+        const std::string fp = sub + "/frontier.bin", tmp = fp + ".tmp";
+        FILE* f = fopen(tmp.c_str(), "wb");
+        if (!f) throw std::runtime_error("checkpoint: cannot write " + tmp);
+        for (unsigned long long r = 0; r < cur_n; r += page_rows) {
+          const size_t k = (size_t)std::min<unsigned long long>(page_rows, cur_n - r);
+          if (fwrite(hcur.row(r), row_bytes, k, f) != k) { fclose(f); throw std::runtime_error("checkpoint: short write"); }
+        }
+        if (fflush(f) != 0 || fsync(fileno(f)) != 0 || fclose(f) != 0 || rename(tmp.c_str(), fp.c_str()) != 0)
+          throw std::runtime_error("checkpoint: cannot finish " + fp);
+      } else {
+        ckpt_write(sub + "/frontier.bin", cur, cur_n * W * 4, stage(), ck_stage_bytes);
+      }
+      ckpt_write(sub + "/trace_parent.bin", trp.p, distinct * 8, stage(), ck_stage_bytes);
+      ckpt_write(sub + "/trace_bind.bin", trb.p, distinct * 2, stage(), ck_stage_bytes);
+      fsync_dir(sub);
       c.sig = model_signature(m);
       c.slots = slots;
       c.generated = generated;
@@ -1390,11 +1691,16 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       c.rate = rate;
       c.levels = m->levels;
       ckpt_write_meta(dir, m, c);
+      if (have_prev) remove_tree(dir + "/" + ckpt_subdir(prev_seq));
       last_ckpt = now();
       if (opt->verbose)
         fprintf(stderr, "[rmc] checkpoint at depth %u in %s (%.3fs)\n", depth, dir.c_str(), secs(tc0, now()));
     }
   }
+  } catch (OutOfHostMemory& oom) {
+    status = 3;
+    message = std::string("capacity overflow: ") + oom.what();
+    HIPCHK(hipDeviceSynchronize());
   } catch (OutOfDeviceMemory& oom) {
     // the level in progress is abandoned; counts are those of the completed levels
     status = 3;
@@ -1416,7 +1722,7 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
   // parent's successors (as the oracle's convention does).
   DevStatus fin;  // before the recount below (which marks the failing chunk a second time)
   HIPCHK(hipMemcpy(&fin, stbuf.p, sizeof fin, hipMemcpyDeviceToHost));
-  if ((status == 1 || status == 2) && bad_key != ~0ULL && stop_front) {
+  if ((status == 1 || status == 2) && bad_key != ~0ULL && (stop_front || stop_hf)) {
     const unsigned long long pg = bad_key >> 20, li = pg - stop_level_base;
     const int ordv = (int)((bad_key >> 10) & 0x3FF);
     const ChunkLog* cl = nullptr;
@@ -1428,8 +1734,12 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       unsigned long long save_base = cur_base;
       cur = const_cast<uint32_t*>(stop_front);
       cur_base = stop_level_base;
+      if (stop_hf) {  // the stopped level's pages (hnxt after the swap)
+        hnxt.h2d(c0, n, A.hwin_in[0].p, stream);
+        HIPCHK(hipStreamSynchronize(stream));
+      }
       LevelArgs a;
-      fill_args(a, c0, n, stop_level);
+      fill_args(a, c0, n, stop_level, stop_hf ? A.hwin_in[0].as<uint32_t>() : nullptr);
       cur = save_cur;
       cur_base = save_base;
       HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
@@ -1518,9 +1828,17 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     fprintf(stderr, "[rmc] fingerprint set: 2^%d slots, load %.3f, %llu growths, %llu chunk redos\n",
             __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);
   }
+  if (hf) {
+    HIPCHK(hipStreamSynchronize(hs.cs));
+    hcur.clear(pool);
+    hnxt.clear(pool);
+    pool.release();
+    for (DevBuf* b : {&A.hwin_in[0], &A.hwin_in[1], &A.hwin_out[0], &A.hwin_out[1]}) b->release();
+    if (opt->verbose) fprintf(stderr, "[rmc] host frontier: %.3fs moving levels to host memory\n", hf_copy_s);
+  }
   HIPCHK(hipStreamDestroy(stream));
   if (!opt->hash_slots) m->hint_slots = slots;
-  if (!opt->frontier_cap) m->hint_fcap = fcap;
+  if (!opt->frontier_cap && !hf) m->hint_fcap = fcap;
   m->hint_trcap = trcap;
   res->generated = generated;
   res->distinct = distinct;
@@ -1642,6 +1960,7 @@ int rmc_check(rmc_model* m, const rmc_options* o, rmc_result* out) {
       g_last_error = "no HIP device available: the raftmc GPU path requires an MI355X (gfx950)";
       return -4;
     }
+    release_shard_buffers();
     m->kmax_user = 0;
     int rc;
     while ((rc = check_impl(m, o, out)) == 1) memset(out, 0, sizeof *out);

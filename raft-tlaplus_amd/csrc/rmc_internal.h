@@ -194,6 +194,98 @@ struct GrowBuf {
   T* as() const { return (T*)p; }
 };
 
+// Host memory ran out (the host-frontier page pool hit its limit).
+struct OutOfHostMemory : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// BFS levels in pinned host memory (SURVEY.md §7 hard part 5: "page the
+// frontier to pinned host memory when a level exceeds its budget").  A level
+// is a sequence of fixed-size pinned pages, each holding `page_rows` packed
+// rows; rows stream through HBM in chunk-sized windows (H2D before expansion,
+// D2H after materialization) with async copies on a copy stream.  Pages of
+// rows already consumed go back to the pool while the level is still being
+// read, so the host peak is about one level plus the growth of the next.
+struct HostPagePool {
+  size_t page_bytes = 0;
+  size_t allocated = 0, limit = 0;  // bytes of pinned pages held / allowed
+  std::vector<void*> free_pages;
+  void* get() {
+    if (!free_pages.empty()) {
+      void* p = free_pages.back();
+      free_pages.pop_back();
+      return p;
+    }
+    if (allocated + page_bytes > limit)
+      throw OutOfHostMemory("host frontier pages exhausted (" + std::to_string(limit >> 30) + " GiB limit)");
+    void* p = nullptr;
+    if (hipHostMalloc(&p, page_bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      throw OutOfHostMemory("pinned host memory exhausted (" + std::to_string(allocated >> 30) + " GiB held)");
+    }
+    allocated += page_bytes;
+    return p;
+  }
+  void put(void* p) { if (p) free_pages.push_back(p); }
+  void release() {
+    for (void* p : free_pages) (void)hipHostFree(p);
+    allocated -= free_pages.size() * page_bytes;
+    free_pages.clear();
+  }
+  ~HostPagePool() { release(); }
+};
+struct HostLevel {
+  std::vector<void*> pages;  // nullptr: recycled (its rows were consumed)
+  unsigned long long rows = 0;
+  size_t page_rows = 1, row_bytes = 4;
+  void init(size_t prow, size_t rb) { pages.clear(); rows = 0; page_rows = prow; row_bytes = rb; }
+  // copy rows [r0, r0 + n) to dev (async on stream)
+  void h2d(unsigned long long r0, unsigned long long n, void* dev, hipStream_t stream) const {
+    char* d = (char*)dev;
+    while (n) {
+      const size_t pg = r0 / page_rows, off = r0 % page_rows, k = std::min<unsigned long long>(n, page_rows - off);
+      if (pg >= pages.size() || !pages[pg]) throw std::runtime_error("host frontier: rows already recycled");
+      HIPCHK(hipMemcpyAsync(d, (char*)pages[pg] + off * row_bytes, k * row_bytes, hipMemcpyHostToDevice, stream));
+      d += k * row_bytes;
+      r0 += k;
+      n -= k;
+    }
+  }
+  // reserve pages for n more rows (may allocate: call before enqueuing the copy)
+  void reserve(unsigned long long n, HostPagePool& pool) {
+    while ((rows + n + page_rows - 1) / page_rows > pages.size()) pages.push_back(pool.get());
+  }
+  // append n rows from dev (async on stream; pages reserved beforehand)
+  void d2h_append(const void* dev, unsigned long long n, hipStream_t stream) {
+    const char* s = (const char*)dev;
+    while (n) {
+      const size_t pg = rows / page_rows, off = rows % page_rows, k = std::min<unsigned long long>(n, page_rows - off);
+      HIPCHK(hipMemcpyAsync((char*)pages[pg] + off * row_bytes, s, k * row_bytes, hipMemcpyDeviceToHost, stream));
+      s += k * row_bytes;
+      rows += k;
+      n -= k;
+    }
+  }
+  // give back the pages whose rows all lie below row r
+  void recycle_below(unsigned long long r, HostPagePool& pool) {
+    for (size_t pg = 0; pg < pages.size() && (pg + 1) * page_rows <= r; pg++) {
+      pool.put(pages[pg]);
+      pages[pg] = nullptr;
+    }
+  }
+  void clear(HostPagePool& pool) {
+    for (void* p : pages) pool.put(p);
+    pages.clear();
+    rows = 0;
+  }
+  const uint32_t* row(unsigned long long r) const {
+    return (const uint32_t*)((const char*)pages[r / page_rows] + (r % page_rows) * row_bytes);
+  }
+};
+// Host memory the host frontier may pin: RMC_HOST_FRONTIER_GIB, or 80% of
+// MemAvailable capped at 200 GiB (a shared host must keep room for others).
+size_t host_frontier_limit();
+
 struct EventTimer {
   hipEvent_t a, b;
   EventTimer() { HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b)); }
@@ -208,6 +300,7 @@ std::vector<uint32_t> init_state(const rmc::Model& M);
 std::string binding_label(const rmc_model* m, int b, int act);
 void set_last_error(const std::string& s);
 void release_shard_buffers();
+void release_single_buffers();
 // Rebuild the behaviour Init -> ... from the binding chain (root first), plus
 // the failing binding (last_b >= 0) whose successor violated or erred.
 void replay_trace(rmc_model* m, const std::vector<int>& binds, int last_b, int status, std::string& message,

@@ -330,6 +330,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("fp_bits 128 is offered by the single-GPU search (rmc_check) only");
   if ((opt->checkpoint_dir && *opt->checkpoint_dir) || (opt->recover_dir && *opt->recover_dir))
     throw std::runtime_error("checkpoint / recover are offered by the single-GPU search (rmc_check) only");
+  if (opt->host_frontier == 1) throw std::runtime_error("host_frontier = 1 is offered by the single-GPU search (rmc_check) only");
   uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);
@@ -345,16 +346,21 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   if (W > 64) throw std::runtime_error("at most 64 shards");
 
   std::vector<Shard> sh(NL);
+  // the model's size hints are whole-search totals (the single-GPU search
+  // keeps them so too): a shard starts at its 1/W share
+  auto share = [&](unsigned long long total) { return total / (unsigned long long)W; };
+  unsigned long long hint_slots_1 = 1;
+  while (hint_slots_1 < share(m->hint_slots)) hint_slots_1 <<= 1;
   for (int i = 0; i < NL; i++) {
     Shard& s = sh[i];
     s.id = comm.local[i];
     s.B = &shard_bufs(i);
     ShardBufs& B = *s.B;
-    s.slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 22, m->hint_slots);
+    s.slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 22, hint_slots_1);
     if (s.slots & (s.slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
     B.table.ensure(s.slots * 16);
     HIPCHK(hipMemsetAsync(B.table.p, 0xFF, s.slots * 16, stream));
-    s.fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 20, m->hint_fcap);
+    s.fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 20, share(m->hint_fcap));
     B.fa.ensure(s.fcap * WD * 4);
     B.fb.ensure(s.fcap * WD * 4);
     s.cur = B.fa.as<uint32_t>();
@@ -373,7 +379,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     size_t stb = scan_temp_bytes(CH);
     B.scantmp.ensure(stb ? stb : 16);
     B.small.ensure(4096);
-    s.trcap = std::max(s.fcap * 4, m->hint_trcap);
+    s.trcap = std::max(s.fcap * 4, share(m->hint_trcap));
     B.trp.ensure(s.trcap * 8);
     B.trb.ensure(s.trcap * 2);
     s.hst.err_key = s.hst.inv_err_key = s.hst.viol_key = ~0ULL;
@@ -876,9 +882,9 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   }
   if (status == 0 && !opt->max_depth && !opt->msg_cap_K) m->hint_kmax = std::max(1u, gmax_msgs);
   res->max_msgs = gmax_msgs;
-  if (!opt->hash_slots) m->hint_slots = sh[0].slots;
-  if (!opt->frontier_cap) m->hint_fcap = sh[0].fcap;
-  m->hint_trcap = sh[0].trcap;
+  if (!opt->hash_slots) m->hint_slots = sh[0].slots * (unsigned long long)W;
+  if (!opt->frontier_cap) m->hint_fcap = sh[0].fcap * (unsigned long long)W;
+  m->hint_trcap = sh[0].trcap * (unsigned long long)W;
   res->generated = generated;
   res->distinct = distinct;
   res->left_on_queue = status == 0 ? 0 : P;
@@ -942,6 +948,7 @@ int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, i
       return -4;
     }
     HIPCHK(hipSetDevice(device));
+    release_single_buffers();
     // The communicator (and its stream) is kept for later checks with the same
     // id, rank and world: repeated checks do not pay ncclCommInitRank again.
     static std::mutex mu;
@@ -985,6 +992,7 @@ int rmc_check_sharded_shm(rmc_model* m, const rmc_options* o, int rank, int worl
       return -4;
     }
     HIPCHK(hipSetDevice(device));
+    release_single_buffers();
     hipStream_t s;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     int rc;
@@ -1012,6 +1020,7 @@ int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result
       set_last_error("no HIP device available: the raftmc GPU path requires an MI355X (gfx950)");
       return -4;
     }
+    release_single_buffers();
     hipStream_t s;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     int rc;

@@ -81,7 +81,10 @@ struct Model {
   int kmax, words;  // words = 1 + 4N + kmax
   int nperm;
   uint32_t perm[MAXPERM];  // permutation p maps server j -> (perm[p] >> 3j) & 7
-  int ninv, inv[5];        // invariant ids in cfg order: 0 LHAAV, 1 NLD, 2 CERM, 3 NTLISE, 4 NIS (KRaft)
+  // invariant ids in cfg order: 0 LHAAV, 1 NLD, 2 CERM, 3 NTLISE, 4 NIS (KRaft); the classic Raft
+  // properties, opt-in (not defined by the reference specs): 5 ElectionSafety, 6 LogMatching,
+  // 7 LeaderCompleteness, 8 StateMachineSafety
+  int ninv, inv[9];
   int nact, act_id[MAXACT], act_kind[MAXACT], act_off[MAXACT];
   int nfixed;
   uint8_t fb_act[MAXFIXED], fb_x[MAXFIXED];  // fixed binding -> (action slot, binding index)
@@ -1595,6 +1598,77 @@ RMC_HD bool inv_no_illegal_state(const PState<SPEC, N>& s) {  // KRaft.tla:887-8
     if (kr_st(s.A(i)) == KS_ILLEGAL) return false;
   return true;
 }
+// The classic Raft safety properties (Ongaro's dissertation, Fig. 3.2), offered
+// as opt-in invariants for the Raft-family modules (the reference's cfgs check
+// only LeaderHasAllAckedValues and NoLogDivergence).  Their
+// TLA+ text, which a user adds to a spec to have TLC check the same thing, is
+// in INTEGRATION.md; sequence indices are bounded by Len, so none can raise an
+// evaluation error.
+//   ElectionSafety == \A s1, s2 \in Server : (s1 # s2 /\ state[s1] = Leader /\ state[s2] = Leader)
+//                       => currentTerm[s1] # currentTerm[s2]
+template <int SPEC, int N>
+RMC_HD bool inv_election_safety(const PState<SPEC, N>& s) {
+  for (int i = 0; i < N; i++)
+    for (int j = i + 1; j < N; j++)
+      if (a_st(s.A(i)) == LEADER && a_st(s.A(j)) == LEADER && a_term(s.A(i)) == a_term(s.A(j))) return false;
+  return true;
+}
+//   LogMatching == \A s1, s2 \in Server : \A i \in 1..Min({Len(log[s1]), Len(log[s2])}) :
+//                    log[s1][i].term = log[s2][i].term => SubSeq(log[s1], 1, i) = SubSeq(log[s2], 1, i)
+template <int SPEC, int N>
+RMC_HD bool inv_log_matching(const PState<SPEC, N>& s) {
+  for (int i = 0; i < N; i++)
+    for (int j = i + 1; j < N; j++) {
+      const int L = a_len(s.A(i)) < a_len(s.A(j)) ? a_len(s.A(i)) : a_len(s.A(j));
+      const uint32_t bi = s.B(i), bj = s.B(j);
+      for (int x = L - 1; x >= 0; x--)  // the longest prefix whose last terms agree
+        if (e_term(bi, x) == e_term(bj, x)) {
+          const uint32_t m = x >= 4 ? 0x3FFFFFFFu : ((1u << (6 * (x + 1))) - 1u);
+          if ((bi & m) != (bj & m)) return false;
+          break;
+        }
+    }
+  return true;
+}
+//   LeaderCompleteness == \A l \in Server :
+//       (state[l] = Leader /\ \A s \in Server : currentTerm[s] <= currentTerm[l]) =>
+//         \A s \in Server : \A i \in 1..Min({commitIndex[s], Len(log[s])}) :
+//           i <= Len(log[l]) /\ log[l][i] = log[s][i]
+// (a leader of the newest term holds every entry any server has committed)
+template <int SPEC, int N>
+RMC_HD bool inv_leader_completeness(const PState<SPEC, N>& s) {
+  for (int l = 0; l < N; l++) {
+    const uint32_t al = s.A(l);
+    if (a_st(al) != LEADER) continue;
+    bool newest = true;
+    for (int k = 0; k < N; k++)
+      if (a_term(s.A(k)) > a_term(al)) newest = false;
+    if (!newest) continue;
+    for (int k = 0; k < N; k++) {
+      const uint32_t ak = s.A(k);
+      const int c = a_commit(ak) < a_len(ak) ? a_commit(ak) : a_len(ak);
+      if (c > a_len(al)) return false;
+      for (int x = 0; x < c; x++)
+        if (((s.B(l) >> (6 * x)) & 63u) != ((s.B(k) >> (6 * x)) & 63u)) return false;
+    }
+  }
+  return true;
+}
+//   StateMachineSafety == \A s1, s2 \in Server :
+//       \A i \in 1..Min({commitIndex[s1], commitIndex[s2], Len(log[s1]), Len(log[s2])}) : log[s1][i] = log[s2][i]
+template <int SPEC, int N>
+RMC_HD bool inv_state_machine_safety(const PState<SPEC, N>& s) {
+  for (int i = 0; i < N; i++)
+    for (int j = i + 1; j < N; j++) {
+      const uint32_t ai = s.A(i), aj = s.A(j);
+      int c = a_commit(ai) < a_commit(aj) ? a_commit(ai) : a_commit(aj);
+      c = c < a_len(ai) ? c : a_len(ai);
+      c = c < a_len(aj) ? c : a_len(aj);
+      for (int x = 0; x < c; x++)
+        if (((s.B(i) >> (6 * x)) & 63u) != ((s.B(j) >> (6 * x)) & 63u)) return false;
+    }
+  return true;
+}
 // returns -1 if all hold, else the position (in cfg order) of the violated one
 template <int SPEC, int N>
 RMC_HD int check_invariants(const PState<SPEC, N>& s, const Model& M, int& err) {
@@ -1606,6 +1680,10 @@ RMC_HD int check_invariants(const PState<SPEC, N>& s, const Model& M, int& err) 
       case 2: ok = inv_committed_majority(s, err); break;
       case 3: ok = inv_never_two_leaders(s); break;
       case 4: ok = inv_no_illegal_state(s); break;
+      case 5: ok = inv_election_safety(s); break;
+      case 6: ok = inv_log_matching(s); break;
+      case 7: ok = inv_leader_completeness(s); break;
+      case 8: ok = inv_state_machine_safety(s); break;
     }
     if (err) return -2;
     if (!ok) return q;

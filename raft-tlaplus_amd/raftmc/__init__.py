@@ -294,6 +294,11 @@ class Model:
         return res
 
 
+def release_device_memory():
+    """Free the device buffers librmc caches per GPU between checks."""
+    lib().rmc_release_device_memory()
+
+
 def check(tla_path, cfg_path=None, **kw):
     """TLC-equivalent run: check(M.tla, M.cfg) -> dict (generated, distinct, depth, ...)."""
     return Model(tla_path, cfg_path).check(**kw)

@@ -149,3 +149,55 @@ KRAFT = [
     ("kraft_n2v2e1r1", dict(n=2, v=2, E=1, R=1)),
     ("kraft_n3v2e1", dict(n=3, v=2, E=1)),
 ]
+
+
+# BASELINE configs 2 and 5 at their scaled bounds (configs/Raft_n3v2e3.cfg,
+# configs/RaftFsync_n3v2e3r1.cfg): exhausting them is beyond one GPU, so they
+# are pinned level by level up to the first level boundary at which the C
+# oracle has found >= max_distinct states; the Python oracle reproduces a
+# shorter prefix.  (name, module, cfg path, C max_distinct, Python max_states)
+LADDERS = [
+    ("raft_n3v2e3_cfg2", "Raft", "configs/Raft_n3v2e3.cfg", 20000000, 20000),
+    ("fsync_n3v2e3r1_cfg5", "RaftFsync", "configs/RaftFsync_n3v2e3r1.cfg", 20000000, 20000),
+    # the exhaustible rungs below them (the bench workload and config 5's
+    # largest exhausted rung), pinned by the oracles on their first levels
+    ("raft_n3v2e2_bench", "Raft", "configs/Raft_n3v2e2.cfg", 20000000, 20000),
+    ("fsync_n3v1e2r1_rung", "RaftFsync", "configs/RaftFsync_n3v1e2r1.cfg", 20000000, 20000),
+]
+
+# FlexibleRaft's Restart (FlexibleRaft.tla:200-208) with MaxRestarts >= 1:
+# (name, kwargs, C max_distinct or 0 = exhaustive, Python max_states or 0 = exhaustive)
+FLEX_RESTART = [
+    ("flex_n3v1e1r1", dict(n=3, v=1, E=1, R=1, ElectionQuorumSize=2, ReplicationQuorumSize=2), 0, 0),
+    ("flex_n2v1e2r1", dict(n=2, v=1, E=2, R=1, ElectionQuorumSize=2, ReplicationQuorumSize=1), 0, 0),
+    ("flex_n3v1e2r1", dict(n=3, v=1, E=2, R=1, ElectionQuorumSize=2, ReplicationQuorumSize=2), 5000000, 30000),
+    ("flex_n3v2e2r1_eq1", dict(n=3, v=2, E=2, R=1, ElectionQuorumSize=1, ReplicationQuorumSize=2), 0, 0),
+    ("flex_n5v1e1r1_eq3rq4", dict(n=5, v=1, E=1, R=1, ElectionQuorumSize=3, ReplicationQuorumSize=4), 400000, 3000),
+]
+
+# The classic Raft safety properties as opt-in invariants (ElectionSafety,
+# LogMatching, LeaderCompleteness, StateMachineSafety; INTEGRATION.md gives
+# their TLA+): (name, module, kwargs, invariants in cfg order).  Safe configs
+# must satisfy them (same counts as with the shipped invariants); the
+# non-intersecting Flexible quorums break ElectionSafety.
+CLASSIC = ("ElectionSafety", "LogMatching", "LeaderCompleteness", "StateMachineSafety")
+SHIPPED_INV = ("LeaderHasAllAckedValues", "NoLogDivergence")
+EXTRAS = [
+    ("raft_n3v1e1_classic", "Raft", dict(n=3, v=1, E=1), SHIPPED_INV + CLASSIC),
+    ("raft_n2v2e2_classic", "Raft", dict(n=2, v=2, E=2), SHIPPED_INV + CLASSIC),
+    ("raft_n3v1e1r1_classic", "Raft", dict(n=3, v=1, E=1, R=1), CLASSIC),
+    ("pull_n3v2e1_classic", "PullRaft", dict(n=3, v=2, E=1), SHIPPED_INV + CLASSIC),
+    ("pull_n2v1e2r1_classic", "PullRaft", dict(n=2, v=1, E=2, R=1), CLASSIC),
+    ("fsync_n3v1e1_classic", "RaftFsync", dict(n=3, v=1, E=1), SHIPPED_INV + CLASSIC),
+    ("fsync_n2v1e2r1_classic", "RaftFsync", dict(n=2, v=1, E=2, R=1), CLASSIC),
+    ("flex_n3v1e1_classic", "FlexibleRaft", dict(n=3, v=1, E=1, ElectionQuorumSize=2, ReplicationQuorumSize=2),
+     SHIPPED_INV + CLASSIC),
+    ("pull2_n3v1e1_classic", "PullRaftVariant2", dict(n=3, v=1, E=1), CLASSIC),
+    # FollowerFsyncBeforeReply = FALSE with a restart: acknowledged entries can be lost
+    ("fsync_n2v1e2r1_nofsync_classic", "RaftFsync", dict(n=2, v=1, E=2, R=1, FollowerFsyncBeforeReply=False), CLASSIC),
+    # quorums of 1 (FlexibleRaft.tla:16-24 lists the valid pairs): two leaders of one term
+    ("flex_n3v1e2_q1_classic", "FlexibleRaft", dict(n=3, v=1, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=1),
+     CLASSIC),
+    ("flex_n3v1e2_q1_lm", "FlexibleRaft", dict(n=3, v=1, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=1),
+     ("LogMatching", "LeaderCompleteness", "StateMachineSafety")),
+]

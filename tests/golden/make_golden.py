@@ -23,8 +23,8 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import (MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM, VARIANT2_N5,  # noqa: E402
-                  VARIANT2_SMALL, cfg_text)
+from cfgs import (EXTRAS, FLEX_RESTART, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
+                  VARIANT2_N5, VARIANT2_SMALL, cfg_text)
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
     ("Raft_cfg", "Raft", "configs/Raft.cfg"),
@@ -161,7 +161,96 @@ def variant2():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def ladders():
+    """--ladders: BASELINE configs 2 and 5 at their scaled bounds (cfgs.LADDERS),
+    level-truncated: the C oracle to the first level boundary past max_distinct,
+    the Python oracle on a shorter prefix that must agree level by level."""
+    out = {}
+    for name, module, path, c_max, py_max in LADDERS:
+        with open(os.path.join(ROOT, path)) as fh:
+            txt = fh.read()
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=8, extra=["--max-distinct", str(c_max)])
+        p = bfs(make_spec(module, cfg), max_states=py_max)
+        pl = [list(x) for x in p.levels]
+        if pl != c["levels"][:len(pl)]:
+            raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pl, c["levels"][:len(pl)]))
+        out[name] = dict(module=module, cfg_path=path, generated=c["generated"], distinct=c["distinct"],
+                         depth=c["depth"], status=c["status"], levels=c["levels"], max_distinct=c_max,
+                         max_msgs=c["max_msgs"], hidden_same_level=c["hidden_same_level"], pyoracle_levels=len(pl),
+                         pinned_by="coracle; first %d levels pyoracle==coracle" % len(pl),
+                         oracle_seconds=c["seconds"])
+        print(name, c["generated"], c["distinct"], c["depth"], "py levels", len(pl), flush=True)
+    with open(os.path.join(HERE, "ladders.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+def flex_restart():
+    """--flex-restart: FlexibleRaft with MaxRestarts >= 1 (cfgs.FLEX_RESTART;
+    FlexibleRaft.tla:200-208).  Exhaustive cases: both oracles on every level
+    (the Python one on a prefix where it would take too long); the 5-server
+    case level-truncated like --n5."""
+    M = "FlexibleRaft"
+    out = {}
+    for name, kw, c_max, py_max in FLEX_RESTART:
+        txt = cfg_text(M, **kw)
+        cfg = parse_cfg(txt)
+        extra = ["--max-distinct", str(c_max)] if c_max else []
+        c = run_c.run(M, cfg["constants"], cfg["invariants"], threads=8, extra=extra + ["--trace"])
+        p = bfs(make_spec(M, cfg), max_states=py_max) if py_max else bfs(make_spec(M, cfg))
+        pl = [list(x) for x in p.levels]
+        if py_max:
+            if pl != c["levels"][:len(pl)]:
+                raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pl, c["levels"][:len(pl)]))
+            pinned = "coracle; first %d levels pyoracle==coracle" % len(pl)
+        else:
+            pr = (p.generated, p.distinct, p.depth, p.status, pl, p.hidden_same_level)
+            cr = (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"], c["hidden_same_level"])
+            if pr != cr:
+                raise SystemExit("oracles disagree on %s: py=%s c=%s" % (name, pr[:4], cr[:4]))
+            pinned = "pyoracle==coracle"
+        out[name] = dict(module=M, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], violated=c["violated"], levels=c["levels"],
+                         action_counts=c["action_counts"], max_msgs=c["max_msgs"],
+                         hidden_same_level=c["hidden_same_level"], trace_len=len(c.get("trace", [])),
+                         pyoracle_levels=len(pl), pinned_by=pinned)
+        if c_max:
+            out[name]["max_distinct"] = c_max
+        print(name, c["generated"], c["distinct"], c["depth"], c["status"], c["violated"], pinned, flush=True)
+    with open(os.path.join(HERE, "flex_restart.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+def extras():
+    """--extras: the opt-in classic invariants (cfgs.EXTRAS) -- both oracles must
+    agree on the counts and on which invariant fails (and the trace length)."""
+    out = {}
+    for name, module, kw, inv in EXTRAS:
+        txt = cfg_text(module, inv=inv, **kw)
+        cfg = parse_cfg(txt)
+        c = run_c.run(module, cfg["constants"], cfg["invariants"], threads=4, extra=["--trace"])
+        p = bfs(make_spec(module, cfg))
+        pr = (p.generated, p.distinct, p.depth, p.status, [list(x) for x in p.levels])
+        cr = (c["generated"], c["distinct"], c["depth"], c["status"], c["levels"])
+        if pr != cr or (c["status"] == "violation" and p.violated != c["violated"]):
+            raise SystemExit("oracles disagree on %s: py=%s %s c=%s %s" % (name, pr[:4], getattr(p, "violated", ""),
+                                                                          cr[:4], c["violated"]))
+        out[name] = dict(module=module, cfg=txt, generated=c["generated"], distinct=c["distinct"], depth=c["depth"],
+                         status=c["status"], violated=c["violated"], levels=c["levels"],
+                         hidden_same_level=c["hidden_same_level"], trace_len=len(c.get("trace", [])),
+                         pinned_by="pyoracle==coracle")
+        print(name, c["generated"], c["distinct"], c["depth"], c["status"], c["violated"], flush=True)
+    with open(os.path.join(HERE, "extras.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--extras" in sys.argv:
+        return extras()
+    if "--ladders" in sys.argv:
+        return ladders()
+    if "--flex-restart" in sys.argv:
+        return flex_restart()
     if "--variant2" in sys.argv:
         return variant2()
     if "--order" in sys.argv:

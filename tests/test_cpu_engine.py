@@ -78,3 +78,21 @@ def test_cpu_engine_refuses_checkpoint(tmp_path):
     m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
     with pytest.raises(raftmc.RaftmcError, match="checkpoint"):
         m.check_cpu(checkpoint_dir=tmp_path)
+
+
+EXTRAS = json.load(open(os.path.join(HERE, "golden", "extras.json")))
+
+
+@pytest.mark.parametrize("name", sorted(EXTRAS))
+def test_cpu_engine_classic_invariants(name):
+    """The opt-in classic Raft properties (ElectionSafety, LogMatching,
+    LeaderCompleteness, StateMachineSafety): both oracles' outcome."""
+    g = EXTRAS[name]
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    r = m.check_cpu(workers=4)
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == \
+        (g["generated"], g["distinct"], g["depth"], g["status"])
+    if g["status"] == "violation":
+        assert r["violated"] == g["violated"] and len(r["trace"]) == g["trace_len"]
+    else:
+        assert r["levels"] == g["levels"]

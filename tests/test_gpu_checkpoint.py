@@ -75,3 +75,35 @@ def test_recover_refuses_another_model(tmp_path):
         model(other).check(recover_dir=tmp_path)
     with pytest.raises(raftmc.RaftmcError, match="no checkpoint"):
         model(g).check(recover_dir=tmp_path / "missing")
+
+
+def test_resume_overflows_message_capacity(tmp_path):
+    """A snapshot packed with fewer message slots than later levels need: the
+    resumed check overflows the capacity after the resume level, re-runs from
+    the same snapshot with more slots (its rows widened on load) and reaches the
+    uninterrupted result -- it neither loops on the snapshot nor fails."""
+    g = SHIPPED["Raft_cfg"]
+    m = model(g)
+    m.selftest_set_hint_kmax(8)
+    a = m.check(max_depth=12, checkpoint_dir=tmp_path, checkpoint_minutes=0)
+    assert a["status"] == "stopped" and a["depth"] == 12
+    snap_slots = a["state_bytes"] // 4 - 1 - 4 * 3
+    assert snap_slots < g["max_msgs"]  # the resumed levels cannot fit the snapshot's rows
+    r = model(g).check(recover_dir=tmp_path)
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    assert r["levels"] == g["levels"]
+    assert r["state_bytes"] // 4 - 1 - 4 * 3 >= g["max_msgs"]
+
+
+def test_snapshot_replaces_the_previous_one(tmp_path):
+    """Each snapshot goes to a fresh subdirectory named by checkpoint.meta; the
+    previous one is removed only after the new one is complete."""
+    g = SHIPPED["Raft_cfg"]
+    model(g).check(max_depth=8, checkpoint_dir=tmp_path, checkpoint_minutes=0)
+    subs = sorted(p.name for p in tmp_path.iterdir() if p.is_dir())
+    assert len(subs) == 1 and subs[0].startswith("snap-")
+    assert sorted(p.name for p in (tmp_path / subs[0]).iterdir()) == \
+        ["fpset.bin", "frontier.bin", "trace_bind.bin", "trace_parent.bin"]
+    assert "snapshot %s" % subs[0][len("snap-"):] in (tmp_path / "checkpoint.meta").read_text()
+    r = model(g).check(recover_dir=tmp_path)
+    assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])

@@ -1,0 +1,111 @@
+"""GPU: BASELINE configs 2 and 5 at their scaled bounds, and the exhaustible
+rungs below them.
+
+* Config 2 (standard-raft, Value = {v1, v2}, MaxElections = 3:
+  configs/Raft_n3v2e3.cfg; Raft.tla:243 gates RequestVote on electionCtr) and
+  config 5 scaled (RaftFsync, Value = {v1, v2}, MaxElections = 3,
+  MaxRestarts = 1: configs/RaftFsync_n3v2e3r1.cfg; Restart truncates to
+  fsyncIndex, RaftFsync.tla:203-218) are beyond one GPU's capacity, so they
+  are pinned level by level (tests/golden/ladders.json): the C oracle to the
+  first level boundary past 2*10^7 distinct states, its first 12 levels also
+  reproduced by the literal Python oracle.  The GPU runs exactly that many
+  levels (max_depth) and must match every (generated, new) pair and the
+  hidden-variable collisions, single-shard and with 2 logical shards.
+* The exhaustible rungs -- the bench workload Raft_n3v2e2 (1.885 * 10^9
+  distinct) and RaftFsync_n3v1e2r1 (6.3 * 10^8) -- are checked in full:
+  counts equal to the committed record (tests/golden/exhausted.json, made by
+  tools/make_exhausted_record.py), its first levels equal to both oracles',
+  64-bit == 128-bit fingerprints, 2 logical shards == 1, host frontier ==
+  device frontier, and the first 25 levels equal to the CPU engine's.
+"""
+import json
+import os
+
+import pytest
+
+import raftmc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LAD = json.load(open(os.path.join(HERE, "golden", "ladders.json")))
+EXH = json.load(open(os.path.join(HERE, "golden", "exhausted.json")))
+BEYOND = ["raft_n3v2e3_cfg2", "fsync_n3v2e3r1_cfg5"]
+
+pytestmark = pytest.mark.gpu
+
+
+def model(g):
+    return raftmc.Model(module=g["module"], cfg_path=os.path.join(ROOT, g["cfg_path"]))
+
+
+def prefix_match(r, g):
+    assert r["levels"] == g["levels"]
+    assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
+    assert r["status"] == "stopped"
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+@pytest.mark.parametrize("name", sorted(LAD))
+def test_ladder_prefix_matches_oracle(name):
+    g = LAD[name]
+    prefix_match(model(g).check(max_depth=g["depth"]), g)
+
+
+@pytest.mark.parametrize("name", BEYOND)
+def test_ladder_prefix_logical_shards(name):
+    g = LAD[name]
+    prefix_match(model(g).check_logical(2, max_depth=g["depth"]), g)
+
+
+@pytest.mark.parametrize("name", BEYOND)
+def test_ladder_prefix_host_frontier(name):
+    g = LAD[name]
+    prefix_match(model(g).check(max_depth=g["depth"], host_frontier=1), g)
+
+
+_full = {}
+
+
+def full(name):
+    if name not in _full:
+        _full[name] = model(EXH[name]).check()
+    return _full[name]
+
+
+def same(r, e):
+    for k in ("generated", "distinct", "depth", "status", "levels", "hidden_var_collisions"):
+        assert r[k] == e[k], k
+
+
+@pytest.mark.parametrize("name", sorted(EXH))
+def test_rung_exhaustive_record(name):
+    e = EXH[name]
+    r = full(name)
+    same(r, e)
+    k = e["oracle_levels"]
+    assert r["levels"][:k] == LAD[name]["levels"][:k]
+
+
+@pytest.mark.parametrize("name", sorted(EXH))
+def test_rung_fp128_equals_fp64(name):
+    want = full(name)
+    raftmc.release_device_memory()  # the 128-bit set (32 B entries) needs the HBM the 64-bit one cached
+    same(model(EXH[name]).check(fp_bits=128), want)
+
+
+@pytest.mark.parametrize("name", sorted(EXH))
+def test_rung_two_logical_shards(name):
+    same(model(EXH[name]).check_logical(2), full(name))
+
+
+@pytest.mark.parametrize("name", sorted(EXH))
+def test_rung_host_frontier(name):
+    want = full(name)
+    raftmc.release_device_memory()
+    same(model(EXH[name]).check(host_frontier=1), want)
+
+
+@pytest.mark.parametrize("name", sorted(EXH))
+def test_rung_cpu_engine_prefix(name):
+    r = model(EXH[name]).check_cpu(max_depth=25)
+    assert r["levels"] == full(name)["levels"][:25]

@@ -1,0 +1,113 @@
+"""GPU: BFS levels in pinned host memory (rmc_options.host_frontier, raftmc
+-hostfrontier; SURVEY.md §7 hard part 5 and step 8).  The current and next
+level live in host pages and stream through double-buffered HBM windows, so
+the fingerprint set can take the whole device.  Whatever the mode -- always
+on the host, switched to the host in the middle of a level (the auto mode's
+reaction to HBM running out: before a chunk, or when the next level's buffer
+cannot grow), tiny pages that rows straddle -- every count, per-level pair,
+hidden-variable collision count, violation and trace must equal the oracle
+fixtures and the device-frontier search."""
+import json
+import os
+
+import pytest
+
+import raftmc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SMALL = json.load(open(os.path.join(HERE, "golden", "small.json")))
+ORDER = json.load(open(os.path.join(HERE, "golden", "order.json")))
+SHIPPED = json.load(open(os.path.join(HERE, "golden", "shipped.json")))
+UNSAFE = json.load(open(os.path.join(HERE, "golden", "unsafe.json")))
+MEDIUM = json.load(open(os.path.join(HERE, "golden", "medium.json")))
+
+pytestmark = pytest.mark.gpu
+
+
+def model(g):
+    if "cfg_path" in g:
+        return raftmc.Model(module=g["module"], cfg_path=os.path.join(ROOT, g["cfg_path"]))
+    return raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+
+
+def same(r, g):
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+@pytest.mark.parametrize("name", sorted(SMALL))
+def test_always_host_small(name):
+    g = SMALL[name]
+    same(model(g).check(host_frontier=1, chunk_parents=500), g)
+
+
+@pytest.mark.parametrize("name", sorted(ORDER))
+def test_always_host_tlc_order(name):
+    """TLC-order first-wins fixtures: chunks stream through alternating windows."""
+    g = ORDER[name]
+    same(model(g).check(host_frontier=1, chunk_parents=777), g)
+
+
+def test_always_host_small_pages(monkeypatch):
+    """Pages of 1,000 rows: chunks and output batches straddle many pages, and
+    consumed pages are recycled while the level is read."""
+    monkeypatch.setenv("RMC_HOST_PAGE_ROWS", "1000")
+    g = SHIPPED["Raft_cfg"]
+    same(model(g).check(host_frontier=1, chunk_parents=30000), g)
+
+
+@pytest.mark.parametrize("how", ["", ":grow"])
+@pytest.mark.parametrize("level", [12, 30])
+def test_auto_switch_mid_level(monkeypatch, how, level):
+    """Auto mode moving the frontiers to the host in the middle of a level:
+    before a chunk (as when the set cannot grow), or with a chunk expanded
+    and marked but not yet materialized (the next level's buffer cannot grow)."""
+    monkeypatch.setenv("RMC_HOST_FRONTIER_AT", "%d%s" % (level, how))
+    g = SHIPPED["Raft_cfg"]
+    same(model(g).check(host_frontier=0, chunk_parents=20000), g)
+
+
+def test_never_host_is_unchanged(monkeypatch):
+    monkeypatch.setenv("RMC_HOST_FRONTIER_AT", "12")
+    g = SHIPPED["Raft_cfg"]
+    same(model(g).check(host_frontier=-1, chunk_parents=20000), g)
+
+
+@pytest.mark.parametrize("fp_bits", [64, 128])
+def test_always_host_shipped(fp_bits):
+    g = SHIPPED["RaftFsync_cfg"]
+    same(model(g).check(host_frontier=1, fp_bits=fp_bits), g)
+
+
+VIOL = dict(UNSAFE)
+VIOL.update({k: v for k, v in MEDIUM.items() if v["status"] == "violation"})
+
+
+@pytest.mark.parametrize("name", sorted(VIOL))
+@pytest.mark.parametrize("chunk", [9, 1000, 0])
+def test_always_host_violation(name, chunk):
+    """A violation found with the host frontier: TLC's counts at the failing
+    state (its chunk re-expanded from the host pages) and the same trace."""
+    g = VIOL[name]
+    dev = model(g).check(chunk_parents=chunk)
+    r = model(g).check(host_frontier=1, chunk_parents=chunk)
+    assert r["status"] == "violation" and r["violated"] == g["violated"]
+    assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
+    assert r["trace"] == dev["trace"] and len(r["trace"]) == g["trace_len"]
+
+
+def test_host_checkpoint_and_recover(tmp_path):
+    """Snapshots written from host pages; a resumed check on the host frontier."""
+    g = SHIPPED["Raft_cfg"]
+    a = model(g).check(host_frontier=1, max_depth=20, checkpoint_dir=tmp_path, checkpoint_minutes=0)
+    assert a["status"] == "stopped"
+    same(model(g).check(host_frontier=1, recover_dir=tmp_path), g)
+    same(model(g).check(recover_dir=tmp_path), g)
+
+
+def test_host_frontier_refused_elsewhere():
+    g = SMALL["raft_n3v1e1"]
+    with pytest.raises(raftmc.RaftmcError, match="host_frontier"):
+        model(g).check_logical(2, host_frontier=1)
