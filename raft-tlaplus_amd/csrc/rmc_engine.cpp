@@ -1008,8 +1008,11 @@ struct HostFrontierStreams {
   }
 };
 
-int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
+int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   auto t0 = std::chrono::steady_clock::now();
+  rmc_options opt_v = *opt_in;  // RMC_VERBOSE=1: per-level progress from any caller (bench.py, tests)
+  if (getenv("RMC_VERBOSE") && atoi(getenv("RMC_VERBOSE")) > 0) opt_v.verbose = 1;
+  const rmc_options* opt = &opt_v;
   Model& M = m->M;
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
   if (opt->fp_bits && opt->fp_bits != 64 && opt->fp_bits != 128)
@@ -1130,11 +1133,15 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
       grown = false;
     }
     if (!grown) return false;
+    const auto tr1 = now();
     HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * ew * 8, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    const auto tr2 = now();
     launch_rehash(table.as<unsigned long long>(), slots, A.table2.as<unsigned long long>(), nslots - 1,
                   stbuf.as<DevStatus>(), stream, ew);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(stream));
+    const auto tr3 = now();
     std::swap(table.p, A.table2.p);
     std::swap(table.bytes, A.table2.bytes);
     slots = nslots;
@@ -1142,7 +1149,8 @@ int check_impl(rmc_model* m, const rmc_options* opt, rmc_result* res) {
     grows++;
     rehash_s += secs(tr0, now());
     if (opt->verbose)
-      fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs)\n", __builtin_ctzll(slots), secs(tr0, now()));
+      fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs: allocate %.3f, fill %.3f, rehash %.3f, free %.3f)\n",
+              __builtin_ctzll(slots), secs(tr0, now()), secs(tr0, tr1), secs(tr1, tr2), secs(tr2, tr3), secs(tr3, now()));
     return true;
   };
 

@@ -67,7 +67,18 @@ enum { FPS_INSERT = 0, FPS_GROUP = 1, FPS_CAS = 2, FPS_CAS_WON = 3, FPS_MIN = 4 
 // too long (the table is too full: the driver grows it and redoes the chunk,
 // whose inserts are idempotent).
 //
-// The probe run is READ, four entries (64 B) per group of plain 16 B loads
+// Two protocols.  The default (below, after #else): the first four entries of
+// the probe run are read with 16 B loads issued together; a hit decides
+// without an atomic (earlier level) or with one atomicMin (same level); else a
+// CAS per slot from the first EMPTY-or-other slot on.  The alternative
+// (-DRMC_FP_READPROBE) reads the whole run in groups of four and takes at most
+// one CAS per probe step.  Measured on the bench workload (r03, CLI, 8M
+// parents per launch, interleaved runs): k_expand 918 ms per check with the
+// default vs 1025 ms with the read probe, though the read probe writes less
+// (WRITE_SIZE 1.43 vs 2.06 GB per launch): its loop of dependent 64 B group
+// loads is longer than the default's single group + CAS.
+//
+// RMC_FP_READPROBE: the probe run is READ, four entries (64 B) per group of plain 16 B loads
 // issued together, up to the first entry that is fp or EMPTY.  Keys are never
 // removed or moved while a level is expanded, so a key read with a plain load
 // is really there -- an earlier level's copy of fp is final (no atomic, no
@@ -80,7 +91,7 @@ enum { FPS_INSERT = 0, FPS_GROUP = 1, FPS_CAS = 2, FPS_CAS_WON = 3, FPS_MIN = 4 
 // 'Global float atomics': the r02 protocol's CAS per slot past the first
 // four entries was a memory round trip and a WRITE_SIZE transaction per
 // occupied slot passed.)
-#ifndef RMC_FP_LEGACY
+#ifdef RMC_FP_READPROBE
 __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T, unsigned long long mask,
                                                            unsigned long long fp, unsigned long long val,
                                                            unsigned long long floor, DevStatus* st) {
@@ -135,7 +146,7 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
   return EMPTY;
 }
 #else
-// r02 protocol (kept for A/B measurement): four entries read, then a CAS per probe
+// default protocol: four entries read, then a CAS per probe
 __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T, unsigned long long mask,
                                                            unsigned long long fp, unsigned long long val,
                                                            unsigned long long floor, DevStatus* st) {

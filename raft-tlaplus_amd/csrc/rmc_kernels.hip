@@ -95,7 +95,9 @@ struct Tile {
 
 // Dynamic LDS layout of k_expand (bytes; the launch computes the same).
 constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
+#ifdef RMC_TILE_DEDUP
 constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-successor round
+#endif
 struct ExpandLds {
   int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, bytes;
 };
@@ -126,8 +128,12 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
   o += (nfixed + 1) * 4;
   L.off_Live = o;  // per parent: bitmask over DOMAIN messages that can enable an action (msg_live)
   o += PB * LIVE_WORDS * 4;
+#ifdef RMC_TILE_DEDUP
   const int hash_end = L.off_Hash + DEDUP * 12;
   L.bytes = o > hash_end ? o : hash_end;
+#else
+  L.bytes = o;
+#endif
   return L;
 }
 
@@ -495,7 +501,10 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   //      candidate gbase + idx, so a wave's candidate stores are contiguous
   //      (binding-major enumeration scattered them: one 32 B write request per
   //      8 B store, ~0.7 GB of extra HBM writes per launch on the bench cfg).
-#ifndef RMC_NO_DEDUP
+#ifdef RMC_TILE_DEDUP
+  // Measured and not the default (r03, bench workload, CLI): k_expand 933 ms
+  // per check with the tile dedup vs 918 ms without -- the LDS table's three
+  // barriers per 256-successor round cost more than the HBM probes it saves.
   if constexpr (FPW == 1) {
     if (!sharded) {
       // Tile-local dedup first.  A BFS level's duplicates are same-level ones
@@ -812,7 +821,6 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int words = cM.words, Wp = words | 1;
   uint32_t* sS = (uint32_t*)lds;
-  uint32_t* sInv = sS + PB * Wp;  // per thread: header + server words of its successor (odd stride)
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
   const uint32_t start = par_off[p0];
@@ -873,14 +881,8 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
       tr_parent[out_base_global + dst] = pg;
       tr_bind[out_base_global + dst] = (uint16_t)b;
       // invariants read only the header and the server words: check them on
-      // an LDS copy instead of reading the row back from HBM
-      uint32_t* iv = sInv + tid * (1 + 4 * N);
-      iv[0] = d.hdr;
-#pragma unroll
-      for (int i = 0; i < N; i++)
-#pragma unroll
-        for (int t = 0; t < 4; t++) iv[1 + 4 * i + t] = i == d.srv ? d.w[t] : s.S[1 + 4 * i + t];
-      PState<SPEC, N> ns{iv};
+      // the parent + delta in place (SuccView), not on the row written to HBM
+      const SuccView<SPEC, N> ns(s, d);
       int ierr = 0;
       int bad = check_invariants<SPEC, N>(ns, cM, ierr);
       if (ierr) atomicMin(&st->inv_err_key, order_key(pg, (int)(ob >> 16), b));
@@ -1115,7 +1117,7 @@ struct Launch {
   static void materialize(const LevelArgs& a, hipStream_t s) {
     constexpr int PB = Tile<N>::PB;  // must be k_expand's tile: a tile's candidates are contiguous only within one expand tile
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
-    size_t lds_bytes = ((size_t)PB * (a.model->words | 1) + MAT_T * (1 + 4 * N)) * 4;
+    size_t lds_bytes = (size_t)PB * (a.model->words | 1) * 4;
     hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(MAT_T), lds_bytes, s, a.frontier, a.nparents,
                        a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
                        a.tr_parent, a.tr_bind, a.st);

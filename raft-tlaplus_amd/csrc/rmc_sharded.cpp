@@ -34,6 +34,9 @@
 #include <vector>
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
+#include <signal.h>
+#include <cerrno>
 #include <unistd.h>
 #include <rccl/rccl.h>
 #include "rmc_internal.h"
@@ -140,6 +143,7 @@ struct ShmComm : Comm {
     int ready;
     int count;  // arrivals at the current barrier
     int sense;  // flips when the last rank arrives
+    int owner;  // rank 0's pid (a segment left by a dead run has a dead owner)
   };
   static constexpr size_t SLOT = 8u << 20;   // bytes per (src, dst) slot and round
   static constexpr int GATHER_MAX = 64;      // values per rank in one allgather
@@ -157,20 +161,51 @@ struct ShmComm : Comm {
     local = {r};
     stream = s;
     bytes = 256 + (size_t)W * GATHER_MAX * 8 + (size_t)W * W * SLOT;
-    int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
-    if (fd < 0) throw std::runtime_error("shm_open " + name + " failed");
-    if (ftruncate(fd, (off_t)bytes) != 0) { close(fd); throw std::runtime_error("ftruncate of the shm segment failed"); }
-    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (p == MAP_FAILED) throw std::runtime_error("mmap of the shm segment failed");
-    base = (unsigned char*)p;
     if (rank == 0) {
+      // a fresh segment: a stale one of the same name (a crashed run) is
+      // unlinked first; its space is allocated now, so a small /dev/shm is a
+      // clean error here rather than a SIGBUS on first write
+      (void)shm_unlink(name.c_str());
+      int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0) throw std::runtime_error("shm_open " + name + " failed: " + strerror(errno));
+      int e = posix_fallocate(fd, 0, (off_t)bytes);
+      if (e != 0) {
+        close(fd);
+        shm_unlink(name.c_str());
+        throw std::runtime_error("shm transport: cannot allocate " + std::to_string(bytes >> 20) + " MiB in /dev/shm: " +
+                                 strerror(e));
+      }
+      void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      close(fd);
+      if (p == MAP_FAILED) throw std::runtime_error("mmap of the shm segment failed");
+      base = (unsigned char*)p;
       __atomic_store_n(&hdr()->count, 0, __ATOMIC_RELAXED);
       __atomic_store_n(&hdr()->sense, 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&hdr()->owner, (int)getpid(), __ATOMIC_RELAXED);
       __atomic_store_n(&hdr()->ready, 1, __ATOMIC_RELEASE);
     } else {
-      for (int t = 0; !__atomic_load_n(&hdr()->ready, __ATOMIC_ACQUIRE); t++) {
+      // attach to rank 0's segment: wait until it exists, is initialised and
+      // is owned by a live process (a dead run's leftover is not joined)
+      for (int t = 0;; t++) {
         if (t > 600000) throw std::runtime_error("shm transport: rank 0 never initialised " + name);
+        int fd = shm_open(name.c_str(), O_RDWR, 0600);
+        if (fd >= 0) {
+          struct stat st;
+          if (fstat(fd, &st) == 0 && (size_t)st.st_size >= bytes) {
+            void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            if (p != MAP_FAILED) {
+              Hdr* h = reinterpret_cast<Hdr*>(p);
+              const int own = __atomic_load_n(&h->ready, __ATOMIC_ACQUIRE) ? __atomic_load_n(&h->owner, __ATOMIC_RELAXED) : 0;
+              if (own > 0 && (kill(own, 0) == 0 || errno == EPERM)) {
+                close(fd);
+                base = (unsigned char*)p;
+                break;
+              }
+              munmap(p, bytes);
+            }
+          }
+          close(fd);
+        }
         usleep(100);
       }
     }
@@ -497,6 +532,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     for (Shard& s : sh) s.next_fill = 0;
     floor = (lbase + 1) << VAL_FLOOR_SHIFT;  // entries below: earlier levels
     for (unsigned long long c = 0; c < rounds && !stop;) {
+      const unsigned long long gen_round0 = gen_lvl, gw_round0 = GW;  // the level's counts before this round
       // ---- room in each owner's table for the local inserts of k_expand (at
       //      the highest rate of new states per parent seen; a full table is
       //      grown and the round redone below)
@@ -824,6 +860,48 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           bad_key = vk;
         }
         stop = true;
+        // TLC's counts at the failing state (as rmc_check): this round's
+        // successors of the parents before the failing one, plus the failing
+        // parent's up to the failing successor (none for an evaluation error
+        // in Next); distinct = the winners among them.  Each shard counts its
+        // own block of the round's parents; the sums are allgathered.
+        const bool parent_key = status == 2 && ek <= iek;
+        const unsigned long long fpg = bad_key >> 20;
+        const int ordv = (int)((bad_key >> 10) & 0x3FF);
+        for (int i = 0; i < NL; i++) {
+          Shard& s = sh[i];
+          unsigned long long gi = 0, di = 0;
+          if (s.n) {
+            const unsigned long long start = lbase + c * W * CH + (unsigned long long)s.id * CH;
+            const unsigned long long k = fpg <= start ? 0 : std::min(s.n, fpg - start);
+            if (k) {
+              std::vector<uint32_t> hn(k), hw(k);
+              HIPCHK(hipMemcpy(hn.data(), s.B->pn.p, k * 4, hipMemcpyDeviceToHost));
+              HIPCHK(hipMemcpy(hw.data(), s.B->pwin.p, k * 4, hipMemcpyDeviceToHost));
+              for (unsigned long long p = 0; p < k; p++) { gi += hn[p]; di += hw[p]; }
+            }
+            if (!parent_key && fpg >= start && fpg < start + s.n) {
+              const unsigned long long pl = fpg - start;
+              uint32_t off = 0, nn = 0;
+              HIPCHK(hipMemcpy(&off, s.B->poff.as<uint32_t>() + pl, 4, hipMemcpyDeviceToHost));
+              HIPCHK(hipMemcpy(&nn, s.B->pn.as<uint32_t>() + pl, 4, hipMemcpyDeviceToHost));
+              std::vector<uint32_t> ob(nn);
+              std::vector<uint16_t> win(nn);
+              if (nn) {
+                HIPCHK(hipMemcpy(ob.data(), s.B->cob.as<uint32_t>() + off, nn * 4, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(win.data(), s.B->cwin.as<uint16_t>() + off, nn * 2, hipMemcpyDeviceToHost));
+              }
+              for (uint32_t q = 0; q < nn; q++)
+                if ((int)(ob[q] >> 16) == ordv) { gi += q + 1; di += win[q]; break; }
+            }
+          }
+          rows[i] = {gi, di};
+        }
+        comm.allgather(rows, all, 2);
+        unsigned long long gsum = 0, dsum = 0;
+        for (int r = 0; r < W; r++) { gsum += all[2 * r]; dsum += all[2 * r + 1]; }
+        gen_lvl = gen_round0 + gsum;
+        GW = gw_round0 + dsum;
       }
       c++;
     }

@@ -1510,24 +1510,59 @@ RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d,
   for (int i = 0; i < N; i++)
 #pragma unroll
     for (int t = 0; t < 4; t++) emit(i == d.srv ? d.w[t] : s.S[1 + 4 * i + t]);
-#pragma unroll 1
-  for (int k = 0; k < n; k++) {
-    uint32_t w = s.msg(k);
+  // The message slots, in lockstep: every lane runs the same M.kmax steps and
+  // makes the same emits, so a wave's 16 B stores are whole-wave instructions
+  // (a data-dependent merge loop made each lane store at its own iterations:
+  // partial-wave store instructions).  Step j outputs the smaller of the next
+  // parent message (in-place ops applied) and the next insert; past both, 0.
+  int k = 0;
+  auto pmsg = [&](int kk) {
+    uint32_t w = kk < n ? s.msg(kk) : NONE;
 #pragma unroll
     for (int q = 0; q < MAXOPS; q++)
-      if (q < d.nops && d.opk[q] == k) w = d.opc[q];
-    while (ins[0] < w) emit(pop_ins());
-    emit(w);
-  }
-  while (ins[0] != NONE) emit(pop_ins());
+      if (q < d.nops && d.opk[q] == kk) w = d.opc[q];
+    return w;
+  };
+  uint32_t wp = pmsg(0);
 #pragma unroll 1
-  for (int k = nn; k < M.kmax; k++) emit(0);
+  for (int j = 0; j < M.kmax; j++) {
+    const bool take_ins = ins[0] < wp;
+    const uint32_t w = take_ins ? ins[0] : wp;
+    emit(w == NONE ? 0u : w);
+    if (take_ins) {
+      (void)pop_ins();
+    } else {
+      k++;
+      wp = pmsg(k);
+    }
+  }
   return E_NONE;
 }
 
 // ------------------------------------------------------------- invariants
+// The successor's header and server words, read in place from the parent and
+// the Delta (k_materialize checks the invariants through it: no copy).  It
+// holds values, not references: a reference to the Delta stored in an
+// aggregate makes the compiler keep the Delta in scratch.
 template <int SPEC, int N>
-RMC_HD bool inv_no_log_divergence(const PState<SPEC, N>& s, int& err) {  // Raft.tla:588-596
+struct SuccView {
+  const uint32_t* S;  // the parent's row
+  uint32_t h, w0, w1, w2, w3;
+  int srv;
+  RMC_HD SuccView(const PState<SPEC, N>& p, const Delta& d)
+      : S(p.S), h(d.hdr), w0(d.w[0]), w1(d.w[1]), w2(d.w[2]), w3(d.w[3]), srv(d.srv) {}
+  RMC_HD uint32_t hdr() const { return h; }
+  RMC_HD uint32_t A(int i) const { return i == srv ? w0 : S[1 + 4 * i]; }
+  RMC_HD uint32_t B(int i) const { return i == srv ? w1 : S[2 + 4 * i]; }
+  RMC_HD uint32_t Cw(int i) const { return i == srv ? w2 : S[3 + 4 * i]; }
+  RMC_HD uint32_t Dw(int i) const { return i == srv ? w3 : S[4 + 4 * i]; }
+  RMC_HD int term(int i) const { return a_term(A(i)); }
+  RMC_HD int st(int i) const { return a_st(A(i)); }
+  RMC_HD int len(int i) const { return a_len(A(i)); }
+};
+
+template <int SPEC, int N, class St>
+RMC_HD bool inv_no_log_divergence(const St& s, int& err) {  // Raft.tla:588-596
   for (int s2 = 0; s2 < N; s2++)
     for (int s1 = 0; s1 < N; s1++) {
       if (s1 == s2) continue;
@@ -1540,8 +1575,8 @@ RMC_HD bool inv_no_log_divergence(const PState<SPEC, N>& s, int& err) {  // Raft
     }
   return true;
 }
-template <int SPEC, int N>
-RMC_HD bool inv_leader_has_all_acked(const PState<SPEC, N>& s, const Model& M) {  // Raft.tla:604-620
+template <int SPEC, int N, class St>
+RMC_HD bool inv_leader_has_all_acked(const St& s, const Model& M) {  // Raft.tla:604-620
   for (int v = 0; v < M.V; v++) {
     if (h_acked(s.hdr(), v) != 2) continue;
     for (int i = 0; i < N; i++) {
@@ -1559,8 +1594,8 @@ RMC_HD bool inv_leader_has_all_acked(const PState<SPEC, N>& s, const Model& M) {
   }
   return true;
 }
-template <int SPEC, int N>
-RMC_HD bool inv_committed_majority(const PState<SPEC, N>& s, int& err) {  // Raft.tla:625-636
+template <int SPEC, int N, class St>
+RMC_HD bool inv_committed_majority(const St& s, int& err) {  // Raft.tla:625-636
   bool any = false;
   for (int i = 0; i < N; i++) if (s.st(i) == LEADER && a_commit(s.A(i)) > 0) any = true;
   if (!any) return true;
@@ -1583,8 +1618,8 @@ RMC_HD bool inv_committed_majority(const PState<SPEC, N>& s, int& err) {  // Raf
   }
   return false;
 }
-template <int SPEC, int N>
-RMC_HD bool inv_never_two_leaders(const PState<SPEC, N>& s) {  // KRaft.tla:916-921
+template <int SPEC, int N, class St>
+RMC_HD bool inv_never_two_leaders(const St& s) {  // KRaft.tla:916-921
   for (int i = 0; i < N; i++)
     for (int j = 0; j < N; j++) {
       const int li = a_voted(s.A(i)), lj = a_voted(s.A(j));
@@ -1592,8 +1627,8 @@ RMC_HD bool inv_never_two_leaders(const PState<SPEC, N>& s) {  // KRaft.tla:916-
     }
   return true;
 }
-template <int SPEC, int N>
-RMC_HD bool inv_no_illegal_state(const PState<SPEC, N>& s) {  // KRaft.tla:887-889
+template <int SPEC, int N, class St>
+RMC_HD bool inv_no_illegal_state(const St& s) {  // KRaft.tla:887-889
   for (int i = 0; i < N; i++)
     if (kr_st(s.A(i)) == KS_ILLEGAL) return false;
   return true;
@@ -1606,8 +1641,8 @@ RMC_HD bool inv_no_illegal_state(const PState<SPEC, N>& s) {  // KRaft.tla:887-8
 // evaluation error.
 //   ElectionSafety == \A s1, s2 \in Server : (s1 # s2 /\ state[s1] = Leader /\ state[s2] = Leader)
 //                       => currentTerm[s1] # currentTerm[s2]
-template <int SPEC, int N>
-RMC_HD bool inv_election_safety(const PState<SPEC, N>& s) {
+template <int SPEC, int N, class St>
+RMC_HD bool inv_election_safety(const St& s) {
   for (int i = 0; i < N; i++)
     for (int j = i + 1; j < N; j++)
       if (a_st(s.A(i)) == LEADER && a_st(s.A(j)) == LEADER && a_term(s.A(i)) == a_term(s.A(j))) return false;
@@ -1615,8 +1650,8 @@ RMC_HD bool inv_election_safety(const PState<SPEC, N>& s) {
 }
 //   LogMatching == \A s1, s2 \in Server : \A i \in 1..Min({Len(log[s1]), Len(log[s2])}) :
 //                    log[s1][i].term = log[s2][i].term => SubSeq(log[s1], 1, i) = SubSeq(log[s2], 1, i)
-template <int SPEC, int N>
-RMC_HD bool inv_log_matching(const PState<SPEC, N>& s) {
+template <int SPEC, int N, class St>
+RMC_HD bool inv_log_matching(const St& s) {
   for (int i = 0; i < N; i++)
     for (int j = i + 1; j < N; j++) {
       const int L = a_len(s.A(i)) < a_len(s.A(j)) ? a_len(s.A(i)) : a_len(s.A(j));
@@ -1635,8 +1670,8 @@ RMC_HD bool inv_log_matching(const PState<SPEC, N>& s) {
 //         \A s \in Server : \A i \in 1..Min({commitIndex[s], Len(log[s])}) :
 //           i <= Len(log[l]) /\ log[l][i] = log[s][i]
 // (a leader of the newest term holds every entry any server has committed)
-template <int SPEC, int N>
-RMC_HD bool inv_leader_completeness(const PState<SPEC, N>& s) {
+template <int SPEC, int N, class St>
+RMC_HD bool inv_leader_completeness(const St& s) {
   for (int l = 0; l < N; l++) {
     const uint32_t al = s.A(l);
     if (a_st(al) != LEADER) continue;
@@ -1656,8 +1691,8 @@ RMC_HD bool inv_leader_completeness(const PState<SPEC, N>& s) {
 }
 //   StateMachineSafety == \A s1, s2 \in Server :
 //       \A i \in 1..Min({commitIndex[s1], commitIndex[s2], Len(log[s1]), Len(log[s2])}) : log[s1][i] = log[s2][i]
-template <int SPEC, int N>
-RMC_HD bool inv_state_machine_safety(const PState<SPEC, N>& s) {
+template <int SPEC, int N, class St>
+RMC_HD bool inv_state_machine_safety(const St& s) {
   for (int i = 0; i < N; i++)
     for (int j = i + 1; j < N; j++) {
       const uint32_t ai = s.A(i), aj = s.A(j);
@@ -1670,20 +1705,20 @@ RMC_HD bool inv_state_machine_safety(const PState<SPEC, N>& s) {
   return true;
 }
 // returns -1 if all hold, else the position (in cfg order) of the violated one
-template <int SPEC, int N>
-RMC_HD int check_invariants(const PState<SPEC, N>& s, const Model& M, int& err) {
+template <int SPEC, int N, class St>
+RMC_HD int check_invariants(const St& s, const Model& M, int& err) {
   for (int q = 0; q < M.ninv; q++) {
     bool ok = true;
     switch (M.inv[q]) {
-      case 0: ok = inv_leader_has_all_acked(s, M); break;
-      case 1: ok = inv_no_log_divergence(s, err); break;
-      case 2: ok = inv_committed_majority(s, err); break;
-      case 3: ok = inv_never_two_leaders(s); break;
-      case 4: ok = inv_no_illegal_state(s); break;
-      case 5: ok = inv_election_safety(s); break;
-      case 6: ok = inv_log_matching(s); break;
-      case 7: ok = inv_leader_completeness(s); break;
-      case 8: ok = inv_state_machine_safety(s); break;
+      case 0: ok = inv_leader_has_all_acked<SPEC, N>(s, M); break;
+      case 1: ok = inv_no_log_divergence<SPEC, N>(s, err); break;
+      case 2: ok = inv_committed_majority<SPEC, N>(s, err); break;
+      case 3: ok = inv_never_two_leaders<SPEC, N>(s); break;
+      case 4: ok = inv_no_illegal_state<SPEC, N>(s); break;
+      case 5: ok = inv_election_safety<SPEC, N>(s); break;
+      case 6: ok = inv_log_matching<SPEC, N>(s); break;
+      case 7: ok = inv_leader_completeness<SPEC, N>(s); break;
+      case 8: ok = inv_state_machine_safety<SPEC, N>(s); break;
     }
     if (err) return -2;
     if (!ok) return q;

@@ -59,6 +59,9 @@ def test_logical_shards_violation_trace(name, shards):
     assert r["status"] == "violation" and r["violated"] == g["violated"]
     assert r["trace"][0][0] == "Initial predicate"
     assert len(r["trace"]) == g["trace_len"]
+    # TLC's counts at the failing state, as the single-shard search reports them
+    assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
+    assert r["levels"] == g["levels"]
 
 
 def test_rccl_single_rank():
@@ -100,3 +103,4 @@ def test_logical_shards_unsafe(name, shards):
     r = m.check_logical(shards, chunk_parents=50)
     assert r["status"] == "violation" and r["violated"] == g["violated"]
     assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]
+    assert (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])

@@ -58,3 +58,5 @@ def test_multiprocess_shards_violation():
     g = json.load(open(os.path.join(HERE, "golden", "kraft.json")))["kraft_n3v1e1r1"]
     for r in run_ranks(2, "kraft.json", "kraft_n3v1e1r1"):
         assert r["status"] == "violation" and r["violated"] == g["violated"] and r["depth"] == g["depth"]
+        # TLC's counts at the failing state, summed over the ranks' blocks of the round
+        assert (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])
