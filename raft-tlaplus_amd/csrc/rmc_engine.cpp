@@ -1123,36 +1123,6 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   // ---- growth: room for `need` entries at <= 0.75 load (0.9 once HBM is full)
   bool full_ok = false;
   unsigned long long grows = 0;
-  auto t_grow = [&](unsigned long long nslots) {  // rehash into nslots (entries and values kept)
-    auto tr0 = now();
-    HIPCHK(hipStreamSynchronize(stream));
-    bool grown = true;
-    try {
-      A.table2.ensure(nslots * ew * 8);
-    } catch (OutOfDeviceMemory&) {
-      grown = false;
-    }
-    if (!grown) return false;
-    const auto tr1 = now();
-    HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * ew * 8, stream));
-    HIPCHK(hipStreamSynchronize(stream));
-    const auto tr2 = now();
-    launch_rehash(table.as<unsigned long long>(), slots, A.table2.as<unsigned long long>(), nslots - 1,
-                  stbuf.as<DevStatus>(), stream, ew);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(stream));
-    const auto tr3 = now();
-    std::swap(table.p, A.table2.p);
-    std::swap(table.bytes, A.table2.bytes);
-    slots = nslots;
-    if (A.table2.bytes >= (1ULL << 30)) A.table2.release();  // large searches need the HBM more than a spare
-    grows++;
-    rehash_s += secs(tr0, now());
-    if (opt->verbose)
-      fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs: allocate %.3f, fill %.3f, rehash %.3f, free %.3f)\n",
-              __builtin_ctzll(slots), secs(tr0, now()), secs(tr0, tr1), secs(tr1, tr2), secs(tr2, tr3), secs(tr3, now()));
-    return true;
-  };
 
   // ---- level 1: Init (Raft.tla:213-218)
   std::vector<uint32_t> init = init_state(M);
@@ -1267,6 +1237,38 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   unsigned long long hwin_c0[2] = {~0ULL, ~0ULL};  // first row of the chunk each input window holds
   unsigned long long lvl_c0 = 0, lvl_next_n = 0;   // chunk-loop position (for a switch to the host frontier)
   double hf_copy_s = 0;
+  // The host-frontier windows (two of a chunk's parents, two of 3 rows per
+  // parent), allocated while HBM still has room: in the auto mode as soon as a
+  // growth would leave less than their size free.  HBM the device frontiers
+  // release when the search moves to the host is not reusable at once on this
+  // driver (a hipMalloc right after hipMemRelease of the frontiers failed on
+  // the GPU box; profiles/r03/vmm_release_probe.txt), so the windows must not
+  // depend on it.
+  const size_t win_in_bytes = chunk * W * 4, win_out_bytes = 3 * chunk * W * 4;
+  bool windows = false;
+  auto reserve_windows = [&]() {
+    if (windows) return;
+    A.hwin_in[0].ensure(win_in_bytes);
+    A.hwin_in[1].ensure(win_in_bytes);
+    A.hwin_out[0].ensure(win_out_bytes);
+    A.hwin_out[1].ensure(win_out_bytes);
+    windows = true;
+  };
+  auto before_growth = [&](size_t request) {  // auto mode: keep the windows' HBM available
+    if (hf || windows || hf_opt != 0) return;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return;
+    const size_t wb = 2 * (win_in_bytes + win_out_bytes);
+    if (fr < request + wb + (2ULL << 30)) {
+      try {
+        reserve_windows();
+      } catch (OutOfDeviceMemory&) {
+      }
+      if (opt->verbose)
+        fprintf(stderr, "[rmc] host-frontier windows %s (%.1f GiB)\n", windows ? "reserved" : "could not be reserved",
+                wb / 1073741824.0);
+    }
+  };
   // Move the current level (all of it) and the next level so far to host
   // pages, free the device frontiers, and continue in host-frontier mode.
   auto enter_hf = [&]() {
@@ -1286,12 +1288,42 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     cur = nxt = nullptr;
     hf = true;
     hwin_c0[0] = hwin_c0[1] = ~0ULL;
-    A.hwin_in[0].ensure(chunk * W * 4);
-    A.hwin_in[1].ensure(chunk * W * 4);
+    reserve_windows();
     hf_copy_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - th0).count();
     if (opt->verbose)
       fprintf(stderr, "[rmc] frontier moved to host memory at depth %u (%.1f GiB of pinned pages, limit %.1f GiB)\n",
               depth, pool.allocated / 1073741824.0, pool.limit / 1073741824.0);
+  };
+  auto t_grow = [&](unsigned long long nslots) {  // rehash into nslots (entries and values kept)
+    auto tr0 = now();
+    HIPCHK(hipStreamSynchronize(stream));
+    bool grown = true;
+    before_growth(nslots * ew * 8);
+    try {
+      A.table2.ensure(nslots * ew * 8);
+    } catch (OutOfDeviceMemory&) {
+      grown = false;
+    }
+    if (!grown) return false;
+    const auto tr1 = now();
+    HIPCHK(hipMemsetAsync(A.table2.p, 0xFF, nslots * ew * 8, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    const auto tr2 = now();
+    launch_rehash(table.as<unsigned long long>(), slots, A.table2.as<unsigned long long>(), nslots - 1,
+                  stbuf.as<DevStatus>(), stream, ew);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(stream));
+    const auto tr3 = now();
+    std::swap(table.p, A.table2.p);
+    std::swap(table.bytes, A.table2.bytes);
+    slots = nslots;
+    if (A.table2.bytes >= (1ULL << 30)) A.table2.release();  // large searches need the HBM more than a spare
+    grows++;
+    rehash_s += secs(tr0, now());
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs: allocate %.3f, fill %.3f, rehash %.3f, free %.3f)\n",
+              __builtin_ctzll(slots), secs(tr0, now()), secs(tr0, tr1), secs(tr1, tr2), secs(tr2, tr3), secs(tr3, now()));
+    return true;
   };
   auto t_fit = [&](unsigned long long need) {
     if (need * 4 <= slots * 3) return;
@@ -1522,6 +1554,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
             if (nb.bytes < need) {
               auto tg0 = now();
               HIPCHK(hipStreamSynchronize(stream));
+              before_growth(need - nb.bytes);
               nb.ensure(need);
               cur = (cur_is_a ? fa : fb).as<uint32_t>();
               nxt = nb.as<uint32_t>();

@@ -238,10 +238,16 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   unsigned long long t_prev = clock64();
 #endif
   // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
-  const uint32_t* src = frontier + p0 * (unsigned long long)words;
-  for (int q = tid; q < np * words; q += 256) {
-    int p = q / words;
-    sS[p * L.Wp + (q - p * words)] = src[q];
+  // rows are a multiple of 4 words (16 B aligned): 16 B loads, 4 LDS writes each
+  const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
+  for (int q = tid; q < np * (words >> 2); q += 256) {
+    const uint4 v = src[q];
+    const int w = q << 2, p = w / words;
+    uint32_t* d = sS + p * L.Wp + (w - p * words);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
   }
   for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
   for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
@@ -824,10 +830,15 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
   const uint32_t start = par_off[p0];
-  const uint32_t* src = frontier + p0 * (unsigned long long)words;
-  for (int q = tid; q < np * words; q += MAT_T) {
-    int p = q / words;
-    sS[p * Wp + (q - p * words)] = src[q];
+  const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
+  for (int q = tid; q < np * (words >> 2); q += MAT_T) {
+    const uint4 v = src[q];
+    const int w = q << 2, p = w / words;
+    uint32_t* d = sS + p * Wp + (w - p * words);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
   }
   for (int q = tid; q < cM.nfixed; q += MAT_T) sDesc[q] = cM.fb_desc[q];
   if (tid < np) {
