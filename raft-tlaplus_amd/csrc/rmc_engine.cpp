@@ -1048,7 +1048,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   // Fingerprint set: starts at hash_slots (or at the size the last check of
   // this model ended with -- TLC's preallocated FPSet, -fpmem, in spirit) and
   // doubles before a chunk whose new states could take it past 0.75 load.
-  unsigned long long slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 24, m->hint_slots);
+  unsigned long long slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 26, m->hint_slots);
   if (recovering) slots = rc.slots;
   if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
@@ -1294,6 +1294,12 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       fprintf(stderr, "[rmc] frontier moved to host memory at depth %u (%.1f GiB of pinned pages, limit %.1f GiB)\n",
               depth, pool.allocated / 1073741824.0, pool.limit / 1073741824.0);
   };
+  // Growth threshold: 0.5 load while the set is at most 32 GiB (short probe
+  // runs: at 0.75 a miss reads ~8 slots, 2-3 dependent 64 B groups), 0.75
+  // beyond (HBM capacity matters more than probe length there).
+  auto over_load = [&](unsigned long long need) {
+    return slots * (unsigned long long)ew * 8 <= (32ULL << 30) ? need * 2 > slots : need * 4 > slots * 3;
+  };
   auto t_grow = [&](unsigned long long nslots) {  // rehash into nslots (entries and values kept)
     auto tr0 = now();
     HIPCHK(hipStreamSynchronize(stream));
@@ -1326,10 +1332,11 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     return true;
   };
   auto t_fit = [&](unsigned long long need) {
-    if (need * 4 <= slots * 3) return;
+    if (!over_load(need)) return;
     if (!full_ok) {
       unsigned long long nslots = slots;
-      while (need * 2 > nslots) nslots <<= 1;  // to <= 0.5 after growing
+      // to <= 0.25 after growing while small (threshold 0.5), else to <= 0.5
+      while (need * 2 > nslots || (nslots * (unsigned long long)ew * 8 <= (32ULL << 30) && need * 4 > nslots)) nslots <<= 1;
       if (t_grow(nslots)) return;
       if (!hf && hf_opt == 0) {  // the device frontiers give their HBM to the set
         enter_hf();
@@ -1436,7 +1443,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       if (!opt->grow_on_overflow) {  // room for this chunk's new states (at the highest rate seen)
         const double r = std::max(rate, c0 ? (double)next_n / (double)c0 : 0.0);
         const unsigned long long need = distinct + next_n + (unsigned long long)((double)n * r * 1.25) + 1024;
-        if (need * 4 > slots * 3) {
+        if (over_load(need)) {
           if (mat_pending) {  // the previous chunk may have ended the search: no growth for nothing
             HIPCHK(hipStreamSynchronize(stream));
             if (finish_mat()) break;
