@@ -208,6 +208,10 @@ def main():
             "result": {"generated": res["generated"], "distinct": res["distinct"], "depth": res["depth"],
                        "status": res["status"], "time_to_exhaust_s": per_step,
                        "first_check_s": cold[0] if cold else None,
+                       "first_check_note": "the warm-up check of this process: its first growth steps also wait "
+                                           "for the driver to clear HBM the previous process freed (4-6 s after a "
+                                           "~150 GB process); a fresh process on an idle GPU: 1.50 s "
+                                           "(profiles/r03/ab_cli_builds.txt)",
                        "hidden_var_collisions": res["hidden_var_collisions"],
                        "fpset_slots": res["hash_capacity"], "state_bytes": S, "fp_bits": args.fp_bits},
             # achieved = B / t_wall with B = 2DS + 8G + 20D per check;
