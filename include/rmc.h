@@ -64,8 +64,8 @@ typedef struct {
   const char* recover_dir;
   /* BFS levels in pinned host memory (SURVEY.md §7 hard part 5): the current and next level's packed states
    * live in host RAM and stream through HBM in chunk-sized windows, so the fingerprint set may take the
-   * whole device.  0 = auto (when a level would not fit beside the set in HBM), 1 = always, -1 = never
-   * (rmc_check only). */
+   * whole device.  0 = auto (at a level boundary when the next level is projected past a quarter of HBM, or
+   * when HBM runs out), 1 = always, -1 = never (rmc_check only; host memory capped by RMC_HOST_FRONTIER_GIB). */
   int host_frontier;
 } rmc_options;
 

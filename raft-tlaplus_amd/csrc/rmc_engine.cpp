@@ -1274,6 +1274,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   auto enter_hf = [&]() {
     auto th0 = std::chrono::steady_clock::now();
     HIPCHK(hipStreamSynchronize(stream));
+    try {  // while the device frontiers still hold their HBM (see reserve_windows)
+      reserve_windows();
+    } catch (OutOfDeviceMemory&) {
+    }
     hs.init(stream);
     hcur.init(page_rows, row_bytes);
     hnxt.init(page_rows, row_bytes);
@@ -1380,9 +1384,24 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   };
   try {
   if (hf_opt == 1 && !hf) enter_hf();
+  size_t hbm_total = 0;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceTotalMem(&hbm_total, dev);
+  }
   while (status == 0 && cur_n > 0) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     if (opt->time_limit > 0 && secs(t0, now()) >= opt->time_limit) { status = 4; message = "time limit"; break; }
+    // auto mode: a next level projected past a quarter of HBM moves the
+    // levels to the host at this boundary, while the device frontiers are
+    // still small -- their HBM is not reusable once released (§3), so a
+    // later switch strands more of it
+    if (!hf && hf_opt == 0 && hbm_total &&
+        (double)cur_n * std::max(rate, 1.0) * 1.25 * (double)(W * 4) > 0.25 * (double)hbm_total) {
+      lvl_c0 = 0;
+      lvl_next_n = 0;
+      enter_hf();
+    }
     unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     if (cur_base + cur_n + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
