@@ -52,7 +52,7 @@ def test_first_wins_across_chunks(name, chunk):
 
 
 @pytest.mark.parametrize("name", sorted(ORDER))
-@pytest.mark.parametrize("shards,chunk", [(2, 0), (3, 5)])
+@pytest.mark.parametrize("shards,chunk", [(2, 0), (3, 13)])
 def test_first_wins_across_shards(name, shards, chunk):
     g = ORDER[name]
     m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
