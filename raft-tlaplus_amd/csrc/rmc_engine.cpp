@@ -1225,6 +1225,12 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   }
   pool.page_bytes = page_rows * row_bytes;
   pool.limit = host_frontier_limit();
+  // pinning threads and the pages they keep ready (RMC_HF_PIN_THREADS,
+  // RMC_HF_PIN_AHEAD; 0 threads = pin on demand in the BFS thread)
+  int hf_pin_threads = 4;
+  size_t hf_pin_ahead = 32;
+  if (const char* e = getenv("RMC_HF_PIN_THREADS")) hf_pin_threads = atoi(e);
+  if (const char* e = getenv("RMC_HF_PIN_AHEAD")) hf_pin_ahead = (size_t)atoll(e);
   HostLevel hcur, hnxt;
   hcur.init(page_rows, row_bytes);
   hnxt.init(page_rows, row_bytes);
@@ -1279,6 +1285,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     } catch (OutOfDeviceMemory&) {
     }
     hs.init(stream);
+    pool.start_fillers(hf_pin_ahead, hf_pin_threads);
     hcur.init(page_rows, row_bytes);
     hnxt.init(page_rows, row_bytes);
     hcur.reserve(cur_n, pool);
@@ -1897,11 +1904,14 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   }
   if (hf) {
     HIPCHK(hipStreamSynchronize(hs.cs));
+    const size_t hf_peak = pool.allocated;
     hcur.clear(pool);
     hnxt.clear(pool);
     pool.release();
     for (DevBuf* b : {&A.hwin_in[0], &A.hwin_in[1], &A.hwin_out[0], &A.hwin_out[1]}) b->release();
-    if (opt->verbose) fprintf(stderr, "[rmc] host frontier: %.3fs moving levels to host memory\n", hf_copy_s);
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] host frontier: %.3fs moving levels to host memory; %.3fs pinning pages (%zu MiB peak)\n", hf_copy_s,
+              pool.alloc_s, hf_peak >> 20);
   }
   HIPCHK(hipStreamDestroy(stream));
   if (!opt->hash_slots) m->hint_slots = slots;

@@ -7,6 +7,11 @@
 #include <utility>
 #include <vector>
 #include <algorithm>
+#include <sys/mman.h>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include "../../include/rmc.h"
 #include "rmc_engine.h"
 
@@ -208,27 +213,117 @@ struct OutOfHostMemory : std::runtime_error {
 // read, so the host peak is about one level plus the growth of the next.
 struct HostPagePool {
   size_t page_bytes = 0;
-  size_t allocated = 0, limit = 0;  // bytes of pinned pages held / allowed
+  size_t allocated = 0, limit = 0;  // bytes of pinned pages held / allowed (including pages being pinned)
+  double alloc_s = 0;               // time the BFS thread spent pinning or waiting for a pinned page
   std::vector<void*> free_pages;
+  // Pinning threads: keep up to `ahead` free pages pinned so the BFS thread
+  // does not wait for pinning while a level grows (hipHostMalloc pages at
+  // 5.5 GB/s dominated host-frontier levels:
+  // profiles/r03/ladder_Raft_n3v2e3_auto_pinning.txt).
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::thread> fillers;
+  size_t ahead = 0, inflight = 0;
+  bool stop = false, failed = false;
+  // One page, outside the lock; nullptr when the host refuses.  Pages are
+  // populated by the calling thread (mmap MAP_POPULATE: the kernel zeroes them
+  // in parallel across threads) and then registered with HIP, which is cheap
+  // on populated memory: 15 GB/s with 4 threads against 5.8 GB/s for
+  // hipHostMalloc, which serialises in the driver (profiles/r03/pin_probe.txt).
+  void* pin() {
+    void* p = mmap(nullptr, page_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
+    if (p == MAP_FAILED) return nullptr;
+    if (hipHostRegister(p, page_bytes, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      munmap(p, page_bytes);
+      return nullptr;
+    }
+    return p;
+  }
+  void unpin(void* p) {
+    (void)hipHostUnregister(p);
+    munmap(p, page_bytes);
+  }
+  void start_fillers(size_t pages, int threads) {
+    if (!fillers.empty() || !pages || threads < 1) return;
+    ahead = pages;
+    stop = failed = false;
+    for (int t = 0; t < threads; ++t) fillers.emplace_back([this] {
+      std::unique_lock<std::mutex> lk(mu);
+      for (;;) {
+        cv.wait(lk, [this] { return stop || (!failed && free_pages.size() + inflight < ahead && allocated + page_bytes <= limit); });
+        if (stop) return;
+        allocated += page_bytes;  // reserved before pinning so get() cannot overshoot the limit
+        ++inflight;
+        lk.unlock();
+        void* p = pin();
+        lk.lock();
+        --inflight;
+        if (!p) {
+          allocated -= page_bytes;
+          failed = true;
+        } else {
+          free_pages.push_back(p);
+        }
+        cv.notify_all();
+      }
+    });
+  }
+  void stop_fillers() {
+    if (fillers.empty()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : fillers) t.join();
+    fillers.clear();
+  }
   void* get() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (free_pages.empty() && !fillers.empty() && !failed) {
+      // the pinning thread is behind: wait for its page rather than pin a second one here
+      const auto t0 = std::chrono::steady_clock::now();
+      cv.notify_all();
+      cv.wait(lk, [this] { return !free_pages.empty() || failed || (!inflight && allocated + page_bytes > limit); });
+      alloc_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
     if (!free_pages.empty()) {
       void* p = free_pages.back();
       free_pages.pop_back();
+      cv.notify_all();
       return p;
     }
     if (allocated + page_bytes > limit)
       throw OutOfHostMemory("host frontier pages exhausted (" + std::to_string(limit >> 30) + " GiB limit)");
-    void* p = nullptr;
-    if (hipHostMalloc(&p, page_bytes, hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
+    allocated += page_bytes;
+    lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
+    void* p = pin();
+    lk.lock();
+    alloc_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!p) {
+      allocated -= page_bytes;
       throw OutOfHostMemory("pinned host memory exhausted (" + std::to_string(allocated >> 30) + " GiB held)");
     }
-    allocated += page_bytes;
     return p;
   }
-  void put(void* p) { if (p) free_pages.push_back(p); }
+  void put(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu);
+    free_pages.push_back(p);
+  }
   void release() {
-    for (void* p : free_pages) (void)hipHostFree(p);
+    stop_fillers();
+    const size_t nt = std::min<size_t>(4, free_pages.size() / 8);  // unmapping frees in parallel
+    if (nt > 1) {
+      std::vector<std::thread> th;
+      for (size_t t = 0; t < nt; ++t)
+        th.emplace_back([this, t, nt] { for (size_t i = t; i < free_pages.size(); i += nt) unpin(free_pages[i]); });
+      for (auto& x : th) x.join();
+    } else {
+      for (void* p : free_pages) unpin(p);
+    }
     allocated -= free_pages.size() * page_bytes;
     free_pages.clear();
   }
