@@ -33,8 +33,9 @@ WORKLOADS = {
     "raft_cfg": ("Raft", "configs/Raft.cfg", "1",
                  "standard-raft Raft.cfg: 3 servers, Value={v1}, MaxElections=2, MaxRestarts=0"),
     "raft_n3v2e2": ("Raft", "configs/Raft_n3v2e2.cfg",
-                    "2 ladder, rung below config 2 (config 2 itself, MaxElections=3, stops at HBM capacity on one "
-                    "GPU: profiles/r02/ladder_Raft_n3v2e3*.txt)",
+                    "2 ladder, rung below config 2 (config 2 itself, MaxElections=3, does not exhaust on one GPU: "
+                    "levels paged to host memory, it stops at depth 29, 2.03e9 distinct, on the 245 GiB host-page "
+                    "limit: profiles/r03/ladder_Raft_n3v2e3_pin4.txt)",
                     "standard-raft: 3 servers, Value={v1,v2} (logs <= 2 entries), MaxElections=2 (terms <= 3), "
                     "MaxRestarts=0; the largest config-2 rung that exhausts on one MI355X"),
     "raft_n3v1e3": ("Raft", "configs/Raft_n3v1e3.cfg", "2 ladder (Value={v1})",
