@@ -980,13 +980,16 @@ size_t host_frontier_limit() {
   return std::min<size_t>(avail / 5 * 4, 200ULL << 30);
 }
 
-// The copy stream and events of the host frontier, created on first use.
+// The copy streams and events of the host frontier, created on first use:
+// parents in (H2D) on `cs`, new rows out (D2H) on `co`, so the two directions
+// of the PCIe link run at once instead of queueing behind each other.
 struct HostFrontierStreams {
-  hipStream_t cs = nullptr;
+  hipStream_t cs = nullptr, co = nullptr;
   hipEvent_t in[2], mat[2], out[2];
   void init(hipStream_t compute) {
     if (cs) return;
     HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&co, hipStreamNonBlocking));
     for (int k = 0; k < 2; k++) {
       HIPCHK(hipEventCreateWithFlags(&in[k], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&mat[k], hipEventDisableTiming));
@@ -996,14 +999,21 @@ struct HostFrontierStreams {
       HIPCHK(hipEventRecord(out[k], compute));
     }
   }
+  void sync() {
+    if (!cs) return;
+    HIPCHK(hipStreamSynchronize(cs));
+    HIPCHK(hipStreamSynchronize(co));
+  }
   ~HostFrontierStreams() {
     if (!cs) return;
     (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(co);
     for (int k = 0; k < 2; k++) {
       (void)hipEventDestroy(in[k]);
       (void)hipEventDestroy(mat[k]);
       (void)hipEventDestroy(out[k]);
     }
+    (void)hipStreamDestroy(co);
     (void)hipStreamDestroy(cs);
   }
 };
@@ -1289,10 +1299,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     hcur.init(page_rows, row_bytes);
     hnxt.init(page_rows, row_bytes);
     hcur.reserve(cur_n, pool);
-    hcur.d2h_append(cur, cur_n, hs.cs);
+    hcur.d2h_append(cur, cur_n, hs.co);
     hnxt.reserve(lvl_next_n, pool);
-    hnxt.d2h_append(nxt, lvl_next_n, hs.cs);
-    HIPCHK(hipStreamSynchronize(hs.cs));
+    hnxt.d2h_append(nxt, lvl_next_n, hs.co);
+    HIPCHK(hipStreamSynchronize(hs.co));
     if (lvl_c0 > chunk) hcur.recycle_below(lvl_c0 - chunk, pool);
     fa.release();
     fb.release();
@@ -1641,9 +1651,9 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       if (hf) {  // the new rows go to host pages (copy stream), after this k_materialize
         HIPCHK(hipEventRecord(hs.mat[hs_k], stream));
         hnxt.reserve(W_chunk, pool);
-        HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k], 0));
-        hnxt.d2h_append(A.hwin_out[hs_k].p, W_chunk, hs.cs);
-        HIPCHK(hipEventRecord(hs.out[hs_k], hs.cs));
+        HIPCHK(hipStreamWaitEvent(hs.co, hs.mat[hs_k], 0));
+        hnxt.d2h_append(A.hwin_out[hs_k].p, W_chunk, hs.co);
+        HIPCHK(hipEventRecord(hs.out[hs_k], hs.co));
         // rows below the previous chunk are consumed (the last two chunks stay
         // for the recount at a violation)
         hcur.recycle_below(prev_c0, pool);
@@ -1663,7 +1673,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       HIPCHK(hipStreamSynchronize(stream));
       finish_mat();
     }
-    if (hf) HIPCHK(hipStreamSynchronize(hs.cs));  // every new row is in its host page
+    if (hf) hs.sync();  // every new row is in its host page
     const unsigned long long gen_before = generated, dist_before = distinct;
     generated += gen_lvl;
     distinct += next_n;
@@ -1903,7 +1913,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
             __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);
   }
   if (hf) {
-    HIPCHK(hipStreamSynchronize(hs.cs));
+    hs.sync();
     const size_t hf_peak = pool.allocated;
     hcur.clear(pool);
     hnxt.clear(pool);
