@@ -186,6 +186,19 @@ def main():
         ach = bytes_check / launches / (avg * 1e-3) if avg > 0 else 0.0
         kern[name] = {"bytes_per_launch": bytes_check / launches, "avg_launch_ms": avg, "achieved": ach / 1e9,
                       "frac": ach / HBM_PEAK, "traffic": kpmc.get(name)}
+    # The peak is HBM's (no MFMA: integer work), but while the check runs far
+    # below it the kernels are bound by memory LATENCY -- k_expand's waves wait
+    # on dependent round trips (row staging, the tile's reservation atomic, the
+    # probe, the CAS) most of their cycles (PMC SQ_WAIT_ANY / SQ_WAVE_CYCLES).
+    frac_check = B / per_step / HBM_PEAK
+    wait_share = None
+    if pmc:
+        for k, v in pmc.get("kernels", {}).items():
+            if k.startswith("rmc::k_expand") and v.get("SQ_WAVE_CYCLES_per_dispatch"):
+                wait_share = v["SQ_WAIT_ANY_per_dispatch"] / v["SQ_WAVE_CYCLES_per_dispatch"]
+    bound = "latency" if frac_check < 0.2 else "hbm"
+    bound_detail = ("k_expand waves wait %.0f%% of their cycles (PMC SQ_WAIT_ANY / SQ_WAVE_CYCLES, %s)"
+                    % (100 * wait_share, pmc_src)) if wait_share is not None else None
     if rank == 0:
         line = {
             "metric": "distinct states/sec + time-to-exhaust, " +
@@ -218,7 +231,8 @@ def main():
             # achieved = B / t_wall with B = 2DS + 8G + 20D per check;
             # the dominant kernels' own shares per launch under "kernels"
             # (HIP-event launch times inside librmc)
-            "roofline": {"bound": "hbm", "achieved": B / per_step / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "roofline": {"bound": bound, "bound_detail": bound_detail, "peak_of": "hbm",
+                         "achieved": B / per_step / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": B / per_step / HBM_PEAK,
                          "traffic": sum(kpmc.values()) * launches if len(kpmc) == 3 else None,
                          "traffic_unit": "HBM bytes per check (PMC: k_expand + k_mark + k_materialize)",

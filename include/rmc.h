@@ -74,11 +74,12 @@ typedef struct {
   uint32_t depth;
   int status; /* 0 ok, 1 invariant violated, 2 evaluation error, 3 capacity overflow, 4 stopped (max_depth, time_limit) */
   char violated[64];
-  char message[256];
   uint64_t hidden_var_collisions; /* same-level duplicates whose VIEW-hidden variables (acked, electionCtr,
                                      restartCtr; Pull: the counters) differ from the first-in-TLC-order winner's
                                      (SURVEY.md §7 hard part 1); equal to the oracle's hidden_same_level */
   double seconds;
+  /* everything below extends SURVEY.md §8b's rmc_result, whose fields above keep its order and offsets */
+  char message[256];    /* evaluation-error / capacity text (TLC's error message), "" otherwise */
   /* measurement (filled by rmc_check) */
   double expand_ms, mark_ms, materialize_ms; /* summed device time per kernel family */
   uint64_t expand_launches;

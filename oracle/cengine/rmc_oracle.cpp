@@ -34,6 +34,9 @@
 #include <vector>
 #include <thread>
 #include <atomic>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 namespace {
 
@@ -993,62 +996,178 @@ Key128 hash_ser(const Ser& o) {
   return {h1, h2 | 1};  // b != 0 marks an occupied slot
 }
 
-// open-addressing set of 128-bit keys, value = (level, hidden)
-struct Slot { uint64_t a, b; uint32_t level; uint32_t hidden; };
-struct FPSet {
+// Fingerprint set: T shards (one per thread, chosen by the key's high bits),
+// open addressing with linear probing over a table of any size (home slot =
+// mulhi(a, size)).  A slot holds 96 bits of the 128-bit canonical-form hash
+// (a + the high half of b; collision odds for 2e9 states ~ n^2 / 2^97 ~ 3e-11)
+// plus the level that inserted it and the hidden (VIEW-dropped) variables: 16 B,
+// so the 1.9e9-state rungs fit this container's memory.  level 0 = empty.
+struct Slot { uint64_t a; uint32_t b; uint16_t level; uint16_t hidden; };
+struct FPShard {
   std::vector<Slot> t;
-  uint64_t mask = 0, count = 0;
-  FPSet() { t.resize(1 << 20); mask = t.size() - 1; memset(t.data(), 0, t.size() * sizeof(Slot)); }
+  uint64_t count = 0;
+  double max_load = 0.5;
+  void init(uint64_t slots, double ml) {
+    max_load = ml;
+    t.assign(std::max<uint64_t>(slots, 1024), Slot{0, 0, 0, 0});
+  }
+  inline uint64_t home(uint64_t a, uint64_t n) const { return (uint64_t)(((unsigned __int128)a * n) >> 64); }
   void grow() {
     std::vector<Slot> old;
     old.swap(t);
-    t.assign(old.size() * 2, Slot{0, 0, 0, 0});
-    mask = t.size() - 1;
+    const uint64_t n = old.size() * 2;
+    t.assign(n, Slot{0, 0, 0, 0});
     for (auto& s : old)
-      if (s.b) {
-        uint64_t h = s.a & mask;
-        while (t[h].b) h = (h + 1) & mask;
+      if (s.level) {
+        uint64_t h = home(s.a, n);
+        while (t[h].level) h = (h + 1 == n) ? 0 : h + 1;
         t[h] = s;
       }
   }
   // returns nullptr if inserted, else the existing slot
-  Slot* insert(Key128 k, uint32_t level, uint32_t hidden) {
-    if ((count + 1) * 2 > t.size()) grow();
-    uint64_t h = k.a & mask;
-    while (t[h].b) {
-      if (t[h].a == k.a && t[h].b == k.b) return &t[h];
-      h = (h + 1) & mask;
+  Slot* insert(Key128 k, uint16_t level, uint16_t hidden) {
+    if ((double)(count + 1) > max_load * (double)t.size()) grow();
+    const uint64_t n = t.size();
+    const uint32_t b = (uint32_t)(k.b >> 32);
+    uint64_t h = home(k.a, n);
+    while (t[h].level) {
+      if (t[h].a == k.a && t[h].b == b) return &t[h];
+      h = (h + 1 == n) ? 0 : h + 1;
     }
-    t[h] = Slot{k.a, k.b, level, hidden};
+    t[h] = Slot{k.a, b, level, hidden};
     count++;
     return nullptr;
   }
 };
 
-uint32_t hidden_of(const State& s) {
-  uint32_t h = (uint32_t)s.electionCtr | ((uint32_t)s.restartCtr << 8);
+// electionCtr | restartCtr | acked[v]: the variables VIEW drops (Raft.tla:115-116;
+// PullRaft keeps acked in its view).  16 bits: E, R <= 15 and V <= 4 are checked.
+uint16_t hidden_of(const State& s) {
+  uint32_t h = (uint32_t)s.electionCtr | ((uint32_t)s.restartCtr << 4);
   if (C.spec != PULL)
-    for (int v = 0; v < C.V; v++) h |= (uint32_t)(s.acked[v] + 1) << (16 + 2 * v);
-  return h;
+    for (int v = 0; v < C.V; v++) h |= (uint32_t)(s.acked[v] + 1) << (8 + 2 * v);
+  return (uint16_t)h;
 }
 
-// compact storage of frontier states
-struct Arena {
-  std::vector<uint8_t> buf;
-  std::vector<uint64_t> off;
-  void push(const State& s) {
-    off.push_back(buf.size());
-    size_t n = FIXED_BYTES + (size_t)s.nmsg * sizeof(Msg);
-    size_t o = buf.size();
-    buf.resize(o + n);
-    memcpy(buf.data() + o, &s, n);
+// ------------------------------------------------------- compact frontier rows
+// A state is stored as its used fields only (N servers, V values, Len(log)
+// entries, |DOMAIN messages| records), each field one nibble when it lies in
+// [-1, 13] (value + 1), else an escape nibble 15 and the raw byte in two
+// nibbles; rows are prefixed with their u16 byte length.  Unused State bytes
+// decode to 0, as Init() leaves them; stale log entries past Len(log) are
+// dropped (nothing reads them: log_at bounds-checks).
+struct NibW {
+  uint8_t* p; size_t n = 0;  // n = nibbles written
+  inline void nib(unsigned v) { if (n & 1) p[n >> 1] |= (uint8_t)(v << 4); else p[n >> 1] = (uint8_t)v; n++; }
+  inline void put(int v) {
+    if (v >= -1 && v <= 13) nib((unsigned)(v + 1));
+    else { nib(15); nib((uint8_t)v & 15); nib((uint8_t)v >> 4); }
   }
-  void get(size_t k, State& s) const {
-    size_t n = (k + 1 < off.size() ? off[k + 1] : buf.size()) - off[k];
-    memcpy(&s, buf.data() + off[k], n);
+};
+struct NibR {
+  const uint8_t* p; size_t n = 0;
+  inline unsigned nib() { unsigned v = (p[n >> 1] >> ((n & 1) * 4)) & 15; n++; return v; }
+  inline int get() {
+    unsigned v = nib();
+    if (v != 15) return (int)v - 1;
+    unsigned lo = nib(), hi = nib();
+    return (int)(int8_t)(uint8_t)(lo | hi << 4);
   }
-  size_t size() const { return off.size(); }
-  void clear() { buf.clear(); off.clear(); }
+};
+constexpr size_t ROW_MAX = 2 + 3 * (FIXED_BYTES + MAXMSG * sizeof(Msg)) / 2 + 8;
+size_t encode_state(const State& s, uint8_t* out) {  // out: u16 length + nibbles
+  NibW w{out + 2};
+  const int N = C.N;
+  w.put(s.nmsg & 255); w.put(s.nmsg >> 8); w.put(s.electionCtr); w.put(s.restartCtr);
+  for (int v = 0; v < C.V; v++) w.put(s.acked[v]);
+  for (int i = 0; i < N; i++) {
+    w.put(s.term[i]); w.put(s.st[i]); w.put(s.voted[i]); w.put(s.voted2[i]); w.put(s.loglen[i]);
+    w.put(s.commit[i]); w.put(s.fsync[i]); w.put((int8_t)s.votes[i]); w.put((int8_t)s.pending[i]);
+    for (int x = 0; x < s.loglen[i]; x++) { w.put(s.log[i][x].term); w.put(s.log[i][x].value); }
+    for (int j = 0; j < N; j++) { w.put(s.next[i][j]); w.put(s.match[i][j]); }
+    if (C.spec == PULL2) for (int j = 0; j < N; j++) { w.put(s.vleI[i][j]); w.put(s.vleT[i][j]); }
+  }
+  for (int k = 0; k < s.nmsg; k++) {
+    const int8_t* b = (const int8_t*)&s.msgs[k];
+    for (size_t f = 0; f < REC_BYTES; f++) w.put(b[f]);
+    w.put((int8_t)s.msgs[k].count);
+  }
+  const size_t bytes = (w.n + 1) / 2;
+  const uint16_t len = (uint16_t)bytes;
+  memcpy(out, &len, 2);
+  return 2 + bytes;
+}
+void decode_state(const uint8_t* row, State& s) {
+  memset(&s, 0, FIXED_BYTES);
+  NibR r{row + 2};
+  const int N = C.N;
+  int lo = r.get() & 255;
+  s.nmsg = (int16_t)(lo | (r.get() << 8));
+  s.electionCtr = (int8_t)r.get(); s.restartCtr = (int8_t)r.get();
+  for (int v = 0; v < C.V; v++) s.acked[v] = (int8_t)r.get();
+  for (int i = 0; i < N; i++) {
+    s.term[i] = (int8_t)r.get(); s.st[i] = (int8_t)r.get(); s.voted[i] = (int8_t)r.get(); s.voted2[i] = (int8_t)r.get();
+    s.loglen[i] = (int8_t)r.get(); s.commit[i] = (int8_t)r.get(); s.fsync[i] = (int8_t)r.get();
+    s.votes[i] = (uint8_t)r.get(); s.pending[i] = (uint8_t)r.get();
+    for (int x = 0; x < s.loglen[i]; x++) { s.log[i][x].term = (int8_t)r.get(); s.log[i][x].value = (int8_t)r.get(); }
+    for (int j = 0; j < N; j++) { s.next[i][j] = (int8_t)r.get(); s.match[i][j] = (int8_t)r.get(); }
+    if (C.spec == PULL2) for (int j = 0; j < N; j++) { s.vleI[i][j] = (int8_t)r.get(); s.vleT[i][j] = (int8_t)r.get(); }
+    for (int j = N; j < MAXN; j++) s.vleI[i][j] = -1;  // Init's value for unused peers
+  }
+  for (int k = 0; k < s.nmsg; k++) {
+    int8_t* b = (int8_t*)&s.msgs[k];
+    for (size_t f = 0; f < REC_BYTES; f++) b[f] = (int8_t)r.get();
+    s.msgs[k].count = (uint8_t)r.get();
+  }
+}
+inline size_t row_len(const uint8_t* row) { uint16_t n; memcpy(&n, row, 2); return 2 + (size_t)n; }
+
+// A BFS level: rows appended in TLC order, either in memory or spilled to a
+// file (--spill-dir) and read back through a read-only mapping.
+struct Level {
+  std::vector<uint8_t> mem;
+  std::string path;
+  FILE* wf = nullptr;
+  const uint8_t* map = nullptr;
+  size_t bytes = 0, count = 0;
+  std::vector<uint8_t> wbuf;
+  void open(const std::string& p) { path = p; }
+  void clear() {
+    if (map) { munmap((void*)map, bytes); map = nullptr; }
+    if (wf) { fclose(wf); wf = nullptr; }
+    mem.clear();
+    mem.shrink_to_fit();
+    bytes = count = 0;
+    if (!path.empty()) {
+      wf = fopen(path.c_str(), "wb");
+      if (!wf) { perror(path.c_str()); exit(3); }
+      wbuf.resize(64 << 20);
+      setvbuf(wf, (char*)wbuf.data(), _IOFBF, wbuf.size());
+    }
+  }
+  void push(const uint8_t* row, size_t n) {
+    if (wf) { if (fwrite(row, 1, n, wf) != n) { perror("spill write"); exit(3); } }
+    else mem.insert(mem.end(), row, row + n);
+    bytes += n;
+    count++;
+  }
+  void finish() {  // writing done: map for reading
+    if (!wf) return;
+    if (fflush(wf) != 0) { perror("spill flush"); exit(3); }
+    fclose(wf);
+    wf = nullptr;
+    if (bytes == 0) return;
+    int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) { perror(path.c_str()); exit(3); }
+    void* m = mmap(nullptr, bytes, PROT_READ, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (m == MAP_FAILED) { perror("spill mmap"); exit(3); }
+    madvise(m, bytes, MADV_SEQUENTIAL);
+    map = (const uint8_t*)m;
+  }
+  const uint8_t* data() const { return map ? map : mem.data(); }
+  size_t size() const { return count; }
+  ~Level() { if (map) munmap((void*)map, bytes); if (wf) fclose(wf); if (!path.empty()) unlink(path.c_str()); }
 };
 
 // ---------------------------------------------------------------- BFS driver
@@ -1063,92 +1182,150 @@ struct Stats {
   double seconds = 0;
 };
 
-struct SuccCollect : Emitter {
-  std::vector<State>* out;
-  std::vector<int>* acts;
-  void emit(const State& t, int a) override { out->push_back(t); acts->push_back(a); }
-};
-
 std::string state_json(const State& s);
 
 struct Checker {
   Stats st;
-  FPSet fps;
+  std::vector<FPShard> fps;
   // trace records (parent global index, ordinal within parent's successors)
   std::vector<uint64_t> parent;
   std::vector<uint16_t> ordinal;
   std::vector<uint8_t> actid;
+  bool trace = true;
   uint64_t max_distinct = 0;
+  uint64_t fp_slots = 0;  // preallocated total slots (0 = start small, grow at 0.5 load)
   double max_seconds = 0;
   int threads = 1;
   bool reverse_order = false;
+  bool progress = false;
+  std::string spill_dir;
   FILE* fpdump = nullptr;
   int64_t bad_index = -1;
 
   void run();
 };
 
-// per-thread expansion buffers for a chunk of parents
+// a successor candidate of one chunk (expanded by the worker that owns its parent)
+enum CandRes : uint8_t { R_NEW = 0, R_DUP = 1, R_DUP_HID_SAME = 2, R_DUP_HID_CROSS = 3 };
 struct Cand {
   Key128 key;
-  uint32_t hidden;
   uint32_t parent_local;
+  uint32_t row_off;      // into the worker's keep buffer
   uint16_t ordinal;
+  uint16_t hidden;
   uint8_t act;
+  uint8_t res;           // CandRes, set by the insert pass
+  int16_t inv;           // -1 ok, k = index into inv_names, -2 evaluation error (see inv_err)
 };
 
-void expand_range(const Arena& cur, size_t lo, size_t hi, std::vector<Cand>& out, Arena& keep,
-                  std::string& err, size_t& err_parent, int& maxmsg) {
-  std::vector<State> succ;
-  std::vector<int> acts;
-  succ.reserve(128);
-  SuccCollect em;
-  em.out = &succ;
-  em.acts = &acts;
+struct Worker {
+  std::vector<Cand> cands;
+  std::vector<uint8_t> keep;
+  std::vector<std::pair<size_t, std::string>> inv_err;  // candidate index -> evaluation error
+  std::string err;
+  size_t err_parent = 0;
+  int maxmsg = 0;
+};
+
+std::vector<std::string> inv_names;  // check_invariants' results, interned
+int16_t intern_inv(const char* n) {
+  for (size_t k = 0; k < inv_names.size(); k++) if (inv_names[k] == n) return (int16_t)k;
+  inv_names.push_back(n);
+  return (int16_t)(inv_names.size() - 1);
+}
+
+struct CandEmit : Emitter {
+  Worker* w;
+  uint32_t parent_local;
+  uint16_t q = 0;
+  uint8_t row[ROW_MAX];
+  void emit(const State& t, int a) override {
+    Ser o;
+    canonical(t, o);
+    Cand c;
+    c.key = hash_ser(o);
+    c.hidden = hidden_of(t);
+    c.parent_local = parent_local;
+    c.ordinal = q++;
+    c.act = (uint8_t)a;
+    c.res = R_NEW;
+    c.inv = -1;
+    try {
+      if (const char* bad = check_invariants(t)) c.inv = intern_inv(bad);
+    } catch (EvalError& e) {
+      c.inv = -2;
+      w->inv_err.push_back({w->cands.size(), std::string("invariant: ") + e.what()});
+    }
+    size_t n = encode_state(t, row);
+    c.row_off = (uint32_t)w->keep.size();
+    w->keep.insert(w->keep.end(), row, row + n);
+    w->cands.push_back(c);
+  }
+};
+
+void expand_range(const uint8_t* const* rows, size_t lo, size_t hi, Worker& W) {
+  CandEmit em;
+  em.w = &W;
   State s;
   for (size_t k = lo; k < hi; k++) {
-    cur.get(k, s);
-    maxmsg = std::max(maxmsg, (int)s.nmsg);
-    succ.clear();
-    acts.clear();
+    decode_state(rows[k], s);
+    W.maxmsg = std::max(W.maxmsg, (int)s.nmsg);
+    em.parent_local = (uint32_t)k;
+    em.q = 0;
+    const size_t before = W.cands.size(), kb = W.keep.size(), eb = W.inv_err.size();
     try {
       Next(s, em);
     } catch (EvalError& e) {
-      err = e.what();
-      err_parent = k;
+      // the parent's successors are not generated: TLC stops at the error
+      W.cands.resize(before);
+      W.keep.resize(kb);
+      W.inv_err.resize(eb);
+      W.err = e.what();
+      W.err_parent = k;
       return;
     }
-    for (size_t q = 0; q < succ.size(); q++) {
-      Ser o;
-      canonical(succ[q], o);
-      Cand c;
-      c.key = hash_ser(o);
-      c.hidden = hidden_of(succ[q]);
-      c.parent_local = (uint32_t)k;
-      c.ordinal = (uint16_t)q;
-      c.act = (uint8_t)acts[q];
-      out.push_back(c);
-      keep.push(succ[q]);
-    }
   }
+}
+
+template <class F> void parallel(int T, F f) {
+  if (T == 1) { f(0); return; }
+  std::vector<std::thread> th;
+  for (int w = 0; w < T; w++) th.emplace_back([&, w]() { f(w); });
+  for (auto& x : th) x.join();
 }
 
 void Checker::run() {
   auto t0 = std::chrono::steady_clock::now();
   auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
-  Arena cur, nxt;
+  const int T = std::max(1, threads);
+  fps.resize(T);
+  for (auto& f : fps) f.init(fp_slots ? (fp_slots + T - 1) / T : (1u << 20), fp_slots ? 0.92 : 0.5);
+  auto shard_of = [T](const Key128& k) { return (int)(((k.a >> 32) * (uint64_t)T) >> 32); };
+  Level lv[2];
+  if (!spill_dir.empty()) {
+    lv[0].open(spill_dir + "/level_a.bin");
+    lv[1].open(spill_dir + "/level_b.bin");
+  }
+  Level* cur = &lv[0];
+  Level* nxt = &lv[1];
+  cur->clear();
   State init = Init();
   st.generated = 1;
+  st.distinct = 1;
   {
     Ser o;
     canonical(init, o);
-    fps.insert(hash_ser(o), 1, hidden_of(init));
-    if (fpdump) { Key128 k = hash_ser(o); fwrite(&k, sizeof k, 1, fpdump); }
+    Key128 k = hash_ser(o);
+    fps[shard_of(k)].insert(k, 1, hidden_of(init));
+    if (fpdump) fwrite(&k, sizeof k, 1, fpdump);
   }
-  parent.push_back(UINT64_MAX);
-  ordinal.push_back(0);
-  actid.push_back(255);
-  cur.push(init);
+  if (trace) { parent.push_back(UINT64_MAX); ordinal.push_back(0); actid.push_back(255); }
+  {
+    uint8_t row[ROW_MAX];
+    size_t n = encode_state(init, row);
+    cur->push(row, n);
+    cur->finish();
+  }
   st.levels.push_back({1, 1});
   st.depth = 1;
   try {
@@ -1156,88 +1333,109 @@ void Checker::run() {
   } catch (EvalError& e) { st.status = "error"; st.error = e.what(); bad_index = 0; }
   uint64_t base = 0;  // global index of cur[0]
   uint32_t level = 1;
-  const int T = std::max(1, threads);
   const size_t CHUNK = 8192 * (size_t)T;
-  std::vector<std::vector<Cand>> cands(T);
-  std::vector<Arena> keeps(T);
-  while (st.status == "ok" && cur.size() > 0) {
-    size_t F = cur.size();
-    nxt.clear();
+  std::vector<Worker> W(T);
+  std::vector<const uint8_t*> rows(CHUNK);
+  double t_exp = 0, t_ins = 0, t_seq = 0;
+  while (st.status == "ok" && cur->size() > 0) {
+    const size_t F = cur->size();
+    nxt->clear();
     uint64_t gen_lvl = 0;
     bool stop = false;
+    const uint8_t* rp = cur->data();
     for (size_t c0 = 0; c0 < F && !stop; c0 += CHUNK) {
-      size_t c1 = std::min(F, c0 + CHUNK);
-      std::vector<std::string> errs(T);
-      std::vector<size_t> errp(T, 0);
-      std::vector<int> mm(T, 0);
-      std::vector<std::thread> th;
-      for (int w = 0; w < T; w++) {
-        size_t lo = c0 + (c1 - c0) * w / T, hi = c0 + (c1 - c0) * (w + 1) / T;
-        cands[w].clear();
-        keeps[w].clear();
-        if (T == 1) expand_range(cur, lo, hi, cands[w], keeps[w], errs[w], errp[w], mm[w]);
-        else th.emplace_back([&, w, lo, hi]() { expand_range(cur, lo, hi, cands[w], keeps[w], errs[w], errp[w], mm[w]); });
-      }
-      for (auto& x : th) x.join();
-      for (int w = 0; w < T; w++) st.max_msgs = std::max(st.max_msgs, mm[w]);
-      // sequential first-wins insertion in (parent, ordinal) order
+      const size_t c1 = std::min(F, c0 + CHUNK);
+      for (size_t k = c0; k < c1; k++) { rows[k - c0] = rp; rp += row_len(rp); }
+      // 1. expand (parallel over parents): successors, canonical keys, invariants
+      auto ta = std::chrono::steady_clock::now();
+      parallel(T, [&](int w) {
+        const size_t n = c1 - c0, lo = n * w / T, hi = n * (w + 1) / T;
+        Worker& X = W[w];
+        X.cands.clear(); X.keep.clear(); X.inv_err.clear(); X.err.clear();
+        expand_range(rows.data(), lo, hi, X);
+        for (auto& c : X.cands) c.parent_local += (uint32_t)c0;
+        if (!X.err.empty()) X.err_parent += c0;
+      });
+      auto tb = std::chrono::steady_clock::now();
+      // 2. insert (parallel over fingerprint shards): each shard sees its keys in
+      //    (parent, ordinal) order, so the first successor in TLC order wins
+      //    (--reverse-order probe: the last one)
+      parallel(T, [&](int s) {
+        for (int w0 = 0; w0 < T; w0++) {
+          const int w = reverse_order ? T - 1 - w0 : w0;
+          auto& cs = W[w].cands;
+          for (size_t q0 = 0; q0 < cs.size(); q0++) {
+            Cand& c = cs[reverse_order ? cs.size() - 1 - q0 : q0];
+            if (shard_of(c.key) != s) continue;
+            Slot* old = fps[s].insert(c.key, (uint16_t)(level + 1), c.hidden);
+            if (!old) c.res = R_NEW;
+            else if (old->hidden == c.hidden) c.res = R_DUP;
+            else c.res = old->level == level + 1 ? R_DUP_HID_SAME : R_DUP_HID_CROSS;
+          }
+        }
+      });
+      auto tc = std::chrono::steady_clock::now();
+      // 3. sequential pass in TLC order: counts, next level, trace, first violation
       for (int w0 = 0; w0 < T && !stop; w0++) {
-        // --reverse-order (probe only): the LAST successor in TLC order wins
-        // within a chunk -- a fixture whose counts change under it is one where
-        // TLC's first-wins rule matters
         const int w = reverse_order ? T - 1 - w0 : w0;
-        for (size_t q0 = 0; q0 < cands[w].size() && !stop; q0++) {
-          const size_t q = reverse_order ? cands[w].size() - 1 - q0 : q0;
-          const Cand& c = cands[w][q];
-          if (!errs[w].empty() && c.parent_local >= errp[w]) break;
+        Worker& X = W[w];
+        st.max_msgs = std::max(st.max_msgs, X.maxmsg);
+        size_t ie = 0;
+        for (size_t q0 = 0; q0 < X.cands.size() && !stop; q0++) {
+          const size_t q = reverse_order ? X.cands.size() - 1 - q0 : q0;
+          const Cand& c = X.cands[q];
           gen_lvl++;
           st.generated++;
           st.act[c.act]++;
-          Slot* old = fps.insert(c.key, level + 1, c.hidden);
-          if (old) {
-            if (old->hidden != c.hidden) {
-              if (old->level == level + 1) st.hidden_same++;
-              else st.hidden_cross++;
-            }
+          if (c.res != R_NEW) {
+            if (c.res == R_DUP_HID_SAME) st.hidden_same++;
+            else if (c.res == R_DUP_HID_CROSS) st.hidden_cross++;
             continue;
           }
+          st.distinct++;
           if (fpdump) fwrite(&c.key, sizeof c.key, 1, fpdump);
-          State t;
-          keeps[w].get(q, t);
-          nxt.push(t);
-          parent.push_back(base + c.parent_local);
-          ordinal.push_back(c.ordinal);
-          actid.push_back(c.act);
-          try {
-            if (const char* bad = check_invariants(t)) {
-              st.status = "violation"; st.violated = bad; bad_index = (int64_t)parent.size() - 1; stop = true;
-            }
-          } catch (EvalError& e) {
-            st.status = "error"; st.error = std::string("invariant: ") + e.what();
-            bad_index = (int64_t)parent.size() - 1; stop = true;
+          const uint8_t* row = X.keep.data() + c.row_off;
+          nxt->push(row, row_len(row));
+          if (trace) { parent.push_back(base + c.parent_local); ordinal.push_back(c.ordinal); actid.push_back(c.act); }
+          const int64_t idx = (int64_t)(st.distinct - 1);
+          if (c.inv >= 0) {
+            st.status = "violation"; st.violated = inv_names[c.inv]; bad_index = idx; stop = true;
+          } else if (c.inv == -2) {
+            while (ie < X.inv_err.size() && X.inv_err[ie].first != q) ie++;
+            st.status = "error";
+            st.error = ie < X.inv_err.size() ? X.inv_err[ie].second : "invariant: evaluation error";
+            bad_index = idx; stop = true;
           }
         }
-        if (!stop && !errs[w].empty()) {
+        if (!stop && !X.err.empty()) {
           st.status = "error";
-          st.error = errs[w];
-          bad_index = (int64_t)(base + errp[w]);
+          st.error = X.err;
+          bad_index = (int64_t)(base + X.err_parent);
           stop = true;
         }
       }
+      auto td = std::chrono::steady_clock::now();
+      t_exp += std::chrono::duration<double>(tb - ta).count();
+      t_ins += std::chrono::duration<double>(tc - tb).count();
+      t_seq += std::chrono::duration<double>(td - tc).count();
     }
-    if (nxt.size() > 0 || gen_lvl > 0) st.levels.push_back({gen_lvl, nxt.size()});
-    if (nxt.size() > 0) st.depth++;
+    nxt->finish();
+    if (nxt->size() > 0 || gen_lvl > 0) st.levels.push_back({gen_lvl, nxt->size()});
+    if (nxt->size() > 0) st.depth++;
+    if (progress)
+      fprintf(stderr, "level %u gen %llu new %llu distinct %llu rows %.2f GB t %.1f s (expand %.1f insert %.1f seq %.1f)\n",
+              level + 1, (unsigned long long)gen_lvl, (unsigned long long)nxt->size(), (unsigned long long)st.distinct,
+              nxt->bytes / 1e9, elapsed(), t_exp, t_ins, t_seq);
     base += F;
     level++;
     std::swap(cur, nxt);
-    if (st.status != "ok") { st.left = cur.size(); break; }
-    if ((max_distinct && fps.count >= max_distinct) || (max_seconds > 0 && elapsed() > max_seconds)) {
+    if (st.status != "ok") { st.left = cur->size(); break; }
+    if ((max_distinct && st.distinct >= max_distinct) || (max_seconds > 0 && elapsed() > max_seconds)) {
       st.status = "truncated";
-      st.left = cur.size();
+      st.left = cur->size();
       break;
     }
   }
-  st.distinct = fps.count;
   st.seconds = elapsed();
 }
 
@@ -1359,6 +1557,10 @@ int main(int argc, char** argv) {
     } else if (k == "--max-distinct") ck.max_distinct = std::stoull(val());
     else if (k == "--max-seconds") ck.max_seconds = std::stod(val());
     else if (k == "--threads") ck.threads = std::stoi(val());
+    else if (k == "--fp-slots") ck.fp_slots = std::stoull(val());
+    else if (k == "--spill-dir") ck.spill_dir = val();
+    else if (k == "--no-trace") ck.trace = false;
+    else if (k == "--progress") ck.progress = true;
     else if (k == "--trace") print_trace = true;
     else if (k == "--reverse-order") ck.reverse_order = true;
     else if (k == "--dump-fps") fpdump = val();
@@ -1366,6 +1568,8 @@ int main(int argc, char** argv) {
   }
   if (C.inv_order.empty() && argc > 0) C.inv_order = {"LeaderHasAllAckedValues", "NoLogDivergence"};
   if (C.N < 1 || C.N > MAXN || C.V < 1 || C.V > MAXV) { fprintf(stderr, "bad N/V\n"); return 2; }
+  if (C.E > 15 || C.R > 15) { fprintf(stderr, "MaxElections/MaxRestarts > 15 do not fit the hidden-variable key\n"); return 2; }
+  if (print_trace && !ck.trace) { fprintf(stderr, "--trace needs the trace records (drop --no-trace)\n"); return 2; }
   if (!fpdump.empty()) ck.fpdump = fopen(fpdump.c_str(), "wb");
   ck.run();
   if (ck.fpdump) fclose(ck.fpdump);

@@ -321,6 +321,19 @@ unsigned long long known_spec_hash(const std::string& module) {
   return it == k.end() ? 0 : it->second;
 }
 
+// Does the module text define operator `name` (a line starting `name ==` or `name(...) ==`)?
+static bool defines_operator(const std::string& tla, const std::string& name) {
+  size_t p = 0;
+  while ((p = tla.find(name, p)) != std::string::npos) {
+    const bool bol = p == 0 || tla[p - 1] == '\n';
+    size_t q = p + name.size();
+    while (q < tla.size() && (tla[q] == ' ' || tla[q] == '\t')) q++;
+    if (bol && q + 1 < tla.size() && tla[q] == '=' && tla[q + 1] == '=') return true;
+    p += name.size();
+  }
+  return false;
+}
+
 rmc_model* load_model(const std::string& module, const std::string& cfg_text, const std::string& tla_text) {
   auto m = new rmc_model();
   try {
@@ -423,6 +436,13 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
       if (spec != KRAFT && n == "LogMatching") id = 6;
       if (spec != KRAFT && n == "LeaderCompleteness") id = 7;
       if (spec != KRAFT && n == "StateMachineSafety") id = 8;
+      // ... but not on the TLC-compatible path (a .tla was given): TLC resolves
+      // an INVARIANT name in the module, and no reference spec defines these,
+      // so there the name is unknown exactly as TLC would report it
+      if (id >= 5 && !tla_text.empty() && !defines_operator(tla_text, n))
+        throw std::runtime_error("invariant " + n + " is not defined in module " + module +
+                                 " (the classic Raft invariants are built-in extras of the checker: load the cfg "
+                                 "with rmc_model_load_text / raftmc -module " + module + ")");
       if (id == -2) continue;  // TestInv == TRUE
       if (id < 0) throw std::runtime_error("unsupported invariant " + n);
       if (M.ninv >= 9) throw std::runtime_error("too many invariants");
@@ -930,6 +950,47 @@ static void ckpt_read_rows(const std::string& path, uint32_t* dev, size_t n, siz
   }
   fclose(f);
 }
+// The same frontier file streamed straight into host-frontier pages (a level
+// that only fit on the host when the snapshot was taken): no device copy.
+static void ckpt_read_rows_host(const std::string& path, HostLevel& h, HostPagePool& pool, size_t n, size_t w0,
+                                size_t w) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("recover: cannot read " + path);
+  fseek(f, 0, SEEK_END);
+  if ((size_t)ftell(f) != n * w0 * 4) { fclose(f); throw std::runtime_error("recover: " + path + " has the wrong size"); }
+  fseek(f, 0, SEEK_SET);
+  h.reserve(n, pool);
+  std::vector<uint32_t> in(w0);
+  for (size_t r0 = 0; r0 < n;) {
+    const size_t k = std::min<size_t>(h.page_rows - r0 % h.page_rows, n - r0);
+    uint32_t* dst = const_cast<uint32_t*>(h.row(r0));
+    if (w == w0) {
+      if (fread(dst, 4, k * w, f) != k * w) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
+    } else {
+      for (size_t r = 0; r < k; r++) {
+        if (fread(in.data(), 4, w0, f) != w0) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
+        memcpy(dst + r * w, in.data(), w0 * 4);
+        memset(dst + r * w + w0, 0, (w - w0) * 4);
+      }
+    }
+    r0 += k;
+  }
+  h.rows = n;
+  fclose(f);
+}
+// Every snap-* subdirectory of dir but `keep` (an interrupted rotation, or a
+// snapshot of another model whose meta was replaced, leaves them behind).
+static void ckpt_remove_stale(const std::string& dir, unsigned long long keep) {
+  std::vector<std::string> stale;
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) {
+      std::string n = e->d_name;
+      if (n.rfind("snap-", 0) == 0 && n != ckpt_subdir(keep)) stale.push_back(n);
+    }
+    closedir(d);
+  }
+  for (auto& n : stale) remove_tree(dir + "/" + n);
+}
 static void ckpt_write_meta(const std::string& dir, const rmc_model* m, const Ckpt& c) {
   const std::string path = dir + "/checkpoint.meta", tmp = path + ".tmp";
   FILE* f = fopen(tmp.c_str(), "w");
@@ -956,7 +1017,12 @@ static Ckpt ckpt_read_meta(const std::string& dir, const rmc_model* m) {
                      "generated %llu distinct %llu depth %u cur_base %llu cur_n %llu hidden %llu rate %lg levels %zu",
                   &ver, module, &c.seq, &c.sig, &c.kmax, &c.fpw, &c.slots, &c.generated, &c.distinct, &c.depth,
                   &c.cur_base, &c.cur_n, &c.hidden, &c.rate, &nl);
-  if (ok != 15 || ver != 2) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
+  if (ok >= 1 && ver != 2) {
+    fclose(f);
+    throw std::runtime_error("recover: " + path + " is checkpoint format version " + std::to_string(ver) +
+                             "; this build reads version 2 (resume it with the build that wrote it)");
+  }
+  if (ok != 15) { fclose(f); throw std::runtime_error("recover: unreadable " + path + " (format version 2 expected)"); }
   for (size_t k = 0; k < nl; k++) {
     unsigned long long g = 0, d = 0;
     if (fscanf(f, "%llu %llu", &g, &d) != 2) { fclose(f); throw std::runtime_error("recover: unreadable " + path); }
@@ -1062,7 +1128,20 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   if (recovering) slots = rc.slots;
   if (slots & (slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
   unsigned long long fcap = opt->frontier_cap ? opt->frontier_cap : std::max(1ULL << 22, m->hint_fcap);
-  if (recovering) fcap = std::max(fcap, rc.cur_n);
+  size_t hbm_total = 0;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceTotalMem(&hbm_total, dev);
+  }
+  // A snapshot whose level is past the auto switch's threshold (or one
+  // resumed with host_frontier = 1) resumes on the host: its rows stream from
+  // the file into pinned pages and never need device frontiers of that size.
+  const bool rec_host = recovering && opt->host_frontier != -1 &&
+                        (opt->host_frontier == 1 ||
+                         (hbm_total && (double)rc.cur_n * std::max(rc.rate, 1.0) * 1.25 * (double)(W * 4) >
+                                           0.25 * (double)hbm_total) ||
+                         getenv("RMC_RECOVER_TO_HOST"));  // test hook
+  if (recovering && !rec_host) fcap = std::max(fcap, rc.cur_n);
   const int maxsucc = M.nfixed + M.kmax;
   // 8M parents per launch (bench cfg: 1.325 s per check vs 1.349 s at 4M; 4M
   // was 4% below 2M, 2M 4% below 1M), held to 2^31 candidates per launch
@@ -1085,11 +1164,11 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   GrowBuf &fa = A.fa, &fb = A.fb, &trp = A.trp, &trb = A.trb;
   table.ensure(slots * ew * 8);
   HIPCHK(hipMemsetAsync(table.p, 0xFF, slots * ew * 8, stream));
-  if (opt->host_frontier != 1) {
+  if (opt->host_frontier != 1 && !rec_host) {
     fa.ensure(fcap * W * 4);
     fb.ensure(fcap * W * 4);
-  } else {  // always host: only Init (or a recovered level) passes through the device
-    fa.ensure((recovering ? std::max(1ULL, rc.cur_n) : 1ULL) * W * 4);
+  } else {  // host levels: only Init (or a small recovered level) passes through the device
+    fa.ensure((recovering && !rec_host ? std::max(1ULL, rc.cur_n) : 1ULL) * W * 4);
   }
   cslot.ensure(cand_cap * 8);
   cob.ensure(cand_cap * 4);
@@ -1181,7 +1260,8 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   if (recovering) {  // resume from the snapshot instead of Init
     const std::string dir = std::string(opt->recover_dir) + "/" + ckpt_subdir(rc.seq);
     ckpt_read(dir + "/fpset.bin", table.p, slots * ew * 8, stage(), ck_stage_bytes);
-    ckpt_read_rows(dir + "/frontier.bin", fa.as<uint32_t>(), rc.cur_n, snap_words, W, stage(), ck_stage_bytes);
+    if (!rec_host)  // else streamed into host pages below, once they exist
+      ckpt_read_rows(dir + "/frontier.bin", fa.as<uint32_t>(), rc.cur_n, snap_words, W, stage(), ck_stage_bytes);
     ckpt_read(dir + "/trace_parent.bin", trp.p, rc.distinct * 8, stage(), ck_stage_bytes);
     ckpt_read(dir + "/trace_bind.bin", trb.p, rc.distinct * 2, stage(), ck_stage_bytes);
     generated = rc.generated;
@@ -1262,6 +1342,14 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   // depend on it.
   const size_t win_in_bytes = chunk * W * 4, win_out_bytes = 3 * chunk * W * 4;
   bool windows = false;
+  struct WindowsGuard {  // every exit path (an E_CAP_MSG re-run, a throw, auto mode that never switched)
+    Arena& A;
+    bool& windows;
+    ~WindowsGuard() {
+      if (windows)
+        for (DevBuf* b : {&A.hwin_in[0], &A.hwin_in[1], &A.hwin_out[0], &A.hwin_out[1]}) b->release();
+    }
+  } windows_guard{A, windows};
   auto reserve_windows = [&]() {
     if (windows) return;
     A.hwin_in[0].ensure(win_in_bytes);
@@ -1400,12 +1488,27 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     a.st = stbuf.as<DevStatus>();
   };
   try {
-  if (hf_opt == 1 && !hf) enter_hf();
-  size_t hbm_total = 0;
-  {
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceTotalMem(&hbm_total, dev);
+  if (rec_host) {  // the snapshot's level goes straight to host pages
+    auto th0 = std::chrono::steady_clock::now();
+    HIPCHK(hipStreamSynchronize(stream));
+    reserve_windows();
+    hs.init(stream);
+    pool.start_fillers(hf_pin_ahead, hf_pin_threads);
+    hcur.init(page_rows, row_bytes);
+    hnxt.init(page_rows, row_bytes);
+    ckpt_read_rows_host(std::string(opt->recover_dir) + "/" + ckpt_subdir(rc.seq) + "/frontier.bin", hcur, pool,
+                        rc.cur_n, snap_words, W);
+    fa.release();
+    fb.release();
+    cur = nxt = nullptr;
+    hf = true;
+    hwin_c0[0] = hwin_c0[1] = ~0ULL;
+    hf_copy_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - th0).count();
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] recovered level of %llu states into host memory (%.1f GiB of pinned pages)\n", rc.cur_n,
+              pool.allocated / 1073741824.0);
   }
+  if (hf_opt == 1 && !hf) enter_hf();
   while (status == 0 && cur_n > 0) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     if (opt->time_limit > 0 && secs(t0, now()) >= opt->time_limit) { status = 4; message = "time limit"; break; }
@@ -1775,7 +1878,8 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       c.rate = rate;
       c.levels = m->levels;
       ckpt_write_meta(dir, m, c);
-      if (have_prev) remove_tree(dir + "/" + ckpt_subdir(prev_seq));
+      (void)prev_seq;
+      ckpt_remove_stale(dir, c.seq);
       last_ckpt = now();
       if (opt->verbose)
         fprintf(stderr, "[rmc] checkpoint at depth %u in %s (%.3fs)\n", depth, dir.c_str(), secs(tc0, now()));
@@ -1980,8 +2084,8 @@ int rmc_abi_layout(uint64_t* out, int cap) {
       offsetof(rmc_options, recover_dir), offsetof(rmc_options, host_frontier),
       sizeof(rmc_result), offsetof(rmc_result, generated), offsetof(rmc_result, distinct),
       offsetof(rmc_result, left_on_queue), offsetof(rmc_result, depth), offsetof(rmc_result, status),
-      offsetof(rmc_result, violated), offsetof(rmc_result, message), offsetof(rmc_result, hidden_var_collisions),
-      offsetof(rmc_result, seconds), offsetof(rmc_result, expand_ms), offsetof(rmc_result, mark_ms),
+      offsetof(rmc_result, violated), offsetof(rmc_result, hidden_var_collisions), offsetof(rmc_result, seconds),
+      offsetof(rmc_result, message), offsetof(rmc_result, expand_ms), offsetof(rmc_result, mark_ms),
       offsetof(rmc_result, materialize_ms), offsetof(rmc_result, expand_launches), offsetof(rmc_result, state_bytes),
       offsetof(rmc_result, max_msgs), offsetof(rmc_result, hash_capacity)};
   const int n = (int)(sizeof v / sizeof v[0]);

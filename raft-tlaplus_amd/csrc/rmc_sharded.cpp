@@ -210,12 +210,15 @@ struct ShmComm : Comm {
       }
     }
     barrier();
+    // every rank has mapped the segment: its name can go now (the mappings
+    // stay valid), so a later check under the same name can never attach to
+    // this one while rank 0 is still tearing it down
+    if (rank == 0) shm_unlink(name.c_str());
   }
   ~ShmComm() override {
     if (!base) return;
     try { barrier(); } catch (...) {}
     munmap(base, bytes);
-    if (rank == 0) shm_unlink(name.c_str());
   }
   // sense-reversing barrier in the segment; a rank that waits 120 s (a peer
   // failed or died) throws instead of hanging

@@ -39,8 +39,8 @@ class Result(ctypes.Structure):
     _fields_ = [("generated", ctypes.c_uint64), ("distinct", ctypes.c_uint64),
                 ("left_on_queue", ctypes.c_uint64), ("depth", ctypes.c_uint32),
                 ("status", ctypes.c_int), ("violated", ctypes.c_char * 64),
-                ("message", ctypes.c_char * 256),
                 ("hidden_var_collisions", ctypes.c_uint64), ("seconds", ctypes.c_double),
+                ("message", ctypes.c_char * 256),
                 ("expand_ms", ctypes.c_double), ("mark_ms", ctypes.c_double),
                 ("materialize_ms", ctypes.c_double), ("expand_launches", ctypes.c_uint64),
                 ("state_bytes", ctypes.c_uint32), ("max_msgs", ctypes.c_uint32),

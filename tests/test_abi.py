@@ -94,3 +94,17 @@ def test_check_without_gpu_fails_loudly():
     m = raftmc.Model(module="Raft", cfg_path=os.path.join(ROOT, "configs", "Raft.cfg"))
     with pytest.raises(raftmc.RaftmcError, match="HIP device|no HIP"):
         m.check()
+
+
+def test_result_prefix_is_survey_8b():
+    """rmc_result starts with SURVEY.md §8b's fields in §8b's order and C
+    layout, so a binding written to §8b reads them at the right offsets; the
+    library's extra fields (message, measurements) come after them."""
+    class Survey8b(ctypes.Structure):
+        _fields_ = [("generated", ctypes.c_uint64), ("distinct", ctypes.c_uint64),
+                    ("left_on_queue", ctypes.c_uint64), ("depth", ctypes.c_uint32), ("status", ctypes.c_int),
+                    ("violated", ctypes.c_char * 64), ("hidden_var_collisions", ctypes.c_uint64),
+                    ("seconds", ctypes.c_double)]
+    for f, _ in Survey8b._fields_:
+        assert getattr(raftmc.Result, f).offset == getattr(Survey8b, f).offset, f
+    assert raftmc.Result.message.offset >= ctypes.sizeof(Survey8b)

@@ -59,3 +59,16 @@ def test_comment_and_layout_edits_pass(tmp_path):
     p = tmp_path / "Raft.tla"
     p.write_text("\\* a local note\n" + txt.replace("\n\n", "\n  \n").replace("Init ==", "Init  =="))
     raftmc.Model(str(p), ref("Raft", ".cfg"))
+
+
+def test_classic_invariants_unknown_on_the_tla_path(tmp_path):
+    """TLC resolves INVARIANT names in the module; the reference Raft.tla does
+    not define ElectionSafety, so on the TLC-compatible path (a .tla given) the
+    name is refused as undefined -- the built-in extras are available only
+    through rmc_model_load_text / raftmc -module."""
+    cfg = open(ref("Raft", ".cfg")).read().replace("NoLogDivergence", "NoLogDivergence\n    ElectionSafety")
+    p = tmp_path / "Raft.cfg"
+    p.write_text(cfg)
+    with pytest.raises(raftmc.RaftmcError, match="not defined in module Raft"):
+        raftmc.Model(ref("Raft", ".tla"), str(p))
+    raftmc.Model(module="Raft", cfg_text=cfg)  # the extras path

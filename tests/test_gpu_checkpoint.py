@@ -107,3 +107,39 @@ def test_snapshot_replaces_the_previous_one(tmp_path):
     assert "snapshot %s" % subs[0][len("snap-"):] in (tmp_path / "checkpoint.meta").read_text()
     r = model(g).check(recover_dir=tmp_path)
     assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
+
+
+@pytest.mark.parametrize("width_change", [False, True])
+def test_recover_into_host_pages(tmp_path, monkeypatch, width_change):
+    """A snapshot taken with the levels on the host (RMC_HOST_FRONTIER_AT moves
+    them there mid-level) and resumed with a small frontier_cap: the saved level
+    streams from the file straight into pinned host pages (RMC_RECOVER_TO_HOST
+    stands for "past the auto switch's threshold"), the device frontiers are
+    never sized for it, and the result equals the uninterrupted check -- also
+    when the resumed level overflows the snapshot's message capacity (rows
+    widened on the way into the pages)."""
+    g = SHIPPED["Raft_cfg"]
+    m = model(g)
+    if width_change:
+        m.selftest_set_hint_kmax(8)
+    monkeypatch.setenv("RMC_HOST_FRONTIER_AT", "12")
+    monkeypatch.setenv("RMC_HOST_PAGE_ROWS", "4099")
+    a = m.check(max_depth=16, checkpoint_dir=tmp_path, checkpoint_minutes=0, chunk_parents=20000)
+    assert a["status"] == "stopped" and a["depth"] == 16
+    monkeypatch.delenv("RMC_HOST_FRONTIER_AT")
+    monkeypatch.setenv("RMC_RECOVER_TO_HOST", "1")
+    r = model(g).check(recover_dir=tmp_path, frontier_cap=1 << 10, chunk_parents=30000)
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+def test_stale_snapshots_are_removed(tmp_path):
+    """Snapshot directories the meta does not name (an interrupted rotation, an
+    earlier model's snapshot) are removed at the next snapshot."""
+    g = SHIPPED["Raft_cfg"]
+    (tmp_path / "snap-77").mkdir()
+    (tmp_path / "snap-77" / "fpset.bin").write_bytes(b"x" * 100)
+    model(g).check(max_depth=6, checkpoint_dir=tmp_path, checkpoint_minutes=0)
+    subs = sorted(p.name for p in tmp_path.iterdir() if p.is_dir())
+    assert len(subs) == 1 and subs[0] != "snap-77"
