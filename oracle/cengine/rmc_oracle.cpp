@@ -1011,7 +1011,10 @@ struct FPShard {
     max_load = ml;
     t.assign(std::max<uint64_t>(slots, 1024), Slot{0, 0, 0, 0});
   }
-  inline uint64_t home(uint64_t a, uint64_t n) const { return (uint64_t)(((unsigned __int128)a * n) >> 64); }
+  // the shard is chosen by a's high bits, so the home slot must not be: mix first
+  inline uint64_t home(uint64_t a, uint64_t n) const {
+    return (uint64_t)(((unsigned __int128)(a * 0x9E3779B97F4A7C15ULL) * n) >> 64);
+  }
   void grow() {
     std::vector<Slot> old;
     old.swap(t);
