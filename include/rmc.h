@@ -155,6 +155,23 @@ int rmc_simulate(rmc_model* m, const rmc_options* o, uint64_t walkers, uint32_t 
 int rmc_check_cpu(rmc_model* m, const rmc_options* o, rmc_result* out);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
 int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
+/* Next as a list of disjuncts: comma-separated operator names of the spec
+ * family's definitions, in Next order (e.g. Raft's "Restart, RequestVote, ...,
+ * HandleAppendEntriesResponse, DuplicateMessage"): the action table a module
+ * whose Next lists exactly those disjuncts lowers to through the TLA+ front
+ * end -- reordered, reduced or with the network actions
+ * Raft.tla:540-541 leaves commented out.  For models loaded without a .tla
+ * (rmc_model_load_text).  Returns 0, or a negative value (unknown name;
+ * rmc_last_error()).  rmc_model_next writes the model's current Next the same
+ * way and returns its length. */
+int rmc_model_set_next(rmc_model* m, const char* disjuncts);
+int rmc_model_next(const rmc_model* m, char* out, size_t len);
+/* The TLA+ front end's structural hashes of a module's definitions (the
+ * closure hashes the lowering matches against its action library; used by
+ * tools/gen_tla_known.py): writes "#module M", "#vars <hash>", then one
+ * "name <hash>" line per definition into out and returns the text length,
+ * or a negative value with the parse error in out. */
+int rmc_tla_hashes(const char* tla_text, char* out, size_t len);
 /* ABI self-description for binding checks (ctypes, JNA): fills up to cap values -- sizeof(rmc_options),
  * the offset of each of its fields in declaration order, then sizeof(rmc_result) and its field offsets --
  * and returns how many there are. */

@@ -30,7 +30,11 @@ class RaftSpec:
     # view == <<messages, serverVars, candidateVars, leaderVars, logVars>> (Raft.tla:115)
     hidden_vars = ("acked", "electionCtr", "restartCtr")
 
-    def __init__(self, consts, invariants=("LeaderHasAllAckedValues", "NoLogDivergence")):
+    def __init__(self, consts, invariants=("LeaderHasAllAckedValues", "NoLogDivergence"), next_order=None):
+        # next_order: Next's disjuncts by operator name, in order (default: the
+        # module's own Next); may drop disjuncts or add the network actions the
+        # module defines but leaves commented out of Next (Raft.tla:540-541)
+        self.next_order = tuple(next_order) if next_order else None
         self.server_names = _sorted_names(consts["Server"])
         self.value_names = _sorted_names(consts["Value"])
         self.N = len(self.server_names)
@@ -259,6 +263,25 @@ class RaftSpec:
     def after_commit(self, s, t, i):
         pass
 
+    def DuplicateMessage(self, s):
+        # Raft.tla:512-514 with Duplicate (:157-160): \E m \in DOMAIN messages, messages[m] + 1
+        for m, c in s["messages"]:
+            d = dict(s["messages"])
+            d[m] = c + 1
+            t = dict(s)
+            t["messages"] = freeze_msgs(d)
+            yield t
+
+    def DropMessage(self, s):
+        # Raft.tla:519-521 with Discard (:164-167): messages[m] > 0, messages[m] - 1
+        for m, _ in s["messages"]:
+            nm = self.Discard(s["messages"], m)
+            if nm is None:
+                continue
+            t = dict(s)
+            t["messages"] = nm
+            yield t
+
     def UpdateTerm(self, s):
         # Raft.tla:348-355
         for m, _ in s["messages"]:
@@ -417,6 +440,27 @@ class RaftSpec:
 
     def actions(self):
         """Next (Raft.tla:527-539) split into TLC actions, in TLC order."""
+        if self.next_order:
+            return self.ordered_actions(self.next_order)
+        return self.default_actions()
+
+    def ordered_actions(self, order):
+        """Next with the given disjuncts (by operator name) in the given order:
+        each disjunct's TLC actions as in the module's own Next, plus the network
+        actions \E m \in DOMAIN messages : DuplicateMessage(m) / DropMessage(m)."""
+        groups = {}
+        for label, fn in self.default_actions():
+            groups.setdefault(label.split("(")[0], []).append((label, fn))
+        groups["DuplicateMessage"] = [("DuplicateMessage", self.DuplicateMessage)]
+        groups["DropMessage"] = [("DropMessage", self.DropMessage)]
+        out = []
+        for name in order:
+            if name not in groups:
+                raise ValueError("no disjunct %s in %s" % (name, self.module))
+            out.extend(groups[name])
+        return out
+
+    def default_actions(self):
         A = []
         n = self.server_names
         vn = self.value_names

@@ -171,7 +171,7 @@ class Result:
                     max_msgs=self.max_msgs)
 
 
-def bfs(spec, max_states=None, keep_states=False, progress=False):
+def bfs(spec, max_states=None, keep_states=False, progress=False, max_depth=None):
     """Exhaustive BFS of `spec` with TLC -workers 1 semantics.
 
     spec must provide: init_states(), actions() -> [(label, fn(state) -> iterable)],
@@ -230,6 +230,10 @@ def bfs(spec, max_states=None, keep_states=False, progress=False):
     res.levels.append((res.generated, len(level)))
     depth = 1
     while level:
+        if max_depth and depth >= max_depth:  # as rmc_options.max_depth: stop after that many levels
+            res.status = "stopped"
+            res.left = len(level)
+            break
         nxt = []
         gen_lvl = 0
         for pidx in level:

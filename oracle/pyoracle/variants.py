@@ -227,7 +227,7 @@ class RaftFsyncSpec(_SendOnceOnly, RaftSpec):
     def after_aeresp(self, s, t, i, j):
         pass
 
-    def actions(self):
+    def default_actions(self):
         """Next (RaftFsync.tla:522-536) split into TLC actions, in TLC order."""
         A = []
         n, vn = self.server_names, self.value_names
@@ -555,7 +555,7 @@ class PullRaftSpec(RaftSpec):
             t["messages"] = msgs
             yield t
 
-    def actions(self):
+    def default_actions(self):
         """Next (PullRaft.tla:542-558) split into TLC actions, in TLC order."""
         A = []
         n, vn = self.server_names, self.value_names
@@ -749,9 +749,9 @@ class PullRaftVariant2Spec(PullRaftSpec):
             t["messages"] = msgs
             yield t
 
-    def actions(self):
+    def default_actions(self):
         """Next (PullRaftVariant2.tla:560-576): PullRaft's disjuncts in the same order."""
-        return PullRaftSpec.actions(self)
+        return PullRaftSpec.default_actions(self)
 
     def permute_value(self, var, val, p):
         # canonical forms only need an injective, totally ordered encoding:

@@ -24,6 +24,7 @@
 #include <vector>
 #include "rmc_internal.h"
 #include "rmc_fpset.h"
+#include "rmc_tla.h"
 
 using namespace rmc;
 using namespace rmcx;
@@ -198,14 +199,19 @@ const char* act_label(int a) {
                             "HandleSuccessPullEntriesResponse", "HandleFailPullEntriesResponse",
                             "RejectFetchRequest", "DivergingFetchRequest", "AcceptFetchRequest",
                             "HandleBeginQuorumRequest", "SendFetchRequest", "HandleSuccessFetchResponse",
-                            "HandleDivergingFetchResponse", "HandleErrorFetchResponse"};
+                            "HandleDivergingFetchResponse", "HandleErrorFetchResponse", "DuplicateMessage",
+                            "DropMessage"};
   return (a >= 0 && a < A_NUM) ? n[a] : "?";
 }
 
-void build_actions(Model& M) {
+// The action table in Next order: the spec's own (the reference modules'
+// Next), or the one the TLA+ front end lowered from the module text.
+void build_actions(Model& M, const std::vector<std::pair<int, int>>* lowered) {
   struct E { int id, kind; };
   std::vector<E> t;
-  switch (M.spec) {
+  if (lowered && !lowered->empty()) {
+    for (auto& a : *lowered) t.push_back({a.first, a.second});
+  } else switch (M.spec) {
     case RAFT: case FLEX:  // Raft.tla:527-539; FlexibleRaft.tla:488-500
       t = {{A_RESTART, K_I}, {A_REQUESTVOTE, K_I}, {A_BECOMELEADER, K_I}, {A_CLIENT, K_IV}, {A_ADVCOMMIT, K_I},
            {A_APPENDENTRIES, K_IJ}, {A_UPDATETERM, K_MSG}, {A_HRVREQ, K_MSG}, {A_HRVRESP, K_MSG},
@@ -227,24 +233,31 @@ void build_actions(Model& M) {
            {A_KSENDFETCH, K_IJ}, {A_KHSUCC, K_MSG}, {A_KHDIV, K_MSG}, {A_KHERR, K_MSG}};
       break;
   }
+  if ((int)t.size() > MAXACT) throw std::runtime_error("Next has more disjuncts than the lowering's " +
+                                                       std::to_string(MAXACT) + " action slots");
   M.nact = (int)t.size();
   int off = 0, nf = 0;
   for (int a = 0; a < A_NUM; a++) M.msg_act_slot[a] = 0;
+  M.msg_act_mask = 0;
   for (int s = 0; s < M.nact; s++) {
     M.act_fb_first[s] = (uint8_t)nf;
     M.act_id[s] = t[s].id;
     M.act_kind[s] = t[s].kind;
     M.act_off[s] = off;
     int size = t[s].kind == K_I ? M.N : t[s].kind == K_IV ? M.N * M.V : t[s].kind == K_IJ ? M.N * M.N : M.kmax;
-    if (t[s].kind == K_MSG) M.msg_act_slot[t[s].id] = s;
-    else
+    if (t[s].kind == K_MSG) {
+      M.msg_act_slot[t[s].id] = s;
+      M.msg_act_mask |= 1ULL << t[s].id;
+    } else
       for (int x = 0; x < size; x++) {
         // bindings the constants disable for good are not evaluated at all
         // (their ordinals stay reserved, so TLC's order is unchanged):
         // AppendEntries / RequestVote(i, j) / SendPullEntriesRequest with i = j
         // (Raft.tla:264, RaftFsync.tla:235, PullRaft.tla:397), Restart with
         // MaxRestarts = 0 (Raft.tla:227), elections with MaxElections = 0
-        const int id = t[s].id, i = x % M.N, j = x / M.N;
+        const int id = t[s].id;
+        // K_M (\E m \in DOMAIN messages): the message slot k = x as (k & 15, k >> 4)
+        const int i = t[s].kind == K_M ? (x & 15) : x % M.N, j = t[s].kind == K_M ? (x >> 4) : x / M.N;
         if (t[s].kind == K_IJ && i == j &&
             (id == A_APPENDENTRIES || id == A_RVIJ || id == A_SENDPULL || id == A_KSENDFETCH))  // KRaft.tla:608
           continue;
@@ -340,31 +353,36 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     m->module = module;
     m->tla_text = tla_text;
     int spec = spec_of_module(module);
-    if (spec < 0)
-      throw std::runtime_error("unsupported module '" + module +
-                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft, PullRaftVariant2, KRaft)");
     if (!tla_text.empty() && tla_text.find("MODULE " + module) == std::string::npos)
       throw std::runtime_error("the .tla file does not declare MODULE " + module);
-    if (!tla_text.empty()) {
-      const unsigned long long h = fnv1a64(normalise_tla(tla_text));
-      if (h != known_spec_hash(module)) {
-        char hb[32];
-        snprintf(hb, sizeof hb, "%016llx", h);
-        throw std::runtime_error("the TLA+ text of " + module + ".tla (normalised hash " + hb +
-                                 ") is not the reference spec this checker lowers (Vanlightly/raft-tlaplus " +
-                                 module + ".tla; comments and layout may differ, the definitions may not); "
-                                 "checking an edited spec needs a TLA+ front end (SURVEY.md 8f rank 4)");
-      }
-    }
+    // The reference text of a module this checker lowers (comments and layout
+    // may differ): its built-in action table.  Any other text goes through the
+    // TLA+ front end (rmc_tla.cpp), which lowers what it can and names what it
+    // cannot.
+    const bool reference_text =
+        tla_text.empty() || (spec >= 0 && fnv1a64(normalise_tla(tla_text)) == known_spec_hash(module));
+    if (tla_text.empty() && spec < 0)
+      throw std::runtime_error("unsupported module '" + module +
+                               "' (supported: Raft, FlexibleRaft, RaftFsync, PullRaft, PullRaftVariant2, KRaft)");
     Cfg c = parse_cfg(cfg_text);
     if (!c.spec.empty()) throw std::runtime_error("SPECIFICATION is not supported; use INIT Init / NEXT Next");
-    if (c.init != "Init" || c.next != "Next")
-      throw std::runtime_error("cfg must bind INIT Init and NEXT Next (got '" + c.init + "', '" + c.next + "')");
     if (!c.properties.empty()) throw std::runtime_error("PROPERTY checking (liveness) is not supported");
     if (!c.constraints.empty()) throw std::runtime_error("CONSTRAINT is not supported");
-    if (c.view != "view") throw std::runtime_error("cfg must set VIEW view (the reference cfgs do)");
-    if (!c.symmetry.empty() && c.symmetry != "symmServers")
-      throw std::runtime_error("only SYMMETRY symmServers is supported");
+    rmc::tla::Lowering low;
+    if (reference_text) {
+      if (c.init != "Init" || c.next != "Next")
+        throw std::runtime_error("cfg must bind INIT Init and NEXT Next (got '" + c.init + "', '" + c.next + "')");
+      if (c.view != "view") throw std::runtime_error("cfg must set VIEW view (the reference cfgs do)");
+      if (!c.symmetry.empty() && c.symmetry != "symmServers")
+        throw std::runtime_error("only SYMMETRY symmServers is supported");
+    } else {
+      if (c.init != "Init") throw std::runtime_error("cfg must bind INIT Init (got '" + c.init + "')");
+      if (c.view.empty()) throw std::runtime_error("cfg must set a VIEW (the lowering fingerprints the spec's view)");
+      low = rmc::tla::lower(tla_text, c.next, c.view, c.symmetry, c.invariants);
+      spec = low.spec;
+      m->lowered_actions = low.actions;
+      m->lowered_labels = low.labels;
+    }
     auto need = [&](const std::string& n) -> CfgVal& {
       auto it = c.consts.find(n);
       if (it == c.consts.end()) throw std::runtime_error("cfg: constant " + n + " is not assigned");
@@ -426,6 +444,15 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     }
     M.ninv = 0;
     for (auto& n : c.invariants) {
+      if (!reference_text) {  // the front end matched the module's invariant definitions
+        auto it = low.invariants.find(n);
+        if (it == low.invariants.end())
+          throw std::runtime_error("invariant " + n + " is not defined in module " + module);
+        if (M.ninv >= 9) throw std::runtime_error("too many invariants");
+        M.inv[M.ninv++] = it->second;
+        m->inv_names.push_back(n);
+        continue;
+      }
       int id = n == "LeaderHasAllAckedValues" ? 0 : n == "NoLogDivergence" ? 1
                                                : n == "CommittedEntriesReachMajority" ? 2
                                                : n == "TestInv" ? -2 : -1;
@@ -494,7 +521,7 @@ void finalize_model(rmc_model* m, uint32_t kmax) {
   M.words = words;
   M.kmax = words - 1 - 4 * M.N;
   M.fpw = 1;
-  build_actions(M);
+  build_actions(M, &m->lowered_actions);
 }
 
 uint32_t default_kmax(const Model& M) {
@@ -742,10 +769,13 @@ std::string binding_label(const rmc_model* m, int b, int act) {
     int slot = M.fb_act[b], x = M.fb_x[b];
     int kind = M.act_kind[slot];
     int i = x % M.N, jv = x / M.N;
+    if (!m->lowered_labels.empty()) name = m->lowered_labels[slot];
+    if (kind == K_M) return name;
     if (kind == K_I) return name + "(" + m->server_names[i] + ")";
     if (kind == K_IV) return name + "(" + m->server_names[i] + ", " + m->value_names[jv] + ")";
     return name + "(" + m->server_names[i] + ", " + m->server_names[jv] + ")";
   }
+  if (!m->lowered_labels.empty() && act >= 0 && act < A_NUM) return m->lowered_labels[M.msg_act_slot[act]];
   return name;
 }
 
@@ -2099,6 +2129,60 @@ void rmc_options_default(rmc_options* o) {
   o->n_gpus = 1;
   o->fp_bits = 64;
   o->tlc_order = 1;
+}
+
+int rmc_model_set_next(rmc_model* m, const char* disjuncts) {
+  if (!m || !disjuncts) { g_last_error = "null argument"; return -1; }
+  try {
+    std::vector<std::string> names;
+    std::string cur;
+    for (const char* p = disjuncts;; p++) {
+      if (*p == ',' || *p == 0) {
+        while (!cur.empty() && cur.back() == ' ') cur.pop_back();
+        if (!cur.empty()) names.push_back(cur);
+        cur.clear();
+        if (!*p) break;
+      } else if (!(cur.empty() && *p == ' ')) {
+        cur += *p;
+      }
+    }
+    if (names.empty()) throw std::runtime_error("empty Next");
+    m->lowered_actions = rmc::tla::actions_by_name(m->M.spec, names);
+    m->lowered_labels = names;
+    m->hint_slots = m->hint_fcap = m->hint_trcap = 0;
+    m->hint_kmax = 0;
+    return 0;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -2;
+  }
+}
+
+int rmc_model_next(const rmc_model* m, char* out, size_t len) {
+  if (!m || !out || !len) return -1;
+  std::string o;
+  if (!m->lowered_actions.empty()) {
+    for (auto& a : m->lowered_actions) o += (o.empty() ? "" : ",") + rmc::tla::action_name(m->M.spec, a.first);
+  } else {
+    Model M = m->M;
+    build_actions(M, nullptr);
+    for (int s = 0; s < M.nact; s++) o += (o.empty() ? "" : ",") + rmc::tla::action_name(M.spec, M.act_id[s]);
+  }
+  snprintf(out, len, "%s", o.c_str());
+  return (int)o.size();
+}
+
+int rmc_tla_hashes(const char* tla_text, char* out, size_t len) {
+  if (!tla_text || !out || !len) return -1;
+  try {
+    const std::string r = rmc::tla::hash_report(tla_text);
+    snprintf(out, len, "%s", r.c_str());
+    return (int)r.size();
+  } catch (std::exception& e) {
+    snprintf(out, len, "error: %s", e.what());
+    g_last_error = e.what();
+    return -2;
+  }
 }
 
 int rmc_model_load_text(const char* module, const char* cfg_text, rmc_model** out, char* err, size_t errlen) {

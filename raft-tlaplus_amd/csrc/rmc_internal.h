@@ -32,6 +32,10 @@ struct rmc_model {
   std::vector<std::string> server_names, value_names, inv_names;
   std::vector<std::string> var_order;
   std::vector<std::pair<std::string, std::string>> cfg_consts;  // cfg CONSTANTS, as written back by the trace module
+  // set when the TLA+ front end lowered the module text (rmc_tla.cpp): the
+  // action table in the module's Next order, and its own operator names
+  std::vector<std::pair<int, int>> lowered_actions;
+  std::vector<std::string> lowered_labels;
   // results of the last check
   std::vector<std::pair<unsigned long long, unsigned long long>> levels;
   std::vector<std::vector<uint32_t>> trace_states;

@@ -57,9 +57,17 @@ enum ActId {
   A_APPENDENTRIES, A_ADVFSYNC, A_UPDATETERM, A_HRVREQ, A_HRVRESP, A_REJAE, A_ACCAE, A_HAERESP,
   A_REJPULL, A_ACCPULL, A_LEARN, A_SENDPULL, A_HSUCC, A_HFAIL,
   // KRaft (pull-raft/KRaft.tla:823-840)
-  A_KREJFETCH, A_KDIVFETCH, A_KACCFETCH, A_KHBQ, A_KSENDFETCH, A_KHSUCC, A_KHDIV, A_KHERR, A_NUM
+  A_KREJFETCH, A_KDIVFETCH, A_KACCFETCH, A_KHBQ, A_KSENDFETCH, A_KHSUCC, A_KHDIV, A_KHERR,
+  // the network actions every module defines but leaves out of Next (Raft.tla:509-522, :540-541):
+  // DuplicateMessage(m) / DropMessage(m), bound by \E m \in DOMAIN messages (the TLA+ front end
+  // lowers them when a module's Next re-enables them; rmc_tla.cpp)
+  A_DUP, A_DROP, A_NUM
 };
-enum ActKind { K_I = 0, K_IV = 1, K_IJ = 2, K_MSG = 3 };
+// binding forms: \E i \in Server (K_I), i \in Server, v \in Value (K_IV), i, j \in Server (K_IJ), a message
+// handler ranging over DOMAIN messages with one enabled action per element (K_MSG), and an action bound
+// by \E m \in DOMAIN messages that is NOT exclusive with the handlers (K_M: its bindings are fixed
+// bindings, one per message slot k = x, encoded in a fixed binding's (i, jv) as k & 15, k >> 4)
+enum ActKind { K_I = 0, K_IV = 1, K_IJ = 2, K_MSG = 3, K_M = 4 };
 enum ErrCode {
   E_NONE = 0,
   E_DOMAIN = 1,     // TLC evaluation error: sequence applied outside its domain
@@ -92,6 +100,7 @@ struct Model {
   uint32_t fb_desc[MAXFIXED];
   uint8_t act_fb_first[MAXACT], act_fb_end[MAXACT];  // action slot -> its fixed bindings [first, end)
   int msg_act_slot[A_NUM];                   // action slot of each message action
+  unsigned long long msg_act_mask;           // bit a: message action a is a disjunct of this model's Next
   int ordinal_limit;
   int fpw;                    // fingerprint width in 64-bit words (1: 64-bit, 2: 128-bit)
   int bind_words, ord_words;  // u32 words of a per-parent bitmask over bindings / over ordinals
@@ -1190,7 +1199,7 @@ RMC_HD bool msg_live(const PState<SPEC, N>& s, uint32_t w) {
 
 // ---- message-bound actions: exactly one can be enabled per DOMAIN element
 template <int SPEC, int N>
-RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
+RMC_HD bool act_message_any(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
   if (SPEC == KRAFT) return kr_message(s, M, k, d);
   uint32_t w = s.msg(k);
   if (!msg_live<SPEC, N>(s, w)) return false;  // fast reject before the full decode
@@ -1360,6 +1369,14 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
   return false;
 }
 
+// ... of those in this model's Next (a module may drop handlers from Next:
+// the handlers' guards are mutually exclusive, so a dropped one leaves its
+// messages with no enabled action rather than passing them to another)
+template <int SPEC, int N>
+RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d) {
+  return act_message_any<SPEC, N>(s, M, k, d) && ((M.msg_act_mask >> d.act) & 1ULL);
+}
+
 // A fixed binding given as (action id, its bound server i, its second bound
 // variable jv) with its TLC ordinal already known: no table lookups, so a lane
 // with its own binding issues no dependent loads before the action's guard.
@@ -1368,6 +1385,21 @@ RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   d.act = act;
   d.ordinal = ordinal;
+  if (act == A_DUP || act == A_DROP) {
+    // DuplicateMessage(m): Duplicate(m) -- m \in DOMAIN messages, messages[m] + 1 (Raft.tla:157-160, :512-514);
+    // DropMessage(m): Discard(m) -- messages[m] > 0, messages[m] - 1 (Raft.tla:164-167, :519-521)
+    const int k = i | (jv << 4);
+    if (k >= s.nmsg()) return false;
+    const uint32_t w = s.msg(k);
+    if (act == A_DROP) {
+      if (!(msg_count(w) > 0)) return false;
+      push_op(d, k, w - 1u);
+      return true;
+    }
+    if (msg_count(w) >= 7) { d.err = E_CAP_COUNT; return true; }
+    push_op(d, k, w + 1u);
+    return true;
+  }
   if (SPEC == KRAFT) return kr_fixed(s, M, act, i, jv, d);
   switch (act) {
     case A_RESTART: return act_restart(s, M, i, d);
@@ -1387,6 +1419,7 @@ RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int
 // with bound-variable index x (first bound variable fastest).
 template <int SPEC, int N>
 RMC_HD bool eval_fixed(const PState<SPEC, N>& s, const Model& M, int slot, int x, Delta& d) {
+  if (M.act_kind[slot] == K_M) return eval_fixed_id(s, M, M.act_id[slot], x & 15, x >> 4, M.act_off[slot] + x, d);
   return eval_fixed_id(s, M, M.act_id[slot], x % N, x / N, M.act_off[slot] + x, d);
 }
 // Binding b whose TLC ordinal is known (k_expand phase C, k_materialize):
@@ -1423,6 +1456,13 @@ template <int SPEC, int N>
 RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
   const uint32_t desc = M.fb_desc[b];
   const int i = (int)((desc >> 24) & 15u), jv = (int)(desc >> 28);
+  {
+    const int act = (int)((desc >> 16) & 0xFFu);
+    if (act == A_DUP || act == A_DROP) {
+      const int k = i | (jv << 4);
+      return k < s.nmsg() && (act == A_DUP || msg_count(s.msg(k)) > 0);
+    }
+  }
   const uint32_t a = s.A(i);
   const int st = a_st(a);
   if (SPEC == KRAFT) {

@@ -53,7 +53,7 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
            "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm",
-           "rmc_abi_layout"]
+           "rmc_abi_layout", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes"]
 
 _lib = None
 
@@ -80,6 +80,9 @@ def lib():
     L.rmc_version.restype = ctypes.c_char_p
     L.rmc_levels.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), c_int]
     L.rmc_abi_layout.argtypes = [ctypes.POINTER(ctypes.c_uint64), c_int]
+    L.rmc_model_set_next.argtypes = [P, ctypes.c_char_p]
+    L.rmc_model_next.argtypes = [P, ctypes.c_char_p, c_size_t]
+    L.rmc_tla_hashes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_size_t]
     L.rmc_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                     ctypes.POINTER(Result)]
@@ -175,6 +178,18 @@ class Model:
         if r.status in (1, 2):
             out["trace"] = self.trace()
         return out
+
+    def set_next(self, disjuncts):
+        """Next as operator names of the spec family's definitions, in order
+        (rmc_model_set_next: the TLA+ front end's lowering of such a Next)."""
+        if lib().rmc_model_set_next(self._h, ",".join(disjuncts).encode()) != 0:
+            raise RaftmcError(lib().rmc_last_error().decode())
+
+    def next(self):
+        """The model's Next, as the library's operator names in order."""
+        buf = ctypes.create_string_buffer(4096)
+        lib().rmc_model_next(self._h, buf, len(buf))
+        return buf.value.decode().split(",")
 
     def check(self, **kw):
         """Run the model check on this process's GPU; returns a dict of TLC's results."""
@@ -314,6 +329,26 @@ def comm_unique_id():
 
 def check_text(module, cfg_text, **kw):
     return Model(module=module, cfg_text=cfg_text).check(**kw)
+
+
+def tla_hashes(text):
+    """The TLA+ front end's closure hash of every definition of a module text
+    (rmc_tla_hashes): {name: hash}, plus "#module" and "#vars"."""
+    buf = ctypes.create_string_buffer(1 << 20)
+    n = lib().rmc_tla_hashes(text.encode(), buf, len(buf))
+    if n < 0:
+        raise RaftmcError(buf.value.decode())
+    out = {}
+    for line in buf.value.decode().splitlines():
+        if line.startswith("#unparsed"):
+            out.setdefault("#unparsed", []).append(line.split()[1])
+        elif line.startswith("#"):
+            k, v = line.split(None, 1)
+            out[k] = v
+        else:
+            k, v = line.split()
+            out[k] = v
+    return out
 
 
 def abi_layout():

@@ -201,3 +201,37 @@ EXTRAS = [
     ("flex_n3v1e2_q1_lm", "FlexibleRaft", dict(n=3, v=1, E=2, ElectionQuorumSize=1, ReplicationQuorumSize=1),
      ("LogMatching", "LeaderCompleteness", "StateMachineSafety")),
 ]
+
+# The TLA+ front end (raft-tlaplus_amd/csrc/rmc_tla.cpp):
+# modules whose Next differs from the reference's -- reordered, reduced, or
+# with the network actions Raft.tla:540-541 leaves commented out -- lowered
+# onto the action library.  (name, module, kwargs, Next as operator names,
+# max_depth: 0 = exhaustive; DuplicateMessage makes the state space infinite,
+# "There is no state-space control for this action", Raft.tla:509-511).
+NEXT_RAFT = ("Restart", "RequestVote", "BecomeLeader", "ClientRequest", "AdvanceCommitIndex", "AppendEntries",
+             "UpdateTerm", "HandleRequestVoteRequest", "HandleRequestVoteResponse", "RejectAppendEntriesRequest",
+             "AcceptAppendEntriesRequest", "HandleAppendEntriesResponse")
+NEXT_FSYNC = ("Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest", "AdvanceCommitIndex",
+              "AppendEntries", "AdvanceFsyncIndex", "UpdateTerm", "HandleRequestVoteRequest",
+              "HandleRequestVoteResponse", "RejectAppendEntriesRequest", "AcceptAppendEntriesRequest",
+              "HandleAppendEntriesResponse")
+NEXT_PULL = ("Restart", "UpdateTerm", "RequestVote", "HandleRequestVoteRequest", "HandleRequestVoteResponse",
+             "BecomeLeader", "ClientRequest", "RejectPullEntriesRequest", "AcceptPullEntriesRequest",
+             "LearnOfLeader", "SendPullEntriesRequest", "HandleSuccessPullEntriesResponse",
+             "HandleFailPullEntriesResponse")
+FRONTEND = [
+    ("raft_dup_n3v1e2", "Raft", dict(n=3, v=1, E=2), NEXT_RAFT + ("DuplicateMessage",), 8),
+    ("raft_dupdrop_n3v1e1", "Raft", dict(n=3, v=1, E=1), NEXT_RAFT + ("DuplicateMessage", "DropMessage"), 8),
+    ("raft_drop_n3v1e1", "Raft", dict(n=3, v=1, E=1), NEXT_RAFT + ("DropMessage",), 0),
+    ("raft_reversed_n3v1e1", "Raft", dict(n=3, v=1, E=1), tuple(reversed(NEXT_RAFT)), 0),
+    # reversed Next with same-level hidden-variable collisions: TLC's winner order changes
+    ("raft_reversed_n2v2e2r1", "Raft", dict(n=2, v=2, E=2, R=1), tuple(reversed(NEXT_RAFT)), 0),
+    ("raft_no_restart_drop_n2v1e2", "Raft", dict(n=2, v=1, E=2, R=1),
+     tuple(d for d in NEXT_RAFT if d != "Restart") + ("DropMessage",), 0),
+    ("raft_no_hrvresp_n3v1e1", "Raft", dict(n=3, v=1, E=1), tuple(d for d in NEXT_RAFT if d != "HandleRequestVoteResponse"), 0),
+    ("flex_dup_n3v1e1", "FlexibleRaft", dict(n=3, v=1, E=1, ElectionQuorumSize=2, ReplicationQuorumSize=2),
+     ("DuplicateMessage",) + NEXT_RAFT, 7),
+    ("fsync_dropdup_n2v1e1r1", "RaftFsync", dict(n=2, v=1, E=1, R=1), NEXT_FSYNC + ("DropMessage", "DuplicateMessage"), 8),
+    ("pull_dup_n3v1e1", "PullRaft", dict(n=3, v=1, E=1), NEXT_PULL + ("DuplicateMessage",), 8),
+    ("pull2_drop_reversed_n3v1e1", "PullRaftVariant2", dict(n=3, v=1, E=1), tuple(reversed(NEXT_PULL)) + ("DropMessage",), 0),
+]

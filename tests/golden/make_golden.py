@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import (EXTRAS, FLEX_RESTART, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
+from cfgs import (EXTRAS, FLEX_RESTART, FRONTEND, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
                   VARIANT2_N5, VARIANT2_SMALL, cfg_text)
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
@@ -244,7 +244,28 @@ def extras():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def frontend():
+    """--frontend: modules whose Next the TLA+ front end lowers differently from
+    the reference's (cfgs.FRONTEND), by the Python oracle with the same Next
+    (every level, hidden-variable collisions; max_depth-truncated where
+    DuplicateMessage makes the space infinite).  The C oracle has no
+    configurable Next, so these are pinned by the Python oracle alone."""
+    out = {}
+    for name, module, kw, nxt, md in FRONTEND:
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        p = bfs(make_spec(module, cfg, next_order=nxt), max_depth=md or None)
+        out[name] = dict(module=module, cfg=txt, next=list(nxt), max_depth=md, generated=p.generated,
+                         distinct=p.distinct, depth=p.depth, status=p.status, levels=[list(x) for x in p.levels],
+                         hidden_same_level=p.hidden_same_level, max_msgs=p.max_msgs, pinned_by="pyoracle")
+        print(name, p.generated, p.distinct, p.depth, p.status, p.hidden_same_level, "%.1fs" % p.seconds, flush=True)
+    with open(os.path.join(HERE, "frontend.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--frontend" in sys.argv:
+        return frontend()
     if "--extras" in sys.argv:
         return extras()
     if "--ladders" in sys.argv:

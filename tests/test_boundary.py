@@ -42,15 +42,17 @@ def test_reference_cfg_same_first_levels(name):
 
 
 def test_edited_spec_is_refused(tmp_path):
-    """Raft with DuplicateMessage re-enabled in Next (Raft.tla:540) is a
-    different spec: refused with a message, not checked as the built-in one."""
+    """Raft with an action whose body computes something else (Restart gated
+    on restartCtr <= MaxRestarts instead of <, Raft.tla:227) is a different
+    spec: refused with a message naming the action, not checked as the
+    built-in one.  (Re-enabling the commented-out DuplicateMessage disjunct,
+    Raft.tla:540, is lowered instead: tests/test_frontend.py.)"""
     txt = open(ref("Raft", ".tla")).read()
-    edited = txt.replace("\\*        \\/ \\E m \\in DOMAIN messages : DuplicateMessage(m)",
-                         "        \\/ \\E m \\in DOMAIN messages : DuplicateMessage(m)")
+    edited = txt.replace("    /\\ restartCtr < MaxRestarts\n", "    /\\ restartCtr <= MaxRestarts\n")
     assert edited != txt
     p = tmp_path / "Raft.tla"
     p.write_text(edited)
-    with pytest.raises(raftmc.RaftmcError, match="not the reference spec"):
+    with pytest.raises(raftmc.RaftmcError, match="Next disjunct Restart"):
         raftmc.Model(str(p), ref("Raft", ".cfg"))
 
 

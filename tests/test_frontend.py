@@ -1,0 +1,237 @@
+"""The TLA+ front end (raft-tlaplus_amd/csrc/rmc_tla.cpp).
+
+CPU tests.  (1) The parser and closure hashes on small modules written here:
+layout, comments, bound-variable names, record field order and helper names do
+not change a definition's hash; what it computes does.  (2) Next lowered from
+an operator list (rmc_model_set_next, the front end's output form) through
+the CPU engine equals the Python oracle with the same Next
+(tests/golden/frontend.json).  (3) On the reference modules, edited in memory
+(skipped where /root/reference is not mounted -- it never is on the GPU box):
+the front end lowers each reference module to exactly its built-in action
+table, lowers re-enabled DuplicateMessage / DropMessage (Raft.tla:540-541)
+and a reordered Next, accepts renamed helpers and another module name, and
+refuses an action whose body computes something else, naming it."""
+import json
+import os
+import re
+
+import pytest
+
+import raftmc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FRONTEND = json.load(open(os.path.join(HERE, "golden", "frontend.json")))
+SHIPPED = json.load(open(os.path.join(HERE, "golden", "shipped.json")))
+REF = "/root/reference/specifications"
+SPECS = {"Raft": "standard-raft", "FlexibleRaft": "flexible-raft", "PullRaft": "pull-raft",
+         "RaftFsync": "raft-and-fsync", "PullRaftVariant2": "pull-raft", "KRaft": "pull-raft"}
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference not mounted")
+
+TOY = """---- MODULE Toy ----
+EXTENDS Naturals, Sequences
+CONSTANTS S, Nil
+VARIABLES x, y, q
+Helper(a) == a + 1
+Init == /\\ x = [i \\in S |-> 0]
+        /\\ y = {}
+        /\\ q = <<>>
+Inc(i) == /\\ x' = [x EXCEPT ![i] = Helper(@)]
+          /\\ UNCHANGED <<y, q>>
+Put(i) == LET r == [src |-> i, val |-> x[i]]
+          IN  /\\ q' = Append(q, r)
+              /\\ y' = y \\cup {i}
+              /\\ UNCHANGED x
+Pick == /\\ q /= <<>>
+        /\\ \\/ /\\ Head(q).val > 1
+              /\\ y' = {}
+           \\/ /\\ Head(q).val <= 1
+              /\\ y' = y \\ {Head(q).src}
+        /\\ q' = Tail(q)
+        /\\ UNCHANGED x
+Low == CHOOSE v \\in {x[i] : i \\in S} : \\A w \\in {x[i] : i \\in S} : v <= w
+Next == \\/ \\E i \\in S : Inc(i)
+        \\/ \\E i \\in S : Put(i)
+        \\/ Pick
+Spec == Init /\\ [][Next]_<<x, y, q>>
+====
+"""
+
+
+def h(text):
+    return raftmc.tla_hashes(text)
+
+
+def test_toy_parses_and_temporal_is_set_aside():
+    t = h(TOY)
+    assert t["#module"] == "Toy"
+    for d in ("Helper", "Init", "Inc", "Put", "Pick", "Low", "Next"):
+        assert d in t, d
+    assert t["#unparsed"] == ["Spec"]
+
+
+def test_layout_comments_and_bound_names_do_not_matter():
+    base = h(TOY)
+    alt = TOY.replace("Inc(i) == /\\ x' = [x EXCEPT ![i] = Helper(@)]\n          /\\ UNCHANGED <<y, q>>",
+                      "(* a comment *)\nInc(k) == x' = [x EXCEPT ![k] = Helper(@)] /\\ UNCHANGED <<y, q>> \\* inline")
+    alt = alt.replace("[src |-> i, val |-> x[i]]", "[val |-> x[i], src |-> i]")  # record field order
+    alt = alt.replace("CHOOSE v \\in", "CHOOSE u \\in").replace(": v <= w", ": u <= w")
+    a = h(alt)
+    for d in ("Inc", "Put", "Low", "Next"):
+        assert a[d] == base[d], d
+
+
+def test_helper_renamed_keeps_the_callers_hash():
+    a = h(TOY.replace("Helper", "Successor"))
+    assert a["Inc"] == h(TOY)["Inc"] and a["Next"] == h(TOY)["Next"]
+
+
+def test_what_an_action_computes_changes_its_hash():
+    base = h(TOY)
+    assert h(TOY.replace("a + 1", "a + 2"))["Inc"] != base["Inc"]          # through the helper
+    assert h(TOY.replace("Head(q).val > 1", "Head(q).val > 2"))["Pick"] != base["Pick"]
+    assert h(TOY.replace("y \\cup {i}", "y \\cup {x[i]}"))["Put"] != base["Put"]
+
+
+def test_junction_lists_follow_their_columns():
+    """(p /\\ q) \\/ r laid out as bullets equals the inline form and differs
+    from p /\\ (q \\/ r): the item extent is decided by the bullet column."""
+    mod = "---- MODULE J ----\nVARIABLE p, q, r\n%s\n====\n"
+    bullets = h(mod % "A == \\/ /\\ p\n        /\\ q\n     \\/ r")["A"]
+    inline = h(mod % "A == (p /\\ q) \\/ r")["A"]
+    other = h(mod % "A == /\\ p\n     /\\ \\/ q\n        \\/ r")["A"]
+    assert bullets == inline != other
+    assert h(mod % "A == p /\\ (q \\/ r)")["A"] == other
+
+
+def model(g):
+    m = raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+    m.set_next(g["next"])
+    return m
+
+
+@pytest.mark.parametrize("name", sorted(FRONTEND))
+def test_lowered_next_cpu_engine_equals_oracle(name):
+    g = FRONTEND[name]
+    m = model(g)
+    assert m.next() == g["next"]
+    r = m.check_cpu(workers=8, max_depth=g["max_depth"])
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (
+        g["generated"], g["distinct"], g["depth"], g["status"])
+    assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+def test_set_next_refuses_unknown_actions():
+    m = raftmc.Model(module="Raft", cfg_text=FRONTEND["raft_dup_n3v1e2"]["cfg"])
+    with pytest.raises(raftmc.RaftmcError, match="no action Timeout"):
+        m.set_next(["Restart", "Timeout"])
+
+
+# ---------------------------------------------------------------- reference modules
+def ref_text(module):
+    return open(os.path.join(REF, SPECS[module], module + ".tla")).read()
+
+
+def load(tmp_path, text, cfg, module="Raft"):
+    p = tmp_path / (module + ".tla")
+    p.write_text(text)
+    c = tmp_path / (module + ".cfg")
+    c.write_text(cfg)
+    return raftmc.Model(str(p), str(c))
+
+
+def add_unused(text):
+    """A semantics-preserving edit that changes the file's hash: the module
+    then goes through the front end instead of the verbatim-text check."""
+    i = text.rindex("====")
+    return text[:i] + "\nFrontEndProbe == 42\n" + text[i:]
+
+
+@needs_ref
+@pytest.mark.parametrize("module", sorted(SPECS))
+def test_front_end_lowers_each_reference_module_to_its_builtin_table(tmp_path, module):
+    cfg = open(os.path.join(REF, SPECS[module], module + ".cfg")).read()
+    fe = load(tmp_path, add_unused(ref_text(module)), cfg, module)
+    builtin = raftmc.Model(module=module, cfg_text=cfg)
+    assert fe.next() == builtin.next()
+
+
+@needs_ref
+def test_front_end_reference_raft_counts(tmp_path):
+    g = SHIPPED["Raft_cfg"]
+    cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
+    r = load(tmp_path, add_unused(ref_text("Raft")), cfg).check_cpu(workers=8, max_depth=16)
+    assert r["levels"] == g["levels"][:16]
+
+
+def enable_network(text, dup=True, drop=False):
+    if dup:
+        text = text.replace("\\*        \\/ \\E m \\in DOMAIN messages : DuplicateMessage(m)",
+                            "        \\/ \\E m \\in DOMAIN messages : DuplicateMessage(m)")
+    if drop:
+        text = text.replace("\\*        \\/ \\E m \\in DOMAIN messages : DropMessage(m)",
+                            "        \\/ \\E m \\in DOMAIN messages : DropMessage(m)")
+    return text
+
+
+@needs_ref
+@pytest.mark.parametrize("name,dup,drop", [("raft_dup_n3v1e2", True, False), ("raft_dupdrop_n3v1e1", True, True),
+                                           ("raft_drop_n3v1e1", False, True)])
+def test_reenabled_network_actions_are_checked(tmp_path, name, dup, drop):
+    """Raft.tla with DuplicateMessage / DropMessage re-enabled in Next
+    (Raft.tla:540-541) is lowered, not refused, and gives the Python oracle's
+    counts with those disjuncts added."""
+    g = FRONTEND[name]
+    text = enable_network(ref_text("Raft"), dup, drop)
+    assert text != ref_text("Raft")
+    m = load(tmp_path, text, g["cfg"])
+    assert m.next() == g["next"]
+    r = m.check_cpu(workers=8, max_depth=g["max_depth"])
+    assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (
+        g["generated"], g["distinct"], g["depth"], g["levels"])
+
+
+def next_block(text):
+    m = re.search(r"\nNext == *\n((?:[ \t]+\\/[^\n]*\n)+)", text)
+    return m, [l for l in m.group(1).splitlines() if l.strip()]
+
+
+@needs_ref
+def test_reordered_next_follows_the_module_order(tmp_path):
+    text = ref_text("Raft")
+    m, lines = next_block(text)
+    text2 = text[:m.start(1)] + "\n".join(reversed(lines)) + "\n" + text[m.end(1):]
+    g = FRONTEND["raft_reversed_n3v1e1"]
+    mod = load(tmp_path, text2, g["cfg"])
+    assert mod.next() == g["next"]
+    r = mod.check_cpu(workers=8)
+    assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (
+        g["generated"], g["distinct"], g["depth"], g["levels"])
+
+
+@needs_ref
+def test_renamed_helpers_and_module_are_accepted(tmp_path):
+    text = ref_text("Raft").replace("LastTerm", "LastLogTerm").replace("MODULE Raft", "MODULE MyRaft")
+    cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
+    m = load(tmp_path, text, cfg, module="MyRaft")
+    assert m.next() == raftmc.Model(module="Raft", cfg_text=cfg).next()
+
+
+@needs_ref
+def test_changed_action_is_refused_by_name(tmp_path):
+    text = ref_text("Raft")
+    edited = text.replace("    /\\ electionCtr < MaxElections \n", "    /\\ electionCtr <= MaxElections \n")
+    assert edited != text
+    cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
+    with pytest.raises(raftmc.RaftmcError, match="RequestVote"):
+        load(tmp_path, edited, cfg)
+
+
+@needs_ref
+def test_changed_binding_is_refused(tmp_path):
+    text = ref_text("Raft").replace("AppendEntries(i, j)\n        \\/ UpdateTerm",
+                                    "AppendEntries(j, i)\n        \\/ UpdateTerm")
+    assert text != ref_text("Raft")
+    cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
+    with pytest.raises(raftmc.RaftmcError, match="form the lowering does not bind"):
+        load(tmp_path, text, cfg)
