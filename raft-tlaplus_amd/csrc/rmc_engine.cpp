@@ -815,14 +815,23 @@ struct Arena {
   // table/table2: the fingerprint set and its growth target
   DevBuf table, table2, cslot, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   DevBuf hwin_in[2], hwin_out[2];  // host-frontier windows: parents in, new rows out (double-buffered)
+  // compact host rows (per window parity): out = pack side, in = unpack side
+  DevBuf hf_pack[2], hf_olen32[2], hf_olen8[2], hf_ooff[2], hf_oscan[2];
+  DevBuf hf_stage[2], hf_ilen32[2], hf_ilen8[2], hf_ioff[2], hf_iscan[2];
+  void release_hf() {
+    for (int k = 0; k < 2; k++)
+      for (DevBuf* b : {&hwin_in[k], &hwin_out[k], &hf_pack[k], &hf_olen32[k], &hf_olen8[k], &hf_ooff[k], &hf_oscan[k],
+                        &hf_stage[k], &hf_ilen32[k], &hf_ilen8[k], &hf_ioff[k], &hf_iscan[k]})
+        b->release();
+  }
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   HostReadback* hrb = nullptr;
   void release() {
     if (hrb) (void)hipHostFree(hrb);
     hrb = nullptr;
-    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp,
-                      &hwin_in[0], &hwin_in[1], &hwin_out[0], &hwin_out[1]})
+    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
       b->release();
+    release_hf();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
 };
@@ -983,29 +992,22 @@ static void ckpt_read_rows(const std::string& path, uint32_t* dev, size_t n, siz
 // The same frontier file streamed straight into host-frontier pages (a level
 // that only fit on the host when the snapshot was taken): no device copy.
 static void ckpt_read_rows_host(const std::string& path, HostLevel& h, HostPagePool& pool, size_t n, size_t w0,
-                                size_t w) {
+                                int hdr_words) {
+  // the snapshot's rows (w0 words each) compacted on the way into the pages;
+  // the compact form does not depend on the row width, so a resumed level
+  // with more message slots unpacks them zero-padded
   FILE* f = fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("recover: cannot read " + path);
   fseek(f, 0, SEEK_END);
   if ((size_t)ftell(f) != n * w0 * 4) { fclose(f); throw std::runtime_error("recover: " + path + " has the wrong size"); }
   fseek(f, 0, SEEK_SET);
-  h.reserve(n, pool);
-  std::vector<uint32_t> in(w0);
-  for (size_t r0 = 0; r0 < n;) {
-    const size_t k = std::min<size_t>(h.page_rows - r0 % h.page_rows, n - r0);
-    uint32_t* dst = const_cast<uint32_t*>(h.row(r0));
-    if (w == w0) {
-      if (fread(dst, 4, k * w, f) != k * w) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
-    } else {
-      for (size_t r = 0; r < k; r++) {
-        if (fread(in.data(), 4, w0, f) != w0) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
-        memcpy(dst + r * w, in.data(), w0 * 4);
-        memset(dst + r * w + w0, 0, (w - w0) * 4);
-      }
-    }
-    r0 += k;
+  const size_t batch = 1 << 16;
+  std::vector<uint32_t> in(batch * w0);
+  for (size_t r0 = 0; r0 < n; r0 += batch) {
+    const size_t k = std::min(batch, n - r0);
+    if (fread(in.data(), 4, k * w0, f) != k * w0) { fclose(f); throw std::runtime_error("recover: short read from " + path); }
+    h.append_fixed_host(in.data(), k, w0, hdr_words, pool);
   }
-  h.rows = n;
   fclose(f);
 }
 // Every snap-* subdirectory of dir but `keep` (an interrupted rotation, or a
@@ -1079,36 +1081,38 @@ size_t host_frontier_limit() {
 // The copy streams and events of the host frontier, created on first use:
 // parents in (H2D) on `cs`, new rows out (D2H) on `co`, so the two directions
 // of the PCIe link run at once instead of queueing behind each other.
+// The compact rows are packed on `cp` (after the chunk's k_materialize:
+// event mat; packed = the output window is free again), then copied out on
+// `co` (event out = the pack buffer is free again).
 struct HostFrontierStreams {
-  hipStream_t cs = nullptr, co = nullptr;
-  hipEvent_t in[2], mat[2], out[2];
+  hipStream_t cs = nullptr, co = nullptr, cp = nullptr;
+  hipEvent_t in[2], mat[2], out[2], packed[2];
   void init(hipStream_t compute) {
     if (cs) return;
     HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&co, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&cp, hipStreamNonBlocking));
     for (int k = 0; k < 2; k++) {
-      HIPCHK(hipEventCreateWithFlags(&in[k], hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&mat[k], hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&out[k], hipEventDisableTiming));
-      HIPCHK(hipEventRecord(in[k], compute));
-      HIPCHK(hipEventRecord(mat[k], compute));
-      HIPCHK(hipEventRecord(out[k], compute));
+      for (hipEvent_t* e : {&in[k], &mat[k], &out[k], &packed[k]}) {
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(*e, compute));
+      }
     }
   }
   void sync() {
     if (!cs) return;
     HIPCHK(hipStreamSynchronize(cs));
+    HIPCHK(hipStreamSynchronize(cp));
     HIPCHK(hipStreamSynchronize(co));
   }
   ~HostFrontierStreams() {
     if (!cs) return;
     (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(cp);
     (void)hipStreamSynchronize(co);
-    for (int k = 0; k < 2; k++) {
-      (void)hipEventDestroy(in[k]);
-      (void)hipEventDestroy(mat[k]);
-      (void)hipEventDestroy(out[k]);
-    }
+    for (int k = 0; k < 2; k++)
+      for (hipEvent_t e : {in[k], mat[k], out[k], packed[k]}) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(cp);
     (void)hipStreamDestroy(co);
     (void)hipStreamDestroy(cs);
   }
@@ -1352,8 +1356,8 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   if (const char* e = getenv("RMC_HF_PIN_THREADS")) hf_pin_threads = atoi(e);
   if (const char* e = getenv("RMC_HF_PIN_AHEAD")) hf_pin_ahead = (size_t)atoll(e);
   HostLevel hcur, hnxt;
-  hcur.init(page_rows, row_bytes);
-  hnxt.init(page_rows, row_bytes);
+  hcur.init(pool.page_bytes, row_bytes);
+  hnxt.init(pool.page_bytes, row_bytes);
   struct LevelPagesGuard {  // every exit path returns the levels' pages to the pool (freed with it)
     HostLevel &a, &b;
     HostPagePool& pool;
@@ -1376,23 +1380,116 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     Arena& A;
     bool& windows;
     ~WindowsGuard() {
-      if (windows)
-        for (DevBuf* b : {&A.hwin_in[0], &A.hwin_in[1], &A.hwin_out[0], &A.hwin_out[1]}) b->release();
+      if (windows) A.release_hf();
     }
   } windows_guard{A, windows};
+  // ---- compact host rows (HostLevel): pack before D2H, unpack after H2D
+  const int hdr_words = 1 + 4 * M.N;
+  auto hf_ensure_out = [&](int k, unsigned long long n) {
+    A.hf_pack[k].ensure(std::max<size_t>(n * W * 4, 16));
+    A.hf_olen32[k].ensure(std::max<size_t>(n * 4, 16));
+    A.hf_olen8[k].ensure(std::max<size_t>(n, 16));
+    A.hf_ooff[k].ensure(std::max<size_t>(n * 4, 16));
+    A.hf_oscan[k].ensure(std::max<size_t>(scan_temp_bytes(n), 16));
+  };
+  auto hf_ensure_in = [&](int k, unsigned long long n) {
+    A.hf_stage[k].ensure(std::max<size_t>(n * W * 4, 16));
+    A.hf_ilen32[k].ensure(std::max<size_t>(n * 4, 16));
+    A.hf_ilen8[k].ensure(std::max<size_t>(n, 16));
+    A.hf_ioff[k].ensure(std::max<size_t>(n * 4, 16));
+    A.hf_iscan[k].ensure(std::max<size_t>(scan_temp_bytes(n), 16));
+  };
+  // rows [r0, r0 + n) of a host level -> fixed-stride rows at dev (on stream st, with input buffers k)
+  auto hf_load = [&](const HostLevel& h, unsigned long long r0, unsigned long long n, void* dev, int k,
+                     hipStream_t st) {
+    if (!n) return;
+    hf_ensure_in(k, n);
+    const unsigned long long b0 = h.byte_of(r0), b1 = h.byte_of(r0 + n);
+    h.copy_in(b0, b1 - b0, A.hf_stage[k].p, st);
+    HIPCHK(hipMemcpyAsync(A.hf_ilen8[k].p, h.lens.data() + r0, n, hipMemcpyHostToDevice, st));
+    launch_widen_lens(A.hf_ilen8[k].as<uint8_t>(), n, A.hf_ilen32[k].as<uint32_t>(), st);
+    launch_scan(A.hf_iscan[k].p, A.hf_iscan[k].bytes, A.hf_ilen32[k].as<uint32_t>(), A.hf_ioff[k].as<uint32_t>(), n,
+                st);
+    launch_unpack_rows(A.hf_stage[k].as<uint32_t>(), n, (int)W, A.hf_ioff[k].as<uint32_t>(),
+                       A.hf_ilen32[k].as<uint32_t>(), (uint32_t*)dev, st);
+    HIPCHK(hipGetLastError());
+  };
+  // n fixed rows on the device -> appended to a host level (synchronous, in slices; the switch to the host)
+  auto hf_from_device = [&](HostLevel& h, const uint32_t* rows, unsigned long long n) {
+    if (!n) return;
+    DevBuf local[5];
+    const bool have = A.hf_pack[0].p != nullptr;
+    unsigned long long S = have ? A.hf_pack[0].bytes / (W * 4) : std::max<unsigned long long>(1, (256ULL << 20) / (W * 4));
+    S = std::max<unsigned long long>(1, std::min<unsigned long long>(S, 1ULL << 24));
+    DevBuf& pk = have ? A.hf_pack[0] : local[0];
+    DevBuf& l32 = have ? A.hf_olen32[0] : local[1];
+    DevBuf& l8 = have ? A.hf_olen8[0] : local[2];
+    DevBuf& off = have ? A.hf_ooff[0] : local[3];
+    DevBuf& sc = have ? A.hf_oscan[0] : local[4];
+    pk.ensure(S * W * 4);
+    l32.ensure(S * 4);
+    l8.ensure(S);
+    off.ensure(S * 4);
+    sc.ensure(std::max<size_t>(scan_temp_bytes(S), 16));
+    std::vector<uint8_t> l;
+    for (unsigned long long r = 0; r < n; r += S) {
+      const unsigned long long k = std::min(S, n - r);
+      launch_row_words(rows + r * W, k, (int)W, hdr_words, l32.as<uint32_t>(), l8.as<uint8_t>(), stream);
+      launch_scan(sc.p, sc.bytes, l32.as<uint32_t>(), off.as<uint32_t>(), k, stream);
+      launch_pack_rows(rows + r * W, k, (int)W, off.as<uint32_t>(), l32.as<uint32_t>(), pk.as<uint32_t>(), stream);
+      HIPCHK(hipGetLastError());
+      l.resize(k);
+      HIPCHK(hipMemcpyAsync(l.data(), l8.p, k, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      h.append_dev(l.data(), k, pk.p, stream, pool);
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+  };
+  // the chunk's new rows (output window k, n rows) are packed on cp after its
+  // k_materialize; their bytes are appended to hnxt at the next host sync
+  // point (hf_flush), when the compact sizes are known
+  struct PendingOut { bool on; int k; unsigned long long n; } hf_pend{false, 0, 0};
+  auto hf_pack_async = [&](int k, unsigned long long n) {
+    hf_ensure_out(k, n);
+    HIPCHK(hipStreamWaitEvent(hs.cp, hs.mat[k], 0));  // the rows are written
+    HIPCHK(hipStreamWaitEvent(hs.cp, hs.out[k], 0));  // the pack buffer's last copy-out is done
+    launch_row_words(A.hwin_out[k].as<uint32_t>(), n, (int)W, hdr_words, A.hf_olen32[k].as<uint32_t>(),
+                     A.hf_olen8[k].as<uint8_t>(), hs.cp);
+    launch_scan(A.hf_oscan[k].p, A.hf_oscan[k].bytes, A.hf_olen32[k].as<uint32_t>(), A.hf_ooff[k].as<uint32_t>(), n,
+                hs.cp);
+    launch_pack_rows(A.hwin_out[k].as<uint32_t>(), n, (int)W, A.hf_ooff[k].as<uint32_t>(),
+                     A.hf_olen32[k].as<uint32_t>(), A.hf_pack[k].as<uint32_t>(), hs.cp);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(hs.packed[k], hs.cp));
+    hf_pend = {true, k, n};
+  };
+  std::vector<uint8_t> hf_lens_tmp;
+  auto hf_flush = [&]() {
+    if (!hf_pend.on) return;
+    hf_pend.on = false;
+    HIPCHK(hipEventSynchronize(hs.packed[hf_pend.k]));
+    hf_lens_tmp.resize(hf_pend.n);
+    HIPCHK(hipMemcpy(hf_lens_tmp.data(), A.hf_olen8[hf_pend.k].p, hf_pend.n, hipMemcpyDeviceToHost));
+    hnxt.append_dev(hf_lens_tmp.data(), hf_pend.n, A.hf_pack[hf_pend.k].p, hs.co, pool);
+    HIPCHK(hipEventRecord(hs.out[hf_pend.k], hs.co));
+  };
   auto reserve_windows = [&]() {
     if (windows) return;
     A.hwin_in[0].ensure(win_in_bytes);
     A.hwin_in[1].ensure(win_in_bytes);
     A.hwin_out[0].ensure(win_out_bytes);
     A.hwin_out[1].ensure(win_out_bytes);
+    for (int k = 0; k < 2; k++) {  // the compact-row buffers (pack out, unpack in)
+      hf_ensure_out(k, 3 * chunk);
+      hf_ensure_in(k, chunk);
+    }
     windows = true;
   };
   auto before_growth = [&](size_t request) {  // auto mode: keep the windows' HBM available
     if (hf || windows || hf_opt != 0) return;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return;
-    const size_t wb = 2 * (win_in_bytes + win_out_bytes);
+    const size_t wb = 4 * (win_in_bytes + win_out_bytes);  // windows + the compact-row buffers
     if (fr < request + wb + (2ULL << 30)) {
       try {
         reserve_windows();
@@ -1414,13 +1511,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     }
     hs.init(stream);
     pool.start_fillers(hf_pin_ahead, hf_pin_threads);
-    hcur.init(page_rows, row_bytes);
-    hnxt.init(page_rows, row_bytes);
-    hcur.reserve(cur_n, pool);
-    hcur.d2h_append(cur, cur_n, hs.co);
-    hnxt.reserve(lvl_next_n, pool);
-    hnxt.d2h_append(nxt, lvl_next_n, hs.co);
-    HIPCHK(hipStreamSynchronize(hs.co));
+    hcur.init(pool.page_bytes, row_bytes);
+    hnxt.init(pool.page_bytes, row_bytes);
+    hf_from_device(hcur, cur, cur_n);
+    hf_from_device(hnxt, nxt, lvl_next_n);
     if (lvl_c0 > chunk) hcur.recycle_below(lvl_c0 - chunk, pool);
     fa.release();
     fb.release();
@@ -1524,10 +1618,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     reserve_windows();
     hs.init(stream);
     pool.start_fillers(hf_pin_ahead, hf_pin_threads);
-    hcur.init(page_rows, row_bytes);
-    hnxt.init(page_rows, row_bytes);
+    hcur.init(pool.page_bytes, row_bytes);
+    hnxt.init(pool.page_bytes, row_bytes);
     ckpt_read_rows_host(std::string(opt->recover_dir) + "/" + ckpt_subdir(rc.seq) + "/frontier.bin", hcur, pool,
-                        rc.cur_n, snap_words, W);
+                        rc.cur_n, snap_words, 1 + 4 * M.N);
     fa.release();
     fb.release();
     cur = nxt = nullptr;
@@ -1623,7 +1717,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       const int hs_k = ck & 1;  // host frontier: this chunk's windows
       if (hf && hwin_c0[hs_k] != c0) {  // parents not prefetched: copy them in (window free after chunk ck-2)
         HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k], 0));
-        hcur.h2d(c0, n, A.hwin_in[hs_k].p, hs.cs);
+        hf_load(hcur, c0, n, A.hwin_in[hs_k].p, hs_k, hs.cs);
         HIPCHK(hipEventRecord(hs.in[hs_k], hs.cs));
         hwin_c0[hs_k] = c0;
       }
@@ -1644,7 +1738,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
         // prefetch the next chunk's parents into the other window once chunk
         // ck-1's k_materialize (which re-reads that window) is done
         HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k ^ 1], 0));
-        hcur.h2d(c0 + n, std::min(chunk, cur_n - c0 - n), A.hwin_in[hs_k ^ 1].p, hs.cs);
+        hf_load(hcur, c0 + n, std::min(chunk, cur_n - c0 - n), A.hwin_in[hs_k ^ 1].p, hs_k ^ 1, hs.cs);
         HIPCHK(hipEventRecord(hs.in[hs_k ^ 1], hs.cs));
         hwin_c0[hs_k ^ 1] = c0 + n;
       }
@@ -1654,6 +1748,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       HIPCHK(hipMemcpyAsync(&hrb->lastwin, a.par_win + (n - 1), 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&hrb->st, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
+      if (hf) hf_flush();  // the previous chunk's compact rows go out now that their sizes are known
       // the previous chunk's k_materialize outcome first: if it stopped the
       // search, this chunk's expand never happened as far as the counts go
       if (mat_pending && finish_mat()) break;
@@ -1754,7 +1849,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
           // parents (k_materialize re-reads them) go to its input window
           lvl_next_n = next_n;
           enter_hf();
-          hcur.h2d(c0, n, A.hwin_in[hs_k].p, hs.cs);
+          hf_load(hcur, c0, n, A.hwin_in[hs_k].p, hs_k, hs.cs);
           HIPCHK(hipStreamSynchronize(hs.cs));
           hwin_c0[hs_k] = c0;
           a.frontier = A.hwin_in[hs_k].as<uint32_t>();
@@ -1764,10 +1859,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
         // output window hs_k: free once chunk ck-2's rows have left it
         const size_t need = (size_t)W_chunk * W * 4;
         if (A.hwin_out[hs_k].bytes < need) {
-          HIPCHK(hipEventSynchronize(hs.out[hs_k]));
+          HIPCHK(hipEventSynchronize(hs.packed[hs_k]));
           A.hwin_out[hs_k].ensure(need + need / 4);
         }
-        HIPCHK(hipStreamWaitEvent(stream, hs.out[hs_k], 0));
+        HIPCHK(hipStreamWaitEvent(stream, hs.packed[hs_k], 0));  // chunk ck-2's rows have been packed
         a.out = A.hwin_out[hs_k].as<uint32_t>();
       } else {
         a.out = nxt + next_n * W;
@@ -1783,10 +1878,8 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       HIPCHK(hipMemcpyAsync(&hrb->mat, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
       if (hf) {  // the new rows go to host pages (copy stream), after this k_materialize
         HIPCHK(hipEventRecord(hs.mat[hs_k], stream));
-        hnxt.reserve(W_chunk, pool);
-        HIPCHK(hipStreamWaitEvent(hs.co, hs.mat[hs_k], 0));
-        hnxt.d2h_append(A.hwin_out[hs_k].p, W_chunk, hs.co);
-        HIPCHK(hipEventRecord(hs.out[hs_k], hs.co));
+        hf_flush();  // (normally already flushed at this chunk's sync point)
+        hf_pack_async(hs_k, W_chunk);
         // rows below the previous chunk are consumed (the last two chunks stay
         // for the recount at a violation)
         hcur.recycle_below(prev_c0, pool);
@@ -1806,7 +1899,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       HIPCHK(hipStreamSynchronize(stream));
       finish_mat();
     }
-    if (hf) hs.sync();  // every new row is in its host page
+    if (hf) {
+      hf_flush();
+      hs.sync();  // every new row is in its host page
+    }
     const unsigned long long gen_before = generated, dist_before = distinct;
     generated += gen_lvl;
     distinct += next_n;
@@ -1883,9 +1979,11 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
         const std::string fp = sub + "/frontier.bin", tmp = fp + ".tmp";
         FILE* f = fopen(tmp.c_str(), "wb");
         if (!f) throw std::runtime_error("checkpoint: cannot write " + tmp);
-        for (unsigned long long r = 0; r < cur_n; r += page_rows) {
-          const size_t k = (size_t)std::min<unsigned long long>(page_rows, cur_n - r);
-          if (fwrite(hcur.row(r), row_bytes, k, f) != k) { fclose(f); throw std::runtime_error("checkpoint: short write"); }
+        std::vector<uint32_t> buf(std::min<unsigned long long>(cur_n, 1ULL << 16) * W);
+        for (unsigned long long r = 0; r < cur_n; r += 1ULL << 16) {  // fixed-stride rows, as a device snapshot
+          const size_t k = (size_t)std::min<unsigned long long>(1ULL << 16, cur_n - r);
+          hcur.read_fixed_host(r, k, buf.data());
+          if (fwrite(buf.data(), row_bytes, k, f) != k) { fclose(f); throw std::runtime_error("checkpoint: short write"); }
         }
         if (fflush(f) != 0 || fsync(fileno(f)) != 0 || fclose(f) != 0 || rename(tmp.c_str(), fp.c_str()) != 0)
           throw std::runtime_error("checkpoint: cannot finish " + fp);
@@ -1953,7 +2051,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       cur = const_cast<uint32_t*>(stop_front);
       cur_base = stop_level_base;
       if (stop_hf) {  // the stopped level's pages (hnxt after the swap)
-        hnxt.h2d(c0, n, A.hwin_in[0].p, stream);
+        hf_load(hnxt, c0, n, A.hwin_in[0].p, 0, stream);
         HIPCHK(hipStreamSynchronize(stream));
       }
       LevelArgs a;
@@ -2052,7 +2150,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     hcur.clear(pool);
     hnxt.clear(pool);
     pool.release();
-    for (DevBuf* b : {&A.hwin_in[0], &A.hwin_in[1], &A.hwin_out[0], &A.hwin_out[1]}) b->release();
+    A.release_hf();
     if (opt->verbose)
       fprintf(stderr, "[rmc] host frontier: %.3fs moving levels to host memory; %.3fs pinning pages (%zu MiB peak)\n", hf_copy_s,
               pool.alloc_s, hf_peak >> 20);

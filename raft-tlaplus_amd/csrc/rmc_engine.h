@@ -61,6 +61,21 @@ void launch_materialize(int spec, int N, const LevelArgs& a, hipStream_t s);
 void launch_rehash(const unsigned long long* old, unsigned long long nold, unsigned long long* nt,
                    unsigned long long nmask, DevStatus* st, hipStream_t s, int ew = 2);
 
+// compact host-frontier rows (rmc_kernels.hip): words per row (1 + 4N + nmsg), pack / unpack
+void launch_row_words(const uint32_t* rows, unsigned long long n, int W, int hdr_words, uint32_t* lens32,
+                      uint8_t* lens8, hipStream_t s);
+void launch_widen_lens(const uint8_t* lens8, unsigned long long n, uint32_t* lens32, hipStream_t s);
+void launch_pack_rows(const uint32_t* rows, unsigned long long n, int W, const uint32_t* offs, const uint32_t* lens32,
+                      uint32_t* out, hipStream_t s);
+void launch_unpack_rows(const uint32_t* in, unsigned long long n, int W, const uint32_t* offs, const uint32_t* lens32,
+                        uint32_t* rows, hipStream_t s);
+// batched device-to-device copies (one launch for a whole exchange step)
+struct CopyDesc {
+  const void* src;
+  void* dst;
+  unsigned long long bytes;
+};
+void launch_multi_copy(const CopyDesc* d, int n, unsigned long long max_bytes, hipStream_t s);
 size_t scan_temp_bytes(unsigned long long n);
 void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, unsigned long long n,
                  hipStream_t s);

@@ -2,6 +2,7 @@
 // (rmc_engine.cpp) and the sharded multi-GPU driver (rmc_sharded.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -333,41 +334,132 @@ struct HostPagePool {
   }
   ~HostPagePool() { release(); }
 };
+// A level in host memory, COMPACT: each packed row trimmed after its last
+// DOMAIN message (1 + 4N + nmsg words), rows back to back in a byte stream
+// over pinned pages (a row may straddle two pages).  lens[r] = row r's words;
+// cum[k] = byte offset of row k * IDX (a chunk's byte range is found from
+// them).  Rows are packed on the device before they cross PCIe and unpacked
+// into fixed-stride rows on the way back (rmc_kernels.hip k_pack_rows /
+// k_unpack_rows), so the kernels never see this form.
 struct HostLevel {
+  static constexpr unsigned long long IDX = 4096;
   std::vector<void*> pages;  // nullptr: recycled (its rows were consumed)
-  unsigned long long rows = 0;
-  size_t page_rows = 1, row_bytes = 4;
-  void init(size_t prow, size_t rb) { pages.clear(); rows = 0; page_rows = prow; row_bytes = rb; }
-  // copy rows [r0, r0 + n) to dev (async on stream)
-  void h2d(unsigned long long r0, unsigned long long n, void* dev, hipStream_t stream) const {
-    char* d = (char*)dev;
-    while (n) {
-      const size_t pg = r0 / page_rows, off = r0 % page_rows, k = std::min<unsigned long long>(n, page_rows - off);
-      if (pg >= pages.size() || !pages[pg]) throw std::runtime_error("host frontier: rows already recycled");
-      HIPCHK(hipMemcpyAsync(d, (char*)pages[pg] + off * row_bytes, k * row_bytes, hipMemcpyHostToDevice, stream));
-      d += k * row_bytes;
-      r0 += k;
-      n -= k;
+  size_t page_bytes = 1, row_bytes = 4;
+  unsigned long long rows = 0, bytes = 0;
+  std::vector<uint8_t> lens;
+  std::vector<unsigned long long> cum;
+  void init(size_t pbytes, size_t rb) {
+    pages.clear();
+    lens.clear();
+    cum.clear();
+    rows = bytes = 0;
+    page_bytes = pbytes;
+    row_bytes = rb;
+  }
+  unsigned long long byte_of(unsigned long long r) const {  // r <= rows
+    if (r >= rows) return bytes;
+    unsigned long long b = cum[r / IDX];
+    for (unsigned long long q = r / IDX * IDX; q < r; q++) b += 4ULL * lens[q];
+    return b;
+  }
+  void reserve_bytes(unsigned long long nb, HostPagePool& pool) {
+    while ((bytes + nb + page_bytes - 1) / page_bytes > pages.size()) pages.push_back(pool.get());
+  }
+  // record n rows of the given word counts; returns their bytes (the caller copies them in)
+  unsigned long long add_rows(const uint8_t* l, unsigned long long n) {
+    unsigned long long b = bytes, nb = 0;
+    lens.reserve(lens.size() + n);
+    for (unsigned long long q = 0; q < n; q++) {
+      if ((rows + q) % IDX == 0) cum.push_back(b + nb);
+      lens.push_back(l[q]);
+      nb += 4ULL * l[q];
     }
+    return nb;
   }
-  // reserve pages for n more rows (may allocate: call before enqueuing the copy)
-  void reserve(unsigned long long n, HostPagePool& pool) {
-    while ((rows + n + page_rows - 1) / page_rows > pages.size()) pages.push_back(pool.get());
-  }
-  // append n rows from dev (async on stream; pages reserved beforehand)
-  void d2h_append(const void* dev, unsigned long long n, hipStream_t stream) {
+  // byte stream [b0, b0 + nb) <-> a contiguous buffer (async copies, page by page)
+  void copy_out(const void* dev, unsigned long long b0, unsigned long long nb, hipStream_t stream) {
     const char* s = (const char*)dev;
-    while (n) {
-      const size_t pg = rows / page_rows, off = rows % page_rows, k = std::min<unsigned long long>(n, page_rows - off);
-      HIPCHK(hipMemcpyAsync((char*)pages[pg] + off * row_bytes, s, k * row_bytes, hipMemcpyDeviceToHost, stream));
-      s += k * row_bytes;
-      rows += k;
-      n -= k;
+    while (nb) {
+      const size_t pg = b0 / page_bytes, off = b0 % page_bytes, k = std::min<unsigned long long>(nb, page_bytes - off);
+      HIPCHK(hipMemcpyAsync((char*)pages[pg] + off, s, k, hipMemcpyDeviceToHost, stream));
+      s += k;
+      b0 += k;
+      nb -= k;
     }
   }
-  // give back the pages whose rows all lie below row r
+  void copy_in(unsigned long long b0, unsigned long long nb, void* dev, hipStream_t stream) const {
+    char* d = (char*)dev;
+    while (nb) {
+      const size_t pg = b0 / page_bytes, off = b0 % page_bytes, k = std::min<unsigned long long>(nb, page_bytes - off);
+      if (pg >= pages.size() || !pages[pg]) throw std::runtime_error("host frontier: rows already recycled");
+      HIPCHK(hipMemcpyAsync(d, (char*)pages[pg] + off, k, hipMemcpyHostToDevice, stream));
+      d += k;
+      b0 += k;
+      nb -= k;
+    }
+  }
+  void read_host(unsigned long long b0, unsigned long long nb, void* out) const {
+    char* d = (char*)out;
+    while (nb) {
+      const size_t pg = b0 / page_bytes, off = b0 % page_bytes, k = std::min<unsigned long long>(nb, page_bytes - off);
+      memcpy(d, (const char*)pages[pg] + off, k);
+      d += k;
+      b0 += k;
+      nb -= k;
+    }
+  }
+  void write_host(const void* src, unsigned long long nb) {  // at the end of the stream (pages reserved)
+    const char* s = (const char*)src;
+    unsigned long long b0 = bytes;
+    while (nb) {
+      const size_t pg = b0 / page_bytes, off = b0 % page_bytes, k = std::min<unsigned long long>(nb, page_bytes - off);
+      memcpy((char*)pages[pg] + off, s, k);
+      s += k;
+      b0 += k;
+      nb -= k;
+    }
+  }
+  // append n compact rows (word counts l) whose bytes are in dev, async on stream
+  void append_dev(const uint8_t* l, unsigned long long n, const void* dev, hipStream_t stream, HostPagePool& pool) {
+    unsigned long long nb = 0;
+    for (unsigned long long q = 0; q < n; q++) nb += 4ULL * l[q];
+    reserve_bytes(nb, pool);
+    add_rows(l, n);
+    copy_out(dev, bytes, nb, stream);
+    bytes += nb;
+    rows += n;
+  }
+  // append fixed-stride host rows (hdr_words + nmsg words each), compacting them on the host
+  void append_fixed_host(const uint32_t* fixed, unsigned long long n, size_t W, int hdr_words, HostPagePool& pool) {
+    std::vector<uint8_t> l(n);
+    unsigned long long nb = 0;
+    for (unsigned long long q = 0; q < n; q++) {
+      l[q] = (uint8_t)(hdr_words + (fixed[q * W] & 0xFFu));
+      nb += 4ULL * l[q];
+    }
+    reserve_bytes(nb, pool);
+    add_rows(l.data(), n);
+    for (unsigned long long q = 0; q < n; q++) {
+      write_host(fixed + q * W, 4ULL * l[q]);
+      bytes += 4ULL * l[q];
+    }
+    rows += n;
+  }
+  // rows [r0, r0 + n) as fixed-stride rows (host side; checkpoints)
+  void read_fixed_host(unsigned long long r0, unsigned long long n, uint32_t* out) const {
+    const size_t W = row_bytes / 4;
+    unsigned long long b = byte_of(r0);
+    for (unsigned long long q = 0; q < n; q++) {
+      const unsigned L = lens[r0 + q];
+      memset(out + q * W, 0, row_bytes);
+      read_host(b, 4ULL * L, out + q * W);
+      b += 4ULL * L;
+    }
+  }
+  // give back the pages whose bytes all lie below row r
   void recycle_below(unsigned long long r, HostPagePool& pool) {
-    for (size_t pg = 0; pg < pages.size() && (pg + 1) * page_rows <= r; pg++) {
+    const unsigned long long b = byte_of(std::min(r, rows));
+    for (size_t pg = 0; pg < pages.size() && (pg + 1) * page_bytes <= b; pg++) {
       pool.put(pages[pg]);
       pages[pg] = nullptr;
     }
@@ -375,10 +467,9 @@ struct HostLevel {
   void clear(HostPagePool& pool) {
     for (void* p : pages) pool.put(p);
     pages.clear();
-    rows = 0;
-  }
-  const uint32_t* row(unsigned long long r) const {
-    return (const uint32_t*)((const char*)pages[r / page_rows] + (r % page_rows) * row_bytes);
+    lens.clear();
+    cum.clear();
+    rows = bytes = 0;
   }
 };
 // Host memory the host frontier may pin: RMC_HOST_FRONTIER_GIB, or 80% of

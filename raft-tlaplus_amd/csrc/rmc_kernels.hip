@@ -1217,6 +1217,106 @@ void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* ou
   (void)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
 }
 
+// ------------------------------------------------ compact host rows
+// Host-frontier levels are kept compact: each packed row trimmed after its
+// last DOMAIN message (1 + 4N + nmsg words, nmsg from the header word), rows
+// back to back.  Rows are packed on the device before they
+// cross PCIe and unpacked into fixed-stride rows in the input window, so the
+// kernels never see the compact form.  A wave per row: lane l moves word l
+// (coalesced on both sides); rows in the same wave-step are consecutive.
+__global__ __launch_bounds__(256) void k_row_words(const uint32_t* __restrict__ rows, unsigned long long n, int W,
+                                                   int hdr_words, uint32_t* __restrict__ lens32,
+                                                   uint8_t* __restrict__ lens8) {
+  const unsigned long long r = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t len = (uint32_t)hdr_words + (rows[r * (unsigned long long)W] & 0xFFu);
+  lens32[r] = len;
+  lens8[r] = (uint8_t)len;
+}
+__global__ __launch_bounds__(256) void k_widen_lens(const uint8_t* __restrict__ lens8, unsigned long long n,
+                                                    uint32_t* __restrict__ lens32) {
+  const unsigned long long r = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n) lens32[r] = lens8[r];
+}
+__global__ __launch_bounds__(256) void k_pack_rows(const uint32_t* __restrict__ rows, unsigned long long n, int W,
+                                                   const uint32_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ lens32, uint32_t* __restrict__ out) {
+  const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x / WAVE);
+  for (unsigned long long r = (unsigned long long)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; r < n;
+       r += waves) {
+    const uint32_t len = lens32[r];
+    const uint32_t* src = rows + r * (unsigned long long)W;
+    uint32_t* dst = out + offs[r];
+    for (uint32_t l = lane_id(); l < len; l += WAVE) dst[l] = src[l];
+  }
+}
+__global__ __launch_bounds__(256) void k_unpack_rows(const uint32_t* __restrict__ in, unsigned long long n, int W,
+                                                     const uint32_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens32, uint32_t* __restrict__ rows) {
+  const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x / WAVE);
+  for (unsigned long long r = (unsigned long long)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; r < n;
+       r += waves) {
+    const uint32_t len = lens32[r];
+    const uint32_t* src = in + offs[r];
+    uint32_t* dst = rows + r * (unsigned long long)W;
+    for (uint32_t l = lane_id(); l < (uint32_t)W; l += WAVE) dst[l] = l < len ? src[l] : 0u;
+  }
+}
+static unsigned grid_for(unsigned long long n, unsigned per) {
+  unsigned long long g = (n + per - 1) / per;
+  return (unsigned)(g < 1 ? 1 : g > (1u << 20) ? (1u << 20) : g);
+}
+void launch_row_words(const uint32_t* rows, unsigned long long n, int W, int hdr_words, uint32_t* lens32,
+                      uint8_t* lens8, hipStream_t s) {
+  if (!n) return;
+  k_row_words<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(rows, n, W, hdr_words, lens32, lens8);
+}
+void launch_widen_lens(const uint8_t* lens8, unsigned long long n, uint32_t* lens32, hipStream_t s) {
+  if (!n) return;
+  k_widen_lens<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(lens8, n, lens32);
+}
+void launch_pack_rows(const uint32_t* rows, unsigned long long n, int W, const uint32_t* offs, const uint32_t* lens32,
+                      uint32_t* out, hipStream_t s) {
+  if (!n) return;
+  k_pack_rows<<<grid_for(n, 4), 256, 0, s>>>(rows, n, W, offs, lens32, out);
+}
+void launch_unpack_rows(const uint32_t* in, unsigned long long n, int W, const uint32_t* offs, const uint32_t* lens32,
+                        uint32_t* rows, hipStream_t s) {
+  if (!n) return;
+  k_unpack_rows<<<grid_for(n, 4), 256, 0, s>>>(in, n, W, offs, lens32, rows);
+}
+
+// ------------------------------------------------ batched device copies
+// The logical-shard transport (rmc_sharded.cpp LocalComm): every transfer of
+// one exchange step in ONE launch (blockIdx.y = transfer, blockIdx.x = 64 KiB
+// piece) instead of a hipMemcpyAsync per (source, destination, buffer).
+__global__ __launch_bounds__(256) void k_multi_copy(const CopyDesc* __restrict__ d, int n) {
+  constexpr unsigned long long PIECE = 64 << 10;
+  for (int q = blockIdx.y; q < n; q += gridDim.y) {
+    const CopyDesc c = d[q];
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * PIECE; b0 < c.bytes;
+         b0 += (unsigned long long)gridDim.x * PIECE) {
+      const unsigned long long b1 = c.bytes < b0 + PIECE ? c.bytes : b0 + PIECE;
+      const char* src = (const char*)c.src + b0;
+      char* dst = (char*)c.dst + b0;
+      unsigned long long done = 0;
+      if ((((unsigned long long)src | (unsigned long long)dst) & 15ULL) == 0) {
+        const unsigned long long nv = (b1 - b0) >> 4;
+        for (unsigned long long i = threadIdx.x; i < nv; i += blockDim.x)
+          reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+        done = nv << 4;
+      }
+      for (unsigned long long i = done + threadIdx.x; i < b1 - b0; i += blockDim.x) dst[i] = src[i];
+    }
+  }
+}
+void launch_multi_copy(const CopyDesc* d, int n, unsigned long long max_bytes, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned long long pieces = (max_bytes + (64 << 10) - 1) / (64 << 10);
+  dim3 grid((unsigned)(pieces < 1 ? 1 : pieces > 2048 ? 2048 : pieces), (unsigned)(n > 65535 ? 65535 : n));
+  k_multi_copy<<<grid, 256, 0, s>>>(d, n);
+}
+
 // ------------------------------------------------ simulation (TLC -simulate)
 // One lane per walker: a random behaviour from Init, up to `depth` steps.  Each
 // step evaluates every Next binding of the current state (all lanes of a wave

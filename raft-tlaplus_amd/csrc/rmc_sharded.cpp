@@ -78,9 +78,43 @@ struct LocalComm : Comm {
     for (int i = 0; i < world; i++)
       for (int j = 0; j < k; j++) out[(size_t)i * k + j] = in[i][j];
   }
+  // the step's transfers in one batched copy kernel (k_multi_copy): a
+  // hipMemcpyAsync each cost ~15,000 launches per check at W = 8
+  std::vector<CopyDesc> desc;
+  DevBuf ddesc;
+  CopyDesc* hdesc = nullptr;  // pinned staging of the descriptors
+  size_t hcap = 0;
+  hipEvent_t hdone = nullptr;  // the last descriptor upload has been read
+  ~LocalComm() override {
+    if (hdone) (void)hipEventSynchronize(hdone), (void)hipEventDestroy(hdone);
+    if (hdesc) (void)hipHostFree(hdesc);
+  }
   void alltoallv(const std::vector<Xfer>& x) override {
+    desc.clear();
+    unsigned long long mx = 0;
     for (auto& t : x)
-      if (t.bytes) HIPCHK(hipMemcpyAsync(t.rbuf, t.sbuf, t.bytes, hipMemcpyDeviceToDevice, stream));
+      if (t.bytes) {
+        desc.push_back({t.sbuf, t.rbuf, (unsigned long long)t.bytes});
+        mx = std::max<unsigned long long>(mx, t.bytes);
+      }
+    if (desc.empty()) return;
+    if (desc.size() == 1) {
+      HIPCHK(hipMemcpyAsync(desc[0].dst, desc[0].src, desc[0].bytes, hipMemcpyDeviceToDevice, stream));
+      return;
+    }
+    if (!hdone) HIPCHK(hipEventCreateWithFlags(&hdone, hipEventDisableTiming));
+    else HIPCHK(hipEventSynchronize(hdone));  // the staging is free again
+    if (hcap < desc.size()) {
+      if (hdesc) HIPCHK(hipHostFree(hdesc));
+      hcap = std::max<size_t>(desc.size(), 1024);
+      HIPCHK(hipHostMalloc((void**)&hdesc, hcap * sizeof(CopyDesc), hipHostMallocDefault));
+    }
+    memcpy(hdesc, desc.data(), desc.size() * sizeof(CopyDesc));
+    ddesc.ensure(hcap * sizeof(CopyDesc));
+    HIPCHK(hipMemcpyAsync(ddesc.p, hdesc, desc.size() * sizeof(CopyDesc), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipEventRecord(hdone, stream));
+    launch_multi_copy(ddesc.as<CopyDesc>(), (int)desc.size(), mx, stream);
+    HIPCHK(hipGetLastError());
   }
 };
 

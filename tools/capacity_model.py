@@ -67,8 +67,8 @@ def extrapolate(levels, window, kind):
 
 
 def known_config2():
-    """Config 2's per-level new states from the host-frontier ladder (depth 29 reached)."""
-    txt = open(os.path.join(ROOT, "profiles", "r03", "ladder_Raft_n3v2e3_twostreams.txt")).read()
+    """Config 2 per-level new states from the compact host-frontier ladder (depth 31 reached)."""
+    txt = open(os.path.join(ROOT, "profiles", "r04", "ladder_Raft_n3v2e3_hf1_compact.txt")).read()
     lv = {1: 1}
     for d, new in re.findall(r"depth (\d+): (\d+) new", txt):
         lv[int(d)] = int(new)
@@ -83,7 +83,7 @@ def main():
     windows = (4, 6, 8, 10, 14)
     print("Capacity model (tools/capacity_model.py): linear fit of the level growth ratio r_k = n_{k+1}/n_k")
     print("on the last W known levels, extended until r <= 0 or a level falls below one state.  Config 2 is known")
-    print("to depth %d (profiles/r03/ladder_Raft_n3v2e3_twostreams.txt: %d distinct states)." % (cut0, sum(c2)))
+    print("to depth %d (profiles/r04/ladder_Raft_n3v2e3_hf1_compact.txt: %d distinct states)." % (cut0, sum(c2)))
     print("(A quadratic fit of r_k was tried too: on these prefixes it curves back up and diverges -- unusable.)")
     print()
     print("Validation on the two rungs that exhaust (tests/golden/exhausted.json), cut at depths %s:" % (cuts,))
