@@ -86,6 +86,8 @@ typedef struct {
   uint32_t state_bytes; /* packed frontier state size */
   uint32_t max_msgs;    /* largest |DOMAIN messages| seen */
   uint64_t hash_capacity;
+  uint64_t device_bytes; /* HBM held by the check's buffers at its end (they only grow within a check): the
+                            single-GPU search's total; the sharded search's largest shard on this process */
 } rmc_result;
 
 /* Load M.tla + M.cfg, as TLC reads them (`tlc2.TLC -config M.cfg M.tla`; a

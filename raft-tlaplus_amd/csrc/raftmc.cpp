@@ -53,6 +53,7 @@ int main(int argc, char** argv) {
   std::string dump_fmt, dump_file;
   unsigned long long sim_walkers = 1ULL << 20, sim_num = 0, sim_seed = 0;
   unsigned sim_depth = 100;
+  std::string next_ops;
   double sim_seconds = 0;
   for (int a = 1; a < argc; a++) {
     std::string k = argv[a];
@@ -89,12 +90,13 @@ int main(int argc, char** argv) {
       if (dump_fmt != "tla" && dump_fmt != "json") { fprintf(stderr, "raftmc: -dumpTrace tla|json FILE\n"); return 2; }
     }
     else if (k == "-v") o.verbose = 1;
+    else if (k == "-next") next_ops = val();  // Next as disjunct names (with -module): the front end's form
     else if (!k.empty() && k[0] == '-') { fprintf(stderr, "raftmc: unknown option %s\n", k.c_str()); return 2; }
     else tla = k;
   }
   if (tla.empty() == module.empty() || (!module.empty() && cfg.empty())) {
-    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-hostfrontier -1|0|1] [-checkpoint MIN] [-metadir DIR] [-recover DIR] [-config M.cfg] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
-                    "       raftmc [options] -module M -config X.cfg   (the built-in lowering of module M, no .tla)\n"
+    fprintf(stderr, "usage: raftmc [-deadlock] [-workers N] [-cpu] [-shards W] [-fpwidth 64|128] [-hostfrontier -1|0|1] [-checkpoint MIN] [-metadir DIR] [-recover DIR] [-config M.cfg] [-maxdepth D] [-dumpTrace tla|json FILE] [-json] [-v] M.tla\n"
+                    "       raftmc [options] -module M -config X.cfg [-next \"A, B, ...\"]   (module M's lowering, no .tla)\n"
                     "       raftmc -simulate [-depth D] [-num BEHAVIOURS] [-seed S] [-walkers W] [-seconds T] ...\n");
     return 2;
   }
@@ -112,6 +114,10 @@ int main(int argc, char** argv) {
       return 1;
     }
     tla = module + " (built-in lowering)";
+    if (!next_ops.empty() && rmc_model_set_next(m, next_ops.c_str()) != 0) {
+      fprintf(stderr, "raftmc: %s\n", rmc_last_error());
+      return 1;
+    }
   } else if (rmc_model_load(tla.c_str(), cfg.empty() ? nullptr : cfg.c_str(), &m, err, sizeof err) != 0) {
     fprintf(stderr, "raftmc: %s\n", err);
     return 1;

@@ -1065,6 +1065,14 @@ static Ckpt ckpt_read_meta(const std::string& dir, const rmc_model* m) {
   return c;
 }
 
+// The auto switch's threshold: a next level projected past this fraction of
+// HBM moves the levels to the host at a level boundary (RMC_HF_HBM_FRACTION,
+// default 0.25; tests lower it to exercise the switch on small configs).
+double hf_hbm_fraction() {
+  if (const char* e = getenv("RMC_HF_HBM_FRACTION")) return atof(e);
+  return 0.25;
+}
+
 size_t host_frontier_limit() {
   if (const char* e = getenv("RMC_HOST_FRONTIER_GIB")) return (size_t)(atof(e) * 1073741824.0);
   unsigned long long avail_kb = 0;
@@ -1641,7 +1649,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     // still small -- their HBM is not reusable once released (§3), so a
     // later switch strands more of it
     if (!hf && hf_opt == 0 && hbm_total &&
-        (double)cur_n * std::max(rate, 1.0) * 1.25 * (double)(W * 4) > 0.25 * (double)hbm_total) {
+        (double)cur_n * std::max(rate, 1.0) * 1.25 * (double)(W * 4) > hf_hbm_fraction() * (double)hbm_total) {
       lvl_c0 = 0;
       lvl_next_n = 0;
       enter_hf();
@@ -2172,6 +2180,18 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   res->expand_launches = expand_launches;
   res->hash_capacity = slots;
   res->max_msgs = hst.max_msgs;
+  {
+    size_t b = 0;
+    for (DevBuf* x : {&A.table, &A.table2, &A.cslot, &A.cob, &A.cwin, &A.poff, &A.pn, &A.pwin, &A.ppos, &A.counters,
+                      &A.stbuf, &A.scantmp})
+      b += x->bytes;
+    for (int k = 0; k < 2; k++)
+      for (DevBuf* x : {&A.hwin_in[k], &A.hwin_out[k], &A.hf_pack[k], &A.hf_olen32[k], &A.hf_olen8[k], &A.hf_ooff[k],
+                        &A.hf_oscan[k], &A.hf_stage[k], &A.hf_ilen32[k], &A.hf_ilen8[k], &A.hf_ioff[k], &A.hf_iscan[k]})
+        b += x->bytes;
+    for (GrowBuf* x : {&A.fa, &A.fb, &A.trp, &A.trb}) b += x->bytes;
+    res->device_bytes = b;
+  }
   // the next check's row packing: the peak |DOMAIN messages| of a complete
   // check (a resumed one saw only the levels after its snapshot)
   if (status == 0 && !opt->max_depth && !opt->msg_cap_K && !recovering) m->hint_kmax = std::max(1u, hst.max_msgs);
@@ -2215,7 +2235,7 @@ int rmc_abi_layout(uint64_t* out, int cap) {
       offsetof(rmc_result, violated), offsetof(rmc_result, hidden_var_collisions), offsetof(rmc_result, seconds),
       offsetof(rmc_result, message), offsetof(rmc_result, expand_ms), offsetof(rmc_result, mark_ms),
       offsetof(rmc_result, materialize_ms), offsetof(rmc_result, expand_launches), offsetof(rmc_result, state_bytes),
-      offsetof(rmc_result, max_msgs), offsetof(rmc_result, hash_capacity)};
+      offsetof(rmc_result, max_msgs), offsetof(rmc_result, hash_capacity), offsetof(rmc_result, device_bytes)};
   const int n = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < n && k < cap; k++) out[k] = v[k];
   return n;

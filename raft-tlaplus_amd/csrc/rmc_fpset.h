@@ -196,6 +196,56 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
 }
 #endif
 
+// The default protocol split in two for pure-insert kernels (k_insert_recv):
+// the first four entries of SEVERAL keys' probe runs are loaded before any is
+// decided, so their loads are in flight together; each key then continues
+// from its loaded group exactly as fpset_insert does.
+__device__ __forceinline__ bool fpset_group_load(const unsigned long long* T, unsigned long long mask,
+                                                 unsigned long long fp, ulonglong2 (&e)[4]) {
+  const unsigned long long slot = fp_slot(fp, mask);
+  if (slot + 3 > mask) return false;
+  const ulonglong2* E = reinterpret_cast<const ulonglong2*>(T) + slot;
+#pragma unroll
+  for (int q = 0; q < 4; q++) e[q] = E[q];
+  return true;
+}
+__device__ __forceinline__ unsigned long long fpset_insert_loaded(unsigned long long* T, unsigned long long mask,
+                                                                  unsigned long long fp, unsigned long long val,
+                                                                  unsigned long long floor, DevStatus* st,
+                                                                  const ulonglong2 (&e)[4], bool loaded) {
+  unsigned long long slot = fp_slot(fp, mask);
+  if (loaded) {
+    int k = 4;
+    unsigned long long kv = 0;
+    bool found = false;
+#pragma unroll
+    for (int q = 3; q >= 0; q--)
+      if (e[q].x == fp || e[q].x == EMPTY) { k = q; kv = e[q].y; found = e[q].x == fp; }
+    slot = (slot + (unsigned long long)k) & mask;
+    if (found) {
+      if (kv >= floor && val < kv) atomicMin(T + 2 * slot + 1, val);
+      return slot;
+    }
+  }
+  const unsigned long long limit = mask < 4096 ? mask : 4096;
+  for (unsigned long long probe = 0; probe <= limit; probe++) {
+    unsigned long long* p = T + 2 * slot;
+    const unsigned long long prev = atomicCAS(p, EMPTY, fp);
+    if (prev == EMPTY) {
+      atomicMin(p + 1, val);
+      return slot;
+    }
+    if (prev == fp) {
+      const unsigned long long cur = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur >= floor && val < cur) atomicMin(p + 1, val);
+      return slot;
+    }
+    slot = (slot + 1) & mask;
+  }
+  atomicOr(&st->cap_flags, 1u << E_CAP_TABLE);
+  return EMPTY;
+}
+
 // The value of fp's entry (~0 if absent): read-only probe.
 __device__ __forceinline__ unsigned long long fpset_value(const unsigned long long* T, unsigned long long mask,
                                                           unsigned long long fp) {

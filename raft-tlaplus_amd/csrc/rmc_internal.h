@@ -472,9 +472,56 @@ struct HostLevel {
     rows = bytes = 0;
   }
 };
+// Synchronous compact-row transfers between a host level and fixed-stride
+// device rows (the sharded search's per-shard host frontier; the single-GPU
+// search pipelines the same kernels over its copy streams).
+struct HostRowsIO {
+  DevBuf pack, l32, l8, off, scan, stage, il32, il8, ioff, iscan;
+  static size_t atleast(size_t b) { return b < 16 ? 16 : b; }
+  // rows [r0, r0 + n) of h -> fixed rows at dev, in stream order on st
+  void load(const HostLevel& h, unsigned long long r0, unsigned long long n, uint32_t* dev, size_t W, hipStream_t st) {
+    if (!n) return;
+    stage.ensure(atleast(n * W * 4));
+    il32.ensure(atleast(n * 4));
+    il8.ensure(atleast(n));
+    ioff.ensure(atleast(n * 4));
+    iscan.ensure(atleast(rmc::scan_temp_bytes(n)));
+    const unsigned long long b0 = h.byte_of(r0), b1 = h.byte_of(r0 + n);
+    h.copy_in(b0, b1 - b0, stage.p, st);
+    HIPCHK(hipMemcpyAsync(il8.p, h.lens.data() + r0, n, hipMemcpyHostToDevice, st));
+    rmc::launch_widen_lens(il8.as<uint8_t>(), n, il32.as<uint32_t>(), st);
+    rmc::launch_scan(iscan.p, iscan.bytes, il32.as<uint32_t>(), ioff.as<uint32_t>(), n, st);
+    rmc::launch_unpack_rows(stage.as<uint32_t>(), n, (int)W, ioff.as<uint32_t>(), il32.as<uint32_t>(), dev, st);
+    HIPCHK(hipGetLastError());
+  }
+  // n fixed rows at dev -> appended to h; returns once they are in the pages
+  void store(HostLevel& h, const uint32_t* dev, unsigned long long n, size_t W, int hdr_words, hipStream_t st,
+             HostPagePool& pool) {
+    if (!n) return;
+    pack.ensure(atleast(n * W * 4));
+    l32.ensure(atleast(n * 4));
+    l8.ensure(atleast(n));
+    off.ensure(atleast(n * 4));
+    scan.ensure(atleast(rmc::scan_temp_bytes(n)));
+    rmc::launch_row_words(dev, n, (int)W, hdr_words, l32.as<uint32_t>(), l8.as<uint8_t>(), st);
+    rmc::launch_scan(scan.p, scan.bytes, l32.as<uint32_t>(), off.as<uint32_t>(), n, st);
+    rmc::launch_pack_rows(dev, n, (int)W, off.as<uint32_t>(), l32.as<uint32_t>(), pack.as<uint32_t>(), st);
+    HIPCHK(hipGetLastError());
+    std::vector<uint8_t> lens(n);
+    HIPCHK(hipMemcpyAsync(lens.data(), l8.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    h.append_dev(lens.data(), n, pack.p, st, pool);
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  void release() {
+    for (DevBuf* b : {&pack, &l32, &l8, &off, &scan, &stage, &il32, &il8, &ioff, &iscan}) b->release();
+  }
+};
+
 // Host memory the host frontier may pin: RMC_HOST_FRONTIER_GIB, or 80% of
 // MemAvailable capped at 200 GiB (a shared host must keep room for others).
 size_t host_frontier_limit();
+double hf_hbm_fraction();
 
 struct EventTimer {
   hipEvent_t a, b;

@@ -955,14 +955,40 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
 }
 
 // Owner side: insert every received (fp, val); first in TLC order wins.
+#ifndef RMC_RECV_U
+#define RMC_RECV_U 4
+#endif
+constexpr int RECV_U = RMC_RECV_U;
 __global__ __launch_bounds__(256) void k_insert_recv(const unsigned long long* __restrict__ recv, unsigned long long n,
                                                      unsigned long long* __restrict__ table, unsigned long long mask,
                                                      unsigned long long floor,
                                                      unsigned long long* __restrict__ recv_slot, DevStatus* st) {
-  unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const unsigned long long v = recv[2 * j + 1];
-  recv_slot[j] = cand_word(fpset_insert(table, mask, recv[2 * j], v, floor, st), v);
+  // RECV_U records per thread (consecutive records on consecutive threads of
+  // each step, for the L2 locality of a parent's duplicates): their first
+  // probe groups are loaded together, then inserted in record order
+  constexpr int U = RECV_U;
+  const unsigned long long j0 = (unsigned long long)blockIdx.x * blockDim.x * U + threadIdx.x;
+  unsigned long long fp[U], v[U];
+  ulonglong2 e[U][4];
+  bool ld[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
+    if (j < n) {
+      fp[u] = recv[2 * j];
+      v[u] = recv[2 * j + 1];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
+    ld[u] = j < n && fpset_group_load(table, mask, fp[u], e[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
+    if (j < n) recv_slot[j] = cand_word(fpset_insert_loaded(table, mask, fp[u], v[u], floor, st, e[u], ld[u]), v[u]);
+  }
 }
 
 // Owner side, after all of the round's inserts: did the record win its fp?
@@ -973,23 +999,38 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
                                                    unsigned long long n, const unsigned long long* __restrict__ table,
                                                    unsigned long long floor, uint8_t* __restrict__ flag,
                                                    unsigned long long* __restrict__ newcount, DevStatus* st) {
-  unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  bool w = false;
-  if (j < n) {
-    const unsigned long long rs = recv_slot[j];
-    if (!(rs & CAND_DUP)) {
+  // RECV_U records per thread, their table reads issued together (as k_insert_recv)
+  constexpr int U = RECV_U;
+  const unsigned long long j0 = (unsigned long long)blockIdx.x * blockDim.x * U + threadIdx.x;
+  unsigned long long rs[U], tv[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
+    rs[u] = j < n ? recv_slot[j] : CAND_DUP;
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) tv[u] = (rs[u] & CAND_DUP) ? 0ULL : table[2 * (rs[u] & CAND_SLOT_MASK) + 1];
+  unsigned int wins = 0, colls = 0;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
+    if (j >= n) continue;
+    bool w = false;
+    if (!(rs[u] & CAND_DUP)) {
       const unsigned long long mine = recv[2 * j + 1];
       bool c = false;
-      w = fpset_won(table[2 * (rs & CAND_SLOT_MASK) + 1], mine >> VAL_RANK_SHIFT, floor, mine, c);
-      if (c) atomicAdd(&st->hidden_coll, 1ULL);
+      w = fpset_won(tv[u], mine >> VAL_RANK_SHIFT, floor, mine, c);
+      colls += c;
     }
     flag[j] = w ? 1 : 0;
+    wins += w;
   }
+  if (colls) atomicAdd(&st->hidden_coll, (unsigned long long)colls);
   __shared__ unsigned int c;
   if (threadIdx.x == 0) c = 0;
   __syncthreads();
-  unsigned long long m = __ballot(w);
-  if (lane_id() == 0 && m) atomicAdd(&c, (unsigned)__popcll(m));
+  for (int o = 32; o > 0; o >>= 1) wins += __shfl_xor(wins, o, WAVE);
+  if (lane_id() == 0 && wins) atomicAdd(&c, wins);
   __syncthreads();
   if (threadIdx.x == 0 && c) atomicAdd(newcount, (unsigned long long)c);
 }
@@ -1083,15 +1124,15 @@ void launch_insert_recv(const unsigned long long* recv, unsigned long long n, un
                         unsigned long long mask, unsigned long long floor, unsigned long long* recv_slot, DevStatus* st,
                         hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_insert_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, n, table, mask, floor,
-                     recv_slot, st);
+  hipLaunchKernelGGL(k_insert_recv, dim3((unsigned)((n + 256 * RECV_U - 1) / (256 * RECV_U))), dim3(256), 0, s, recv, n,
+                     table, mask, floor, recv_slot, st);
 }
 void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
                       const unsigned long long* table, unsigned long long floor, uint8_t* flag,
                       unsigned long long* newcount, DevStatus* st, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recv, recv_slot, n, table, floor,
-                     flag, newcount, st);
+  hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 256 * RECV_U - 1) / (256 * RECV_U))), dim3(256), 0, s, recv,
+                     recv_slot, n, table, floor, flag, newcount, st);
 }
 void launch_mark_gen(const LevelArgs& a, int moved, const uint32_t* perm, const uint8_t* flag_back,
                      unsigned long long* newcount, hipStream_t s) {

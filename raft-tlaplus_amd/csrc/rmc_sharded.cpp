@@ -360,6 +360,15 @@ struct Shard {
   unsigned long long ncand = 0, nrecv = 0, nwin = 0, n = 0;
   std::vector<uint64_t> seg_off, rseg_off;  // send segments by owner / recv segments by source
   DevStatus hst;
+  // per-shard host frontier (rmc_options.host_frontier): the shard's current
+  // and next level live in compact host pages; each round's block of parents
+  // is unpacked into win_in, the round's new local rows (a contiguous local
+  // range [fill0, next_fill)) land in win_out and are packed out after it
+  bool hf = false;
+  HostLevel hcur, hnxt;
+  HostRowsIO io;
+  DevBuf win_in, win_out;
+  unsigned long long fill0 = 0;
 };
 
 static unsigned long long local_count(unsigned long long P, int W, unsigned long long CH, int r) {
@@ -402,7 +411,6 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   if (opt->fp_bits && opt->fp_bits != 64) throw std::runtime_error("fp_bits 128 is offered by the single-GPU search (rmc_check) only");
   if ((opt->checkpoint_dir && *opt->checkpoint_dir) || (opt->recover_dir && *opt->recover_dir))
     throw std::runtime_error("checkpoint / recover are offered by the single-GPU search (rmc_check) only");
-  if (opt->host_frontier == 1) throw std::runtime_error("host_frontier = 1 is offered by the single-GPU search (rmc_check) only");
   uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
   if (kmax > 120) kmax = 120;
   finalize_model(m, kmax);
@@ -418,6 +426,24 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   if (W > 64) throw std::runtime_error("at most 64 shards");
 
   std::vector<Shard> sh(NL);
+  // the per-shard host frontier: one pinned-page pool for this process's shards
+  HostPagePool pool;
+  pool.page_bytes = std::max<size_t>(WD * 4, 256ULL << 20);
+  if (const char* e = getenv("RMC_HOST_PAGE_ROWS")) pool.page_bytes = std::max<long long>(1, atoll(e)) * WD * 4;
+  pool.limit = host_frontier_limit();
+  struct PagesGuard {
+    std::vector<Shard>& sh;
+    HostPagePool& pool;
+    ~PagesGuard() {
+      for (Shard& s : sh) { s.hcur.clear(pool); s.hnxt.clear(pool); }
+    }
+  } pages_guard{sh, pool};
+  const int hdr_words = 1 + 4 * M.N;
+  size_t hbm_total = 0;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceTotalMem(&hbm_total, dev);
+  }
   // the model's size hints are whole-search totals (the single-GPU search
   // keeps them so too): a shard starts at its 1/W share
   auto share = [&](unsigned long long total) { return total / (unsigned long long)W; };
@@ -501,6 +527,20 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     if (err) { status = 2; message = "evaluation error in an invariant on the initial state"; bad_state = 0; }
     else if (bad >= 0) { status = 1; snprintf(res->violated, sizeof res->violated, "%s", m->inv_names[bad].c_str()); bad_state = 0; }
   }
+  // a shard's current level (device rows) -> its host pages; the device frontiers are released
+  auto shard_to_host = [&](Shard& s) {
+    if (s.hf) return;
+    s.hcur.init(pool.page_bytes, WD * 4);
+    s.hnxt.init(pool.page_bytes, WD * 4);
+    HIPCHK(hipStreamSynchronize(stream));
+    s.io.store(s.hcur, s.cur, s.ncur, WD, hdr_words, stream, pool);
+    s.B->fa.release();
+    s.B->fb.release();
+    s.cur = s.nxt = nullptr;
+    s.hf = true;
+  };
+  if (opt->host_frontier == 1)
+    for (Shard& s : sh) shard_to_host(s);
   // per-shard kernel timers, read after the round's next stream sync (no sync of their own)
   std::vector<EventTimer> te(NL), tz(NL);
   std::vector<char> te_on(NL, 0), tz_on(NL, 0);
@@ -526,7 +566,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   auto round_args = [&](LevelArgs& a, Shard& s, unsigned long long c) {
     memset(&a, 0, sizeof a);
     a.model = &M;
-    a.frontier = s.cur + c * CH * WD;
+    a.frontier = s.hf ? s.win_in.as<uint32_t>() : s.cur + c * CH * WD;
     a.nparents = s.n;
     a.pbase = lbase + c * W * CH + (unsigned long long)s.id * CH;
     a.level = depth + 1;
@@ -560,6 +600,19 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         break;
       }
     }
+    if (opt->host_frontier == 0 && hbm_total) {
+      // auto: a next level projected past a quarter of this GPU's HBM (per
+      // local shard) moves every shard's levels to host pages at this
+      // boundary -- decided on the allgathered projections, so all agree
+      for (int i = 0; i < NL; i++)
+        rows[i] = {(uint64_t)((double)sh[i].ncur * std::max(rate, 1.0) * 1.25 * (double)(WD * 4) >
+                              hf_hbm_fraction() * (double)hbm_total / NL)};
+      comm.allgather(rows, all, 1);
+      bool any = false;
+      for (int r = 0; r < W; r++) any |= all[r] != 0;
+      if (any)
+        for (Shard& s : sh) shard_to_host(s);
+    }
     const unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     const unsigned long long rounds = (P + W * CH - 1) / (W * CH);
@@ -585,6 +638,10 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       for (int si = 0; si < NL; si++) {
         Shard& s = sh[si];
         HIPCHK(hipMemsetAsync(s.B->counters.p, 0, 64, stream));
+        if (s.n && s.hf) {  // the round's block of this shard's parents, unpacked from host pages
+          s.win_in.ensure(CH * WD * 4);
+          s.io.load(s.hcur, c * CH, s.n, s.win_in.as<uint32_t>(), WD, stream);
+        }
         if (s.n) {
           LevelArgs a;
           round_args(a, s, c);
@@ -775,7 +832,10 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         unsigned long long need = s.next_fill;
         for (auto& pc : pcs)
           if (pc.d == s.id) need = std::max(need, pc.dl + (pc.b - pc.a));
-        {  // the next-level buffer grows in place to exactly what it receives
+        if (s.hf) {  // this round's rows: the local range [next_fill, need) into win_out
+          s.fill0 = s.next_fill;
+          s.win_out.ensure(std::max<unsigned long long>(1, need - s.fill0) * WD * 4);
+        } else {  // the next-level buffer grows in place to exactly what it receives
           bool cur_is_a = s.cur == s.B->fa.as<uint32_t>();
           GrowBuf& nb = cur_is_a ? s.B->fb : s.B->fa;
           grow_keep(nb, need * WD * 4, s.next_fill * WD * 4, stream);
@@ -816,7 +876,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         LevelArgs a;
         round_args(a, s, c);
         if (direct[s.id]) {
-          a.out = s.nxt + direct_dl[s.id] * WD;
+          a.out = s.hf ? s.win_out.as<uint32_t>() + (direct_dl[s.id] - s.fill0) * WD : s.nxt + direct_dl[s.id] * WD;
           a.out_base_global = s.tr_base[depth + 1] + direct_dl[s.id];
           a.tr_parent = s.B->trp.as<unsigned long long>();
           a.tr_bind = s.B->trb.as<uint16_t>();
@@ -852,7 +912,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
             }
             if (s.id == pc.d) {
               unsigned long long tr = s.tr_base[depth + 1] + pc.dl;
-              rowsx.rbuf = s.nxt + pc.dl * WD;
+              rowsx.rbuf = s.hf ? s.win_out.as<uint32_t>() + (pc.dl - s.fill0) * WD : s.nxt + pc.dl * WD;
               parx.rbuf = s.B->trp.as<unsigned long long>() + tr;
               bndx.rbuf = s.B->trb.as<uint16_t>() + tr;
             }
@@ -868,6 +928,11 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       for (Shard& s : sh) read_status(s);
       HIPCHK(hipStreamSynchronize(stream));
       read_timers();
+      for (Shard& s : sh)
+        if (s.hf) {  // the round's new rows to host pages; the round's parents are consumed
+          s.io.store(s.hnxt, s.win_out.as<uint32_t>(), s.next_fill - s.fill0, WD, hdr_words, stream, pool);
+          s.hcur.recycle_below((c + 1) * CH, pool);
+        }
       for (int i = 0; i < NL; i++)
         rows[i] = {sh[i].hst.err_key, sh[i].hst.inv_err_key, sh[i].hst.viol_key,
                    sh[i].hst.cap_flags | ((unsigned long long)sh[i].hst.max_msgs << 32)};
@@ -953,6 +1018,10 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       s.tr_base.push_back(s.tr_base[depth] + local_count(GW, W, CH, s.id));
       s.ncur = local_count(GW, W, CH, s.id);
       std::swap(s.cur, s.nxt);
+      if (s.hf) {
+        s.hcur.clear(pool);
+        std::swap(s.hcur, s.hnxt);
+      }
     }
     if (P) rate = (double)GW / (double)P;
     P = GW;
@@ -1011,6 +1080,19 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   res->materialize_ms = mat_ms;
   res->expand_launches = expand_launches;
   res->hash_capacity = sh[0].slots;
+  res->device_bytes = 0;
+  for (Shard& s : sh) {
+    size_t b = 0;
+    ShardBufs& B = *s.B;
+    for (DevBuf* x : {&B.table, &B.table2, &B.cfp, &B.cval, &B.cob, &B.cwin, &B.poff, &B.pn, &B.pwin, &B.ppos,
+                      &B.counters, &B.stbuf, &B.scantmp, &B.send, &B.perm, &B.recv, &B.rslot, &B.rflag, &B.sflag,
+                      &B.stage, &B.stp, &B.stb, &B.small, &B.bcnt, &B.boff, &B.btmp, &s.win_in, &s.win_out, &s.io.pack,
+                      &s.io.l32, &s.io.l8, &s.io.off, &s.io.scan, &s.io.stage, &s.io.il32, &s.io.il8, &s.io.ioff,
+                      &s.io.iscan})
+      b += x->bytes;
+    for (GrowBuf* x : {&B.fa, &B.fb, &B.trp, &B.trb}) b += x->bytes;
+    res->device_bytes = std::max<uint64_t>(res->device_bytes, b);
+  }
   {  // same-level hidden-variable collisions, summed over the shards
     for (int i = 0; i < NL; i++) {
       DevStatus fin;

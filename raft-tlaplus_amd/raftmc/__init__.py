@@ -44,7 +44,7 @@ class Result(ctypes.Structure):
                 ("expand_ms", ctypes.c_double), ("mark_ms", ctypes.c_double),
                 ("materialize_ms", ctypes.c_double), ("expand_launches", ctypes.c_uint64),
                 ("state_bytes", ctypes.c_uint32), ("max_msgs", ctypes.c_uint32),
-                ("hash_capacity", ctypes.c_uint64)]
+                ("hash_capacity", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64)]
 
 
 # every entry point include/rmc.h declares (checked by tests/test_abi.py)
@@ -172,6 +172,7 @@ class Model:
                    seconds=r.seconds, expand_ms=r.expand_ms, mark_ms=r.mark_ms,
                    materialize_ms=r.materialize_ms, expand_launches=r.expand_launches,
                    state_bytes=r.state_bytes, hash_capacity=r.hash_capacity, max_msgs=r.max_msgs,
+                   device_bytes=r.device_bytes,
                    hidden_var_collisions=r.hidden_var_collisions,
                    levels=[[levels[2 * k], levels[2 * k + 1]] for k in range(min(nl, 1024))])
         self._last = r

@@ -109,3 +109,19 @@ def test_rung_host_frontier(name):
 def test_rung_cpu_engine_prefix(name):
     r = model(EXH[name]).check_cpu(max_depth=25)
     assert r["levels"] == full(name)["levels"][:25]
+
+
+def test_per_shard_device_memory_scales_with_shards():
+    """The sharded search partitions the state-proportional memory: on the
+    bench rung (1.885e9 states) the HBM each logical shard holds at the end of
+    the check (rmc_result.device_bytes: fingerprint set, frontiers, trace
+    records, candidate scratch) is <= 0.6 of the single-GPU search's at W = 2
+    and <= 0.35 at W = 4, with every count equal."""
+    g = EXH["raft_n3v2e2_bench"]
+    cfg = os.path.join(ROOT, g["cfg_path"])
+    single = raftmc.Model(module=g["module"], cfg_path=cfg).check()
+    assert (single["distinct"], single["generated"], single["depth"]) == (g["distinct"], g["generated"], g["depth"])
+    for W, bound in ((2, 0.6), (4, 0.35)):
+        r = raftmc.Model(module=g["module"], cfg_path=cfg).check_logical(W)
+        assert (r["distinct"], r["generated"], r["depth"]) == (g["distinct"], g["generated"], g["depth"])
+        assert r["device_bytes"] <= bound * single["device_bytes"], (W, r["device_bytes"], single["device_bytes"])

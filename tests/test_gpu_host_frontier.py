@@ -111,3 +111,22 @@ def test_host_frontier_refused_elsewhere():
     g = SMALL["raft_n3v1e1"]
     with pytest.raises(raftmc.RaftmcError, match="host_frontier"):
         model(g).check_logical(2, host_frontier=1)
+
+
+@pytest.mark.parametrize("frac", ["0.0000001", "0.00002"])
+def test_auto_switch_at_a_level_boundary(monkeypatch, frac):
+    """The auto mode's level-boundary switch (a next level projected past a
+    fraction of HBM moves both levels to the host before the level starts):
+    RMC_HF_HBM_FRACTION lowers the quarter-of-HBM threshold so it fires on
+    Raft.cfg -- at the first levels, or deeper -- and the counts equal the
+    device-frontier search's and the oracle's."""
+    monkeypatch.setenv("RMC_HF_HBM_FRACTION", frac)
+    g = SHIPPED["Raft_cfg"]
+    same(model(g).check(host_frontier=0, chunk_parents=50000), g)
+
+
+@pytest.mark.parametrize("name", ["fsync_n2v2e2r1_hidden", "raft_n2v2e2r2_order"])
+def test_auto_switch_tlc_order(monkeypatch, name):
+    monkeypatch.setenv("RMC_HF_HBM_FRACTION", "0.000001")
+    g = ORDER[name]
+    same(model(g).check(host_frontier=0, chunk_parents=333), g)

@@ -104,3 +104,43 @@ def test_logical_shards_unsafe(name, shards):
     assert r["status"] == "violation" and r["violated"] == g["violated"]
     assert r["depth"] == g["depth"] and len(r["trace"]) == g["trace_len"]
     assert (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])
+
+
+# ---- per-shard host frontier (rmc_options.host_frontier in the sharded search)
+ORDER_HF = json.load(open(os.path.join(HERE, "golden", "order.json")))
+SHIPPED_HF = json.load(open(os.path.join(HERE, "golden", "shipped.json")))
+
+
+def _model(g):
+    if "cfg_path" in g:
+        return raftmc.Model(module=g["module"], cfg_path=os.path.join(os.path.dirname(HERE), g["cfg_path"]))
+    return raftmc.Model(module=g["module"], cfg_text=g["cfg"])
+
+
+def _same(r, g):
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    assert r["levels"] == g["levels"]
+    assert r["hidden_var_collisions"] == g["hidden_same_level"]
+
+
+@pytest.mark.parametrize("name", sorted(ORDER_HF))
+@pytest.mark.parametrize("W", [2, 3])
+def test_sharded_host_frontier_always(name, W, monkeypatch):
+    """Every shard's levels in compact host pages (small pages, small rounds):
+    the TLC-order fixtures' counts, levels and hidden-variable collisions."""
+    monkeypatch.setenv("RMC_HOST_PAGE_ROWS", "999")
+    g = ORDER_HF[name]
+    _same(_model(g).check_logical(W, host_frontier=1, chunk_parents=501), g)
+
+
+def test_sharded_host_frontier_shipped_raft(monkeypatch):
+    g = SHIPPED_HF["Raft_cfg"]
+    _same(_model(g).check_logical(4, host_frontier=1, chunk_parents=100000), g)
+
+
+def test_sharded_host_frontier_auto_switch(monkeypatch):
+    """The auto mode's level-boundary switch, decided on the allgathered
+    projections (RMC_HF_HBM_FRACTION lowers the threshold so it fires)."""
+    monkeypatch.setenv("RMC_HF_HBM_FRACTION", "0.00002")
+    g = SHIPPED_HF["Raft_cfg"]
+    _same(_model(g).check_logical(2, host_frontier=0, chunk_parents=70000), g)
