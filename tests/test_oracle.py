@@ -126,3 +126,24 @@ def test_unsafe_fixtures_pinned_by_both_oracles(name):
     p = bfs(make_spec(g["module"], parse_cfg(g["cfg"])))
     assert (p.status, p.violated, p.depth, len(p.trace)) == (g["status"], g["violated"], g["depth"], g["trace_len"])
     assert (p.generated, p.distinct) == (g["generated"], g["distinct"])
+
+
+def test_exhausted_rungs_pinned_by_the_c_oracle():
+    """The GPU records of the exhaustible BASELINE rungs (tests/golden/
+    exhausted.json) equal the C oracle's runs over them level for level --
+    the whole rung where the oracle exhausted it (tools/oracle_exhaust.py,
+    tools/fold_oracle_rungs.py)."""
+    ex = json.load(open(os.path.join(HERE, "golden", "exhausted.json")))
+    pinned = 0
+    for name, g in ex.items():
+        o = g.get("oracle")
+        if not o:
+            continue
+        pinned += 1
+        assert o["levels"] == g["levels"][:len(o["levels"])], name
+        assert g["oracle_levels"] == len(o["levels"])
+        if o["status"] == "ok":
+            assert (o["generated"], o["distinct"], o["depth"], o["hidden_same_level"]) == (
+                g["generated"], g["distinct"], g["depth"], g["hidden_var_collisions"]), name
+            assert len(o["levels"]) == len(g["levels"])
+    assert pinned >= 1
