@@ -29,6 +29,15 @@ struct SimStatus {
   unsigned long long walker;
 };
 
+// Where a generator's winners go when the next-level owners share its device
+// (logical shards): winners [first, next piece's first) in the generator's
+// TLC order are rows out[0..], trace records trp[0..] / trb[0..].
+struct MatPiece {
+  unsigned long long first;
+  uint32_t* out;
+  unsigned long long* trp;
+  uint16_t* trb;
+};
 struct LevelArgs {
   const Model* model;
   const uint32_t* frontier;
@@ -50,6 +59,8 @@ struct LevelArgs {
   unsigned long long out_base_global;
   unsigned long long* tr_parent;
   uint16_t* tr_bind;
+  const MatPiece* pieces;  // k_materialize: npieces > 0 replaces out / tr_* (pieces[0].first == 0)
+  int npieces;
   DevStatus* st;
   int diag;  // RMC_DIAG builds: k_expand stops after a phase (rmc_selftest_profile_expand); 0 = the real kernel
 };

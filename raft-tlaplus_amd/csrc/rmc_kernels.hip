@@ -816,7 +816,9 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
                                                      const uint32_t* __restrict__ par_pos, uint32_t* __restrict__ out,
                                                      unsigned long long out_base_global,
                                                      unsigned long long* __restrict__ tr_parent,
-                                                     uint16_t* __restrict__ tr_bind, DevStatus* st) {
+                                                     uint16_t* __restrict__ tr_bind,
+                                                     const MatPiece* __restrict__ pieces, int npieces,
+                                                     DevStatus* st) {
   constexpr int PB = Tile<N>::PB;  // must be k_expand's tile: a tile's candidates are contiguous only within one expand tile
   extern __shared__ __align__(16) unsigned char lds[];
   // winner list: (rank << 16 | candidate index in the tile) and the candidate's ordinal/binding word,
@@ -883,14 +885,28 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
       Delta d;
       eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, (int)(ob >> 16), d);
       const unsigned long long dst = (unsigned long long)sPos[p] + rank;
-      uint32_t* o = out + dst * (unsigned long long)words;
+      uint32_t* o;
+      unsigned long long* tp;
+      uint16_t* tb;
+      if (npieces) {  // logical shards: straight into the next-level owner's rows and trace records
+        int k = 0;
+        while (k + 1 < npieces && pieces[k + 1].first <= dst) k++;
+        const unsigned long long r = dst - pieces[k].first;
+        o = pieces[k].out + r * (unsigned long long)words;
+        tp = pieces[k].trp + r;
+        tb = pieces[k].trb + r;
+      } else {
+        o = out + dst * (unsigned long long)words;
+        tp = tr_parent + out_base_global + dst;
+        tb = tr_bind + out_base_global + dst;
+      }
       int nn = 0;
       int err = apply_delta<SPEC, N>(s, cM, d, o, &nn);
       if (err) atomicOr(&st->cap_flags, 1u << err);
       my_max = nn > my_max ? nn : my_max;
       const unsigned long long pg = pbase + p0 + p;
-      tr_parent[out_base_global + dst] = pg;
-      tr_bind[out_base_global + dst] = (uint16_t)b;
+      *tp = pg;
+      *tb = (uint16_t)b;
       // invariants read only the header and the server words: check them on
       // the parent + delta in place (SuccView), not on the row written to HBM
       const SuccView<SPEC, N> ns(s, d);
@@ -1172,7 +1188,7 @@ struct Launch {
     size_t lds_bytes = (size_t)PB * (a.model->words | 1) * 4;
     hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(MAT_T), lds_bytes, s, a.frontier, a.nparents,
                        a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
-                       a.tr_parent, a.tr_bind, a.st);
+                       a.tr_parent, a.tr_bind, a.pieces, a.npieces, a.st);
   }
 };
 
@@ -1331,23 +1347,51 @@ void launch_unpack_rows(const uint32_t* in, unsigned long long n, int W, const u
 // The logical-shard transport (rmc_sharded.cpp LocalComm): every transfer of
 // one exchange step in ONE launch (blockIdx.y = transfer, blockIdx.x = 64 KiB
 // piece) instead of a hipMemcpyAsync per (source, destination, buffer).
+// Each piece is copied in the widest unit both ends share: when src and dst
+// agree mod 16 (8, 4, 2) a byte head brings both to that alignment, the body
+// moves 16 (8, 4, 2) B per lane with four loads in flight before the stores,
+// and a byte tail ends it.  (The trace records -- 8 B parent indices, 2 B
+// bindings -- and the 1 B win flags land at arbitrary element offsets: a byte
+// loop for anything not 16 B aligned cost them ~1 B per lane per step.)
+template <class T>
+__device__ __forceinline__ void copy_units(const char* src, char* dst, unsigned long long n) {
+  constexpr int U = 4;
+  const unsigned long long head = (sizeof(T) - ((unsigned long long)src & (sizeof(T) - 1))) & (sizeof(T) - 1);
+  const unsigned long long h = head < n ? head : n;
+  if (threadIdx.x < h) dst[threadIdx.x] = src[threadIdx.x];
+  const unsigned long long nv = (n - h) / sizeof(T);
+  const T* s = reinterpret_cast<const T*>(src + h);
+  T* d = reinterpret_cast<T*>(dst + h);
+  for (unsigned long long i0 = threadIdx.x; i0 < nv; i0 += (unsigned long long)blockDim.x * U) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const unsigned long long i = i0 + (unsigned long long)u * blockDim.x;
+      if (i < nv) v[u] = s[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const unsigned long long i = i0 + (unsigned long long)u * blockDim.x;
+      if (i < nv) d[i] = v[u];
+    }
+  }
+  for (unsigned long long i = h + nv * sizeof(T) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
 __global__ __launch_bounds__(256) void k_multi_copy(const CopyDesc* __restrict__ d, int n) {
   constexpr unsigned long long PIECE = 64 << 10;
   for (int q = blockIdx.y; q < n; q += gridDim.y) {
     const CopyDesc c = d[q];
     for (unsigned long long b0 = (unsigned long long)blockIdx.x * PIECE; b0 < c.bytes;
          b0 += (unsigned long long)gridDim.x * PIECE) {
-      const unsigned long long b1 = c.bytes < b0 + PIECE ? c.bytes : b0 + PIECE;
+      const unsigned long long m = (c.bytes < b0 + PIECE ? c.bytes : b0 + PIECE) - b0;
       const char* src = (const char*)c.src + b0;
       char* dst = (char*)c.dst + b0;
-      unsigned long long done = 0;
-      if ((((unsigned long long)src | (unsigned long long)dst) & 15ULL) == 0) {
-        const unsigned long long nv = (b1 - b0) >> 4;
-        for (unsigned long long i = threadIdx.x; i < nv; i += blockDim.x)
-          reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-        done = nv << 4;
-      }
-      for (unsigned long long i = done + threadIdx.x; i < b1 - b0; i += blockDim.x) dst[i] = src[i];
+      const unsigned long long x = (unsigned long long)src ^ (unsigned long long)dst;
+      if (!(x & 15)) copy_units<uint4>(src, dst, m);
+      else if (!(x & 7)) copy_units<uint2>(src, dst, m);
+      else if (!(x & 3)) copy_units<uint32_t>(src, dst, m);
+      else if (!(x & 1)) copy_units<uint16_t>(src, dst, m);
+      else copy_units<uint8_t>(src, dst, m);
     }
   }
 }

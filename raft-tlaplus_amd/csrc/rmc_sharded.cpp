@@ -318,11 +318,12 @@ struct ShmComm : Comm {
 struct ShardBufs {
   DevBuf table, table2, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, small, bcnt, boff, btmp;
+  DevBuf mpc;  // k_materialize's piece map (logical shards)
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   void release() {
     for (DevBuf* b : {&table, &table2, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
                       &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &small, &bcnt,
-                      &boff, &btmp})
+                      &boff, &btmp, &mpc})
       b->release();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
@@ -854,7 +855,24 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       }
       // A generator whose winners all stay with it, in one local run (always
       // at W = 1), writes them straight into its next frontier; the others
-      // materialize into staging and send.
+      // materialize into staging and send -- unless every shard is on this
+      // device (logical shards): then each generator's k_materialize writes
+      // its winners straight into their owners' rows and trace records
+      // through a piece map, and no row crosses the transport.
+      const bool same_device = dynamic_cast<LocalComm*>(&comm) != nullptr;
+      std::vector<std::vector<MatPiece>> hpieces(W);  // alive until the round's stream sync
+      if (same_device) {
+        for (auto& pc : pcs) {
+          Shard* dsh = nullptr;
+          for (Shard& t : sh)
+            if (t.id == pc.d) dsh = &t;
+          const unsigned long long tr = dsh->tr_base[depth + 1] + pc.dl;
+          hpieces[pc.q].push_back({pc.a - (GW + go[pc.q]),
+                                   dsh->hf ? dsh->win_out.as<uint32_t>() + (pc.dl - dsh->fill0) * WD
+                                           : dsh->nxt + pc.dl * WD,
+                                   dsh->B->trp.as<unsigned long long>() + tr, dsh->B->trb.as<uint16_t>() + tr});
+        }
+      }
       std::vector<char> direct(W, 0);
       std::vector<unsigned long long> direct_dl(W, 0);
       for (int q = 0; q < W; q++) {
@@ -867,7 +885,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           first = false;
           expect = pc.dl + (pc.b - pc.a);
         }
-        direct[q] = ok && !first;
+        direct[q] = same_device || (ok && !first);
       }
       // ---- materialize winners (TLC order within the generator)
       for (int si = 0; si < NL; si++) {
@@ -875,7 +893,13 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         if (!s.n || !s.nwin) continue;
         LevelArgs a;
         round_args(a, s, c);
-        if (direct[s.id]) {
+        if (same_device) {
+          const std::vector<MatPiece>& hp = hpieces[s.id];
+          s.B->mpc.ensure(std::max<size_t>(64, hp.size() * sizeof(MatPiece)));
+          HIPCHK(hipMemcpyAsync(s.B->mpc.p, hp.data(), hp.size() * sizeof(MatPiece), hipMemcpyHostToDevice, stream));
+          a.pieces = s.B->mpc.as<MatPiece>();
+          a.npieces = (int)hp.size();
+        } else if (direct[s.id]) {
           a.out = s.hf ? s.win_out.as<uint32_t>() + (direct_dl[s.id] - s.fill0) * WD : s.nxt + direct_dl[s.id] * WD;
           a.out_base_global = s.tr_base[depth + 1] + direct_dl[s.id];
           a.tr_parent = s.B->trp.as<unsigned long long>();

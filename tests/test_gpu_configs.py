@@ -74,7 +74,7 @@ def full(name):
 
 def same(r, e):
     for k in ("generated", "distinct", "depth", "status", "levels", "hidden_var_collisions"):
-        assert r[k] == e[k], k
+        assert r[k] == e[k], (k, r["status"], r.get("message"))
 
 
 @pytest.mark.parametrize("name", sorted(EXH))
@@ -83,7 +83,9 @@ def test_rung_exhaustive_record(name):
     r = full(name)
     same(r, e)
     k = e["oracle_levels"]
-    assert r["levels"][:k] == LAD[name]["levels"][:k]
+    # the C oracle's run over the rung (tools/fold_oracle_rungs.py), else the ladder prefix of both oracles
+    pinned = e["oracle"]["levels"] if "oracle" in e else LAD[name]["levels"]
+    assert r["levels"][:k] == pinned[:k]
 
 
 @pytest.mark.parametrize("name", sorted(EXH))

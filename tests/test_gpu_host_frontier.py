@@ -107,10 +107,10 @@ def test_host_checkpoint_and_recover(tmp_path):
     same(model(g).check(recover_dir=tmp_path), g)
 
 
-def test_host_frontier_refused_elsewhere():
+def test_host_frontier_in_the_sharded_search_too():
+    """r04: the sharded search takes the option per shard (tests/test_gpu_sharded.py has its cases)."""
     g = SMALL["raft_n3v1e1"]
-    with pytest.raises(raftmc.RaftmcError, match="host_frontier"):
-        model(g).check_logical(2, host_frontier=1)
+    same(model(g).check_logical(2, host_frontier=1), g)
 
 
 @pytest.mark.parametrize("frac", ["0.0000001", "0.00002"])
