@@ -824,13 +824,21 @@ struct Arena {
                         &hf_stage[k], &hf_ilen32[k], &hf_ilen8[k], &hf_ioff[k], &hf_iscan[k]})
         b->release();
   }
+  // the second set of per-chunk arrays (two chunks in flight) and
+  // k_materialize's own status (its stream runs beside k_expand's)
+  DevBuf cslot2, cob2, cwin2, poff2, pn2, pwin2, ppos2, counters2, stmat;
+  void release_set2() {
+    for (DevBuf* b : {&cslot2, &cob2, &cwin2, &poff2, &pn2, &pwin2, &ppos2, &counters2}) b->release();
+  }
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   HostReadback* hrb = nullptr;
   void release() {
     if (hrb) (void)hipHostFree(hrb);
     hrb = nullptr;
-    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp})
+    for (DevBuf* b : {&table, &table2, &cslot, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf, &scantmp,
+                      &stmat})
       b->release();
+    release_set2();
     release_hf();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
@@ -1158,6 +1166,33 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   HIPCHK(upload_model(M));
   hipStream_t stream;
   HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  // Two chunks in flight while the frontiers are on the device: chunk i's
+  // k_materialize runs on mstream beside chunk i+1's k_expand / k_mark / scan
+  // on `stream` (k_materialize touches neither the fingerprint set nor the
+  // arrays of the chunk being expanded; chunk i+1's inserts carry larger
+  // ranks than chunk i's, so they cannot change a chunk-i winner).  The
+  // per-chunk arrays alternate between two sets.  RMC_NO_OVERLAP=1: one stream.
+  const bool pipe = opt->host_frontier != 1 && !(getenv("RMC_NO_OVERLAP") && atoi(getenv("RMC_NO_OVERLAP")) > 0);
+  hipStream_t mstream = stream;
+  hipEvent_t matdone[2] = {nullptr, nullptr}, ev_scan = nullptr;
+  if (pipe) {
+    HIPCHK(hipStreamCreateWithFlags(&mstream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&matdone[0], &matdone[1], &ev_scan}) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  struct MStreamGuard {
+    hipStream_t s, m;
+    hipEvent_t* ev;
+    ~MStreamGuard() {
+      if (m != s) {
+        (void)hipStreamSynchronize(m);
+        (void)hipStreamDestroy(m);
+      }
+      for (int i = 0; i < 3; i++)
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+  };
+  hipEvent_t evs[3] = {matdone[0], matdone[1], ev_scan};
+  MStreamGuard mguard{stream, mstream, evs};
   const size_t W = (size_t)M.words;
   res->state_bytes = (uint32_t)(W * 4);
   const auto t_model = std::chrono::steady_clock::now();
@@ -1221,6 +1256,22 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   ppos.ensure(chunk * 4);
   counters.ensure(1024);  // 8 per-XCD candidate counters, 128 B apart (k_expand)
   stbuf.ensure(sizeof(DevStatus));
+  A.stmat.ensure(sizeof(DevStatus));
+  if (pipe && !rec_host) {
+    A.cslot2.ensure(cand_cap * 8);
+    A.cob2.ensure(cand_cap * 4);
+    A.cwin2.ensure(cand_cap * 2);
+    for (DevBuf* b : {&A.poff2, &A.pn2, &A.pwin2, &A.ppos2}) b->ensure(chunk * 4);
+    A.counters2.ensure(1024);
+  }
+  DevBuf* const set_cslot[2] = {&cslot, &A.cslot2};
+  DevBuf* const set_cob[2] = {&cob, &A.cob2};
+  DevBuf* const set_cwin[2] = {&cwin, &A.cwin2};
+  DevBuf* const set_poff[2] = {&poff, &A.poff2};
+  DevBuf* const set_pn[2] = {&pn, &A.pn2};
+  DevBuf* const set_pwin[2] = {&pwin, &A.pwin2};
+  DevBuf* const set_ppos[2] = {&ppos, &A.ppos2};
+  DevBuf* const set_counters[2] = {&counters, &A.counters2};
   if (!A.hrb) HIPCHK(hipHostMalloc((void**)&A.hrb, sizeof(HostReadback), hipHostMallocDefault));
   HostReadback* const hrb = A.hrb;
   size_t stb = scan_temp_bytes(chunk);
@@ -1237,6 +1288,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     hst.max_msgs = 0;
     hst.hidden_coll = 0;
     HIPCHK(hipMemcpyAsync(stbuf.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(A.stmat.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
   };
   reset_status();
   HIPCHK(hipStreamSynchronize(stream));
@@ -1325,6 +1377,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   }
   EventTimer te, tm, tz;
   double expand_ms = 0, mark_ms = 0, mat_ms = 0;
+  unsigned mat_max_msgs = 0;  // k_materialize's largest |DOMAIN messages| (its own status buffer)
   unsigned long long expand_launches = 0, redos = 0;
   // hidden-variable collisions counted up to the last chunk that was kept: a
   // redone chunk's first k_mark has counted its collisions once already
@@ -1513,6 +1566,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   auto enter_hf = [&]() {
     auto th0 = std::chrono::steady_clock::now();
     HIPCHK(hipStreamSynchronize(stream));
+    HIPCHK(hipStreamSynchronize(mstream));  // the chunk in flight has written its rows
     try {  // while the device frontiers still hold their HBM (see reserve_windows)
       reserve_windows();
     } catch (OutOfDeviceMemory&) {
@@ -1598,7 +1652,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   bool stop_hf = false;
   unsigned stop_level = 0;
   auto fill_args = [&](LevelArgs& a, unsigned long long c0, unsigned long long n, unsigned level,
-                       const uint32_t* rows = nullptr) {
+                       const uint32_t* rows = nullptr, int set = 0) {
     memset(&a, 0, sizeof a);
     a.model = &M;
     a.frontier = rows ? rows : cur + c0 * W;
@@ -1608,14 +1662,14 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     a.floor = (cur_base + 1) << VAL_FLOOR_SHIFT;
     a.table = table.as<unsigned long long>();
     a.mask = slots - 1;
-    a.cand_slot = cslot.as<unsigned long long>();
-    a.cand_ob = cob.as<uint32_t>();
-    a.cand_win = cwin.as<uint16_t>();
-    a.par_off = poff.as<uint32_t>();
-    a.par_n = pn.as<uint32_t>();
-    a.par_win = pwin.as<uint32_t>();
-    a.par_pos = ppos.as<uint32_t>();
-    a.counters = counters.as<unsigned long long>();
+    a.cand_slot = set_cslot[set]->as<unsigned long long>();
+    a.cand_ob = set_cob[set]->as<uint32_t>();
+    a.cand_win = set_cwin[set]->as<uint16_t>();
+    a.par_off = set_poff[set]->as<uint32_t>();
+    a.par_n = set_pn[set]->as<uint32_t>();
+    a.par_win = set_pwin[set]->as<uint32_t>();
+    a.par_pos = set_ppos[set]->as<uint32_t>();
+    a.counters = set_counters[set]->as<unsigned long long>();
     a.cand_cap = cand_cap;
     a.st = stbuf.as<DevStatus>();
   };
@@ -1654,6 +1708,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       lvl_next_n = 0;
       enter_hf();
     }
+    if (hf) A.release_set2();  // host-frontier chunks use one array set
     unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
     if (cur_base + cur_n + 1 >= (1ULL << 38)) throw std::runtime_error("more than 2^38 states (the TLC-order rank field)");
@@ -1666,18 +1721,28 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     // after a stream sync.  True when it ended the search (status 3 set, or
     // hst holds the error/violation keys).
     bool mat_pending = false;
+    // k_materialize's status buffer (stmat) is its own: its invariant keys
+    // merge into hst here, its capacity flags end the search
     auto finish_mat = [&]() -> bool {
       mat_pending = false;
       float mms = 0;
       HIPCHK(hipEventElapsedTime(&mms, tz.a, tz.b));
       mat_ms += mms;
-      hst = hrb->mat;
-      if (hst.cap_flags) {
+      const DevStatus& mt = hrb->mat;
+      hst.inv_err_key = std::min(hst.inv_err_key, mt.inv_err_key);
+      hst.viol_key = std::min(hst.viol_key, mt.viol_key);
+      hst.err_key = std::min(hst.err_key, mt.err_key);
+      mat_max_msgs = std::max(mat_max_msgs, mt.max_msgs);
+      if (mt.cap_flags) {
         status = 3;
         message = "capacity overflow while materializing";
         return true;
       }
       return hst.err_key != ~0ULL || hst.inv_err_key != ~0ULL || hst.viol_key != ~0ULL;
+    };
+    auto sync_both = [&]() {
+      HIPCHK(hipStreamSynchronize(stream));
+      if (mstream != stream) HIPCHK(hipStreamSynchronize(mstream));
     };
     if (m->profile_level && level == m->profile_level && !hf) {
       // test hook (RMC_DIAG builds): k_expand on this level's first chunk,
@@ -1706,7 +1771,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       lvl_next_n = next_n;
       if (!hf && hf_opt == 0 && !hf_force_grow && level == hf_force_level && c0 > 0) {
         if (mat_pending) {
-          HIPCHK(hipStreamSynchronize(stream));
+          sync_both();
           if (finish_mat()) break;
         }
         enter_hf();
@@ -1716,13 +1781,15 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
         const unsigned long long need = distinct + next_n + (unsigned long long)((double)n * r * 1.25) + 1024;
         if (over_load(need)) {
           if (mat_pending) {  // the previous chunk may have ended the search: no growth for nothing
-            HIPCHK(hipStreamSynchronize(stream));
+            sync_both();
             if (finish_mat()) break;
           }
           t_fit(need);
         }
       }
       const int hs_k = ck & 1;  // host frontier: this chunk's windows
+      const bool pl = pipe && !hf;  // two chunks in flight (device frontiers)
+      const int ks = pl ? (int)(ck & 1) : 0;  // this chunk's array set
       if (hf && hwin_c0[hs_k] != c0) {  // parents not prefetched: copy them in (window free after chunk ck-2)
         HIPCHK(hipStreamWaitEvent(hs.cs, hs.mat[hs_k], 0));
         hf_load(hcur, c0, n, A.hwin_in[hs_k].p, hs_k, hs.cs);
@@ -1730,9 +1797,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
         hwin_c0[hs_k] = c0;
       }
       if (hf) HIPCHK(hipStreamWaitEvent(stream, hs.in[hs_k], 0));
+      if (pl) HIPCHK(hipStreamWaitEvent(stream, matdone[ks], 0));  // chunk ck-2's k_materialize read this set
       LevelArgs a;
-      fill_args(a, c0, n, level, hf ? A.hwin_in[hs_k].as<uint32_t>() : nullptr);
-      HIPCHK(hipMemsetAsync(counters.p, 0, 1024, stream));
+      fill_args(a, c0, n, level, hf ? A.hwin_in[hs_k].as<uint32_t>() : nullptr, ks);
+      HIPCHK(hipMemsetAsync(a.counters, 0, 1024, stream));
       HIPCHK(hipEventRecord(te.a, stream));
       launch_expand(M.spec, M.N, a, stream);
       HIPCHK(hipGetLastError());
@@ -1751,16 +1819,21 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
         hwin_c0[hs_k ^ 1] = c0 + n;
       }
       unsigned long long ncand = 0;
-      HIPCHK(hipMemcpyAsync(hrb->segc, counters.p, 1024, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(hrb->segc, a.counters, 1024, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&hrb->lastpos, a.par_pos + (n - 1), 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&hrb->lastwin, a.par_win + (n - 1), 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&hrb->st, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
+      sync_both();
       if (hf) hf_flush();  // the previous chunk's compact rows go out now that their sizes are known
       // the previous chunk's k_materialize outcome first: if it stopped the
       // search, this chunk's expand never happened as far as the counts go
       if (mat_pending && finish_mat()) break;
-      hst = hrb->st;
+      {  // expand / mark status of this chunk; the invariant keys k_materialize found stay merged
+        const unsigned long long ik = hst.inv_err_key, vk = hst.viol_key;
+        hst = hrb->st;
+        hst.inv_err_key = std::min(hst.inv_err_key, ik);
+        hst.viol_key = std::min(hst.viol_key, vk);
+      }
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, te.a, te.b));
       expand_ms += ms;
@@ -1879,11 +1952,19 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       a.tr_parent = trp.as<unsigned long long>();
       a.tr_bind = trb.as<uint16_t>();
       // positions from the scan are chunk-local; shift by next_n via out pointer
-      HIPCHK(hipEventRecord(tz.a, stream));
-      launch_materialize(M.spec, M.N, a, stream);
+      const bool plm = pl && !hf;  // (a mid-chunk switch to the host frontier drained mstream)
+      hipStream_t mst = plm ? mstream : stream;
+      if (plm) {  // after everything this chunk put on `stream` (growth included)
+        HIPCHK(hipEventRecord(ev_scan, stream));
+        HIPCHK(hipStreamWaitEvent(mstream, ev_scan, 0));
+      }
+      a.st = A.stmat.as<DevStatus>();
+      HIPCHK(hipEventRecord(tz.a, mst));
+      launch_materialize(M.spec, M.N, a, mst);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(tz.b, stream));
-      HIPCHK(hipMemcpyAsync(&hrb->mat, stbuf.p, sizeof hst, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipEventRecord(tz.b, mst));
+      HIPCHK(hipMemcpyAsync(&hrb->mat, A.stmat.p, sizeof hst, hipMemcpyDeviceToHost, mst));
+      if (plm) HIPCHK(hipEventRecord(matdone[ks], mstream));
       if (hf) {  // the new rows go to host pages (copy stream), after this k_materialize
         HIPCHK(hipEventRecord(hs.mat[hs_k], stream));
         hf_flush();  // (normally already flushed at this chunk's sync point)
@@ -1898,13 +1979,13 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       c0 += n;
       ck++;
       if (hst.err_key != ~0ULL) {  // this chunk's expand hit an evaluation error: the search stops here
-        HIPCHK(hipStreamSynchronize(stream));
+        sync_both();
         finish_mat();
         break;
       }
     }
     if (mat_pending) {
-      HIPCHK(hipStreamSynchronize(stream));
+      sync_both();
       finish_mat();
     }
     if (hf) {
@@ -2036,6 +2117,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     HIPCHK(hipDeviceSynchronize());
   }
   HIPCHK(hipStreamSynchronize(stream));
+  HIPCHK(hipStreamSynchronize(mstream));
   // ---- exact counts at the failing state.  TLC stops at the first violating
   // (or erroring) state in its exploration order; the chunks run whole, so
   // the failing chunk is expanded and marked again (its inserts are idempotent)
@@ -2179,11 +2261,13 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   res->materialize_ms = mat_ms;
   res->expand_launches = expand_launches;
   res->hash_capacity = slots;
+  hst.max_msgs = std::max(hst.max_msgs, mat_max_msgs);
   res->max_msgs = hst.max_msgs;
   {
     size_t b = 0;
     for (DevBuf* x : {&A.table, &A.table2, &A.cslot, &A.cob, &A.cwin, &A.poff, &A.pn, &A.pwin, &A.ppos, &A.counters,
-                      &A.stbuf, &A.scantmp})
+                      &A.stbuf, &A.scantmp, &A.stmat, &A.cslot2, &A.cob2, &A.cwin2, &A.poff2, &A.pn2, &A.pwin2, &A.ppos2,
+                      &A.counters2})
       b += x->bytes;
     for (int k = 0; k < 2; k++)
       for (DevBuf* x : {&A.hwin_in[k], &A.hwin_out[k], &A.hf_pack[k], &A.hf_olen32[k], &A.hf_olen8[k], &A.hf_ooff[k],

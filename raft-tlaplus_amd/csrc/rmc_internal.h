@@ -180,6 +180,11 @@ struct GrowBuf {
     }
   }
   void grow_copy(size_t b, size_t /*keep*/) { ensure(b); }  // contents are always kept
+  // Unmapped and released chunks return their HBM only when the address
+  // range is freed too (measured: profiles/r04/vmm_free_probe.txt -- 80 GiB
+  // stayed in use after hipMemUnmap + hipMemRelease and came back at
+  // hipMemAddressFree), so the range goes as well; the next ensure()
+  // reserves a new one.
   void release() {
     if (vmm) {
       size_t off = 0;
@@ -189,17 +194,17 @@ struct GrowBuf {
         off += c.second;
       }
       chunks.clear();
-      bytes = 0;  // the address range stays reserved for reuse
-    } else {
-      if (p) (void)hipFree(p);
-      p = nullptr;
-      bytes = 0;
+      if (p) (void)hipMemAddressFree(p, reserved);
+      vmm = false;
+      tried = false;
+      reserved = 0;
+    } else if (p) {
+      (void)hipFree(p);
     }
+    p = nullptr;
+    bytes = 0;
   }
-  ~GrowBuf() {
-    release();
-    if (vmm && p) (void)hipMemAddressFree(p, reserved);
-  }
+  ~GrowBuf() { release(); }
   template <class T>
   T* as() const { return (T*)p; }
 };

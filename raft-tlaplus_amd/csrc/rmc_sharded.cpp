@@ -379,11 +379,19 @@ static unsigned long long local_count(unsigned long long P, int W, unsigned long
   return full * CH + (unsigned long long)part;
 }
 
-// Room for need_entries at <= 0.5 load (OutOfDeviceMemory ends the check with status 3).
-static void table_grow(Shard& s, unsigned long long need_entries, hipStream_t stream) {
-  if (need_entries * 2 <= s.slots) return;
+// Room for need_entries (OutOfDeviceMemory ends the check with status 3): at
+// <= 0.5 load while the shard's set is at most 1/W of 32 GiB, <= 0.75 beyond --
+// the single-GPU search's thresholds (rmc_engine.cpp over_load) for the W
+// shards' sets together, so a shard's set is 1/W of the single search's and
+// not twice that (the needs are upper bounds: every candidate counted new).
+static void table_grow(Shard& s, unsigned long long need_entries, hipStream_t stream, int W) {
+  const unsigned long long small = (32ULL << 30) / (unsigned long long)W;
+  auto fits = [&](unsigned long long sl) {
+    return sl * 16 <= small ? need_entries * 2 <= sl : need_entries * 4 <= sl * 3;
+  };
+  if (fits(s.slots)) return;
   unsigned long long nslots = s.slots;
-  while (need_entries * 2 > nslots) nslots <<= 1;
+  while (!fits(nslots)) nslots <<= 1;
   DevBuf& nt = s.B->table2;
   nt.ensure(nslots * 16);
   HIPCHK(hipMemsetAsync(nt.p, 0xFF, nslots * 16, stream));
@@ -632,7 +640,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         const double r = std::max(rate, done ? (double)GW / (double)done : 0.0);
         for (Shard& s : sh) {
           s.n = s.ncur > c * CH ? std::min(CH, s.ncur - c * CH) : 0;
-          if (!opt->grow_on_overflow) table_grow(s, s.entries + (unsigned long long)((double)s.n * r * 1.25) + 1024, stream);
+          if (!opt->grow_on_overflow) table_grow(s, s.entries + (unsigned long long)((double)s.n * r * 1.25) + 1024, stream, W);
         }
       }
       // ---- expand: fp + key per candidate; the fps this shard owns are inserted here
@@ -668,7 +676,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         // redo the round on every shard (inserts are idempotent; nothing else
         // of the round has happened yet)
         for (Shard& s : sh) {
-          if (s.hst.cap_flags) table_grow(s, s.slots, stream);  // doubles
+          if (s.hst.cap_flags) table_grow(s, s.slots, stream, W);  // doubles
           s.hst.cap_flags = 0;
           HIPCHK(hipMemcpyAsync((char*)s.B->stbuf.p + offsetof(DevStatus, cap_flags), &s.hst.cap_flags, 4,
                                 hipMemcpyHostToDevice, stream));
@@ -752,7 +760,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         // ---- owners insert, then mark
         for (Shard& s : sh) {
           // exact bound: the local candidates (inserted) and every received record new
-          table_grow(s, s.entries + s.ncand + s.nrecv, stream);
+          table_grow(s, s.entries + s.ncand + s.nrecv, stream, W);
           launch_insert_recv(s.B->recv.as<unsigned long long>(), s.nrecv, s.B->table.as<unsigned long long>(),
                              s.slots - 1, floor, s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
           HIPCHK(hipGetLastError());
@@ -1116,6 +1124,24 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       b += x->bytes;
     for (GrowBuf* x : {&B.fa, &B.fb, &B.trp, &B.trb}) b += x->bytes;
     res->device_bytes = std::max<uint64_t>(res->device_bytes, b);
+    if (opt->verbose || (getenv("RMC_VERBOSE") && atoi(getenv("RMC_VERBOSE")) > 0)) {
+      auto g = [](std::initializer_list<size_t> l) {
+        size_t t = 0;
+        for (size_t v : l) t += v;
+        return t / 1073741824.0;
+      };
+      fprintf(stderr,
+              "[rmc] shard %d HBM GiB: set %.1f+%.1f candidates %.1f exchange %.1f staging %.1f frontiers %.1f "
+              "trace %.1f host windows %.1f other %.1f (total %.1f)\n",
+              s.id, B.table.bytes / 1073741824.0, B.table2.bytes / 1073741824.0,
+              g({B.cfp.bytes, B.cval.bytes, B.cob.bytes, B.cwin.bytes, B.perm.bytes}),
+              g({B.send.bytes, B.recv.bytes, B.rslot.bytes, B.rflag.bytes, B.sflag.bytes}),
+              g({B.stage.bytes, B.stp.bytes, B.stb.bytes}), g({B.fa.bytes, B.fb.bytes}), g({B.trp.bytes, B.trb.bytes}),
+              g({s.win_in.bytes, s.win_out.bytes, s.io.pack.bytes, s.io.stage.bytes}),
+              g({B.poff.bytes, B.pn.bytes, B.pwin.bytes, B.ppos.bytes, B.scantmp.bytes, B.bcnt.bytes, B.boff.bytes,
+                 B.btmp.bytes}),
+              b / 1073741824.0);
+    }
   }
   {  // same-level hidden-variable collisions, summed over the shards
     for (int i = 0; i < NL; i++) {
