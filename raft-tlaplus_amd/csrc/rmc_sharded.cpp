@@ -433,6 +433,16 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
   const int NL = (int)comm.local.size();
   if (W > 64) throw std::runtime_error("at most 64 shards");
+  {  // cached shard buffers are sized for the partition that grew them: a
+     // check with another shard count starts from nothing (a W = 2 check's
+     // shard 0 holds half of every level, twice what a W = 4 shard needs)
+    static std::map<int, int> last_world;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    int& lw = last_world[dev];
+    if (lw && lw != W) release_shard_buffers();
+    lw = W;
+  }
 
   std::vector<Shard> sh(NL);
   // the per-shard host frontier: one pinned-page pool for this process's shards

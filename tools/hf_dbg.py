@@ -43,6 +43,8 @@ if os.environ.get('DBG_SHARDS'):  # the per-shard breakdown of the bench rung at
         run('logical %d' % W, lambda: model(g).check_logical(W, verbose=True))
     del os.environ['RMC_VERBOSE']
     release('after shards')
+    if os.environ['DBG_SHARDS'] == 'only':
+        sys.exit(0)
 for n in sorted(LAD):
     run('prefix ' + n, lambda: model(LAD[n]).check(max_depth=LAD[n]["depth"]))
 for n in BEYOND:
