@@ -1171,8 +1171,13 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   // on `stream` (k_materialize touches neither the fingerprint set nor the
   // arrays of the chunk being expanded; chunk i+1's inserts carry larger
   // ranks than chunk i's, so they cannot change a chunk-i winner).  The
-  // per-chunk arrays alternate between two sets.  RMC_NO_OVERLAP=1: one stream.
-  const bool pipe = opt->host_frontier != 1 && !(getenv("RMC_NO_OVERLAP") && atoi(getenv("RMC_NO_OVERLAP")) > 0);
+  // per-chunk arrays alternate between two sets.  Opt-in (RMC_OVERLAP=1):
+  // measured on the bench workload (profiles/r04/bench_r04o_*.json) the two
+  // kernels contend for the same memory system -- overlapped, k_expand takes
+  // 1,057 ms per check instead of 755 and k_materialize 420 instead of 347 --
+  // and the check gains 0.5% (1.216-1.219 s vs 1.223-1.224 s) for a second
+  // 7.6 GB candidate set.
+  const bool pipe = opt->host_frontier != 1 && getenv("RMC_OVERLAP") && atoi(getenv("RMC_OVERLAP")) > 0;
   hipStream_t mstream = stream;
   hipEvent_t matdone[2] = {nullptr, nullptr}, ev_scan = nullptr;
   if (pipe) {

@@ -14,10 +14,11 @@
 // No level field is needed: parents of level L+1's states are level L's, and
 // global indices grow level by level, so an entry is from an EARLIER level iff
 // its val < floor = (first global index of the parents' level + 1) << 26.  An
-// insert that finds its fingerprint from an earlier level (most successors:
-// 72% on the bench workload) therefore leaves the entry untouched -- one CAS
-// that fails (and a read of the same, L2-resident line) and no write -- and
-// only new fingerprints and same-level duplicates pay the atomicMin.
+// insert that finds its fingerprint from an earlier level leaves the entry
+// untouched (plain loads, no write); only new fingerprints and same-level
+// duplicates pay the atomicMin.  On the bench workload nearly every duplicate
+// is a same-level one (profiles/r04/fpstats_raft_n3v2e2.txt: 4.09e9 CAS, 1.89e9
+// won; 5.21e9 atomicMin for 6.75e9 inserts).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "rmc_engine.h"
@@ -37,13 +38,20 @@ constexpr int VAL_FLOOR_SHIFT = 26;  // floor = (global index + 1) << 26 (rank <
 // a key's home slot in a table of 2^a slots is the prefix of its home slot in
 // one of 2^b >= 2^a slots, so a rehash into a larger table walks the new table
 // in address order.
+//
+// RMC_SLOT_ALIGN = 4: the home slot is rounded down to a multiple of 4 (a
+// 64 B aligned group of 16 B entries), so the insert's first group load
+// touches one aligned 64 B block instead of straddling two 3 times in 4.
+#ifndef RMC_SLOT_ALIGN
+#define RMC_SLOT_ALIGN 1
+#endif
 __host__ __device__ __forceinline__ unsigned long long fp_slot(unsigned long long fp, unsigned long long mask) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int sh = __clzll((long long)mask);
 #else
   const int sh = __builtin_clzll(mask);
 #endif
-  return ((fp * 0x9E3779B97F4A7C15ULL) >> sh) & mask;
+  return ((fp * 0x9E3779B97F4A7C15ULL) >> sh) & mask & ~(unsigned long long)(RMC_SLOT_ALIGN - 1);
 }
 
 // Owner of a fingerprint among W shards (sharded search): multiply-shift range
@@ -159,8 +167,20 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
   if (RMC_FP_FAST > 0 && slot + (RMC_FP_FAST - 1) <= mask) {
     const ulonglong2* E = reinterpret_cast<const ulonglong2*>(T) + slot;
     ulonglong2 e[RMC_FP_FAST > 0 ? RMC_FP_FAST : 1];
+#ifdef RMC_FP_COHERENT
+    // agent-scope loads: served coherently with the other XCDs' atomics
+    // instead of from a possibly stale line in this XCD's L2 (a stale EMPTY
+    // sends a same-level duplicate into a CAS that fails)
+#pragma unroll
+    for (int q = 0; q < RMC_FP_FAST; q++) {
+      e[q].x = __hip_atomic_load(T + 2 * (slot + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e[q].y = __hip_atomic_load(T + 2 * (slot + q) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    (void)E;
+#else
 #pragma unroll
     for (int q = 0; q < RMC_FP_FAST; q++) e[q] = E[q];
+#endif
     int k = RMC_FP_FAST;
     unsigned long long kv = 0;
     bool found = false;
@@ -185,8 +205,16 @@ __device__ __forceinline__ unsigned long long fpset_insert(unsigned long long* T
       return slot;
     }
     if (prev == fp) {
+#ifdef RMC_FP_BLINDMIN
+      // claimed since the group load: the atomicMin without reading the value
+      // first (no dependent round trip; an earlier level's value is below
+      // floor <= val, so the min leaves it unchanged)
+      FPSTAT(FPS_MIN);
+      atomicMin(e + 1, val);
+#else
       const unsigned long long cur = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (cur >= floor && val < cur) { FPSTAT(FPS_MIN); atomicMin(e + 1, val); }
+#endif
       return slot;
     }
     slot = (slot + 1) & mask;
