@@ -18,6 +18,7 @@ with W shards on one GPU (a measurement of the protocol's overhead).
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 """
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -98,11 +99,25 @@ def cpu_baseline(module, cfg_path, seconds=15.0):
     cores, model = host_cores()
     m = raftmc.Model(module=module, cfg_path=os.path.join(ROOT, cfg_path))
     r = m.check_cpu(workers=cores, time_limit=seconds)
-    return dict(value=r["distinct"] / max(r["seconds"], 1e-9), unit="distinct states/s", cores=cores,
-                kind="port", cpu_model=model,
-                sample="librmc CPU engine (rmc_check_cpu, %d threads) on the same cfg until the first level boundary "
-                       "past %.0f s: %d levels, %d distinct, %d generated in %.1f s (status %s)"
-                       % (cores, seconds, r["depth"], r["distinct"], r["generated"], r["seconds"], r["status"]))
+    out = dict(value=r["distinct"] / max(r["seconds"], 1e-9), unit="distinct states/s", cores=cores,
+               kind="port", cpu_model=model,
+               sample="librmc CPU engine (rmc_check_cpu, %d threads) on the same cfg until the first level boundary "
+                      "past %.0f s: %d levels, %d distinct, %d generated in %.1f s (status %s)"
+                      % (cores, seconds, r["depth"], r["distinct"], r["generated"], r["seconds"], r["status"]))
+    # the whole check on a CPU, for time-to-exhaust: the C oracle's committed
+    # run over this cfg (not timed here; measured in the build container)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "oracle_*.json")), reverse=True):
+        try:
+            o = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if o.get("cfg_path") == cfg_path and o.get("status") == "ok":
+            out["full_check"] = dict(seconds=o["seconds"], threads=o["threads"], distinct=o["distinct"],
+                                     source=os.path.relpath(path, ROOT),
+                                     what="C oracle (exact canonical forms) over the whole check, in the build "
+                                          "container, not on this host")
+            break
+    return out
 
 
 def main():

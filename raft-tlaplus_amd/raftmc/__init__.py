@@ -14,7 +14,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "librmc.so")
+# RAFTMC_BUILD=<dir under raft-tlaplus_amd/>: load an in-tree variant build
+# (A/B measurements); the default is build/
+LIB_PATH = os.path.join(os.path.dirname(_HERE), os.environ.get("RAFTMC_BUILD", "build"), "librmc.so")
 
 STATUS = {0: "ok", 1: "violation", 2: "error", 3: "capacity", 4: "stopped"}
 
