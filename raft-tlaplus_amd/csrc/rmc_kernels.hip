@@ -240,9 +240,13 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
   // rows are a multiple of 4 words (16 B aligned): 16 B loads, 4 LDS writes each
   const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
+  // (Staging only each row's used words -- headers first, then the 16 B units
+  // up to the last message -- was measured and rejected: k_expand 852 vs 829
+  // ms, k_materialize 447 vs 432 per check; the dependent header load costs
+  // more than the bytes it saves.  profiles/r04/ab_stage_trim_r04u.txt)
   for (int q = tid; q < np * (words >> 2); q += 256) {
-    const uint4 v = src[q];
     const int w = q << 2, p = w / words;
+    const uint4 v = src[q];
     uint32_t* d = sS + p * L.Wp + (w - p * words);
     d[0] = v.x;
     d[1] = v.y;
@@ -834,8 +838,8 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   const uint32_t start = par_off[p0];
   const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
   for (int q = tid; q < np * (words >> 2); q += MAT_T) {
-    const uint4 v = src[q];
     const int w = q << 2, p = w / words;
+    const uint4 v = src[q];
     uint32_t* d = sS + p * Wp + (w - p * words);
     d[0] = v.x;
     d[1] = v.y;
