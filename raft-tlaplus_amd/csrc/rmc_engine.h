@@ -99,13 +99,14 @@ void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_
                         unsigned int* blk_counts, hipStream_t s);
 void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
                    unsigned long long n, int W, const unsigned int* blk_off, unsigned long long* send, uint32_t* perm,
-                   hipStream_t s);
+                   hipStream_t s, const unsigned long long* dbase = nullptr);
 void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
                         unsigned long long mask, unsigned long long floor, unsigned long long* recv_slot, DevStatus* st,
                         hipStream_t s);
 void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
                       const unsigned long long* table, unsigned long long floor, uint8_t* flag,
-                      unsigned long long* newcount, DevStatus* st, hipStream_t s);
+                      unsigned long long* newcount, DevStatus* st, hipStream_t s,
+                      const unsigned long long* fbase = nullptr, const unsigned long long* rseg = nullptr, int W = 0);
 // k_mark for the sharded search: a (cand_ob, cand_slot, cand_val,
 // par_off/par_n -> cand_win/par_win, table/mask/floor, pbase, st); moved = the
 // table grew since k_expand (local-owner candidates are found by fp)

@@ -956,10 +956,17 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
                                                 const unsigned long long* __restrict__ cand_val,
                                                 const uint32_t* __restrict__ cand_ob, unsigned long long n, int W,
                                                 const unsigned int* __restrict__ blk_off,
-                                                unsigned long long* __restrict__ send, uint32_t* __restrict__ perm) {
+                                                unsigned long long* __restrict__ send, uint32_t* __restrict__ perm,
+                                                const unsigned long long* __restrict__ dbase) {
   __shared__ unsigned int h[BUCKET_MAXW];
+  __shared__ unsigned long long db[BUCKET_MAXW];
   const unsigned nb = gridDim.x;
-  if (threadIdx.x < W) h[threadIdx.x] = blk_off[(size_t)threadIdx.x * nb + blockIdx.x];
+  if (threadIdx.x < W) {
+    h[threadIdx.x] = blk_off[(size_t)threadIdx.x * nb + blockIdx.x];
+    // dbase (shards sharing the device): record `pos` of owner o goes to the
+    // byte address db[o] + 16 * pos -- straight into o's receive buffer
+    db[threadIdx.x] = dbase ? dbase[threadIdx.x] : (unsigned long long)send;
+  }
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -968,9 +975,11 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
     return;
   }
   unsigned long long fp = cand_fp[t];
-  unsigned pos = atomicAdd(&h[fp_owner(fp, W)], 1u);
-  send[2ULL * pos] = fp;
-  send[2ULL * pos + 1] = cand_val[t];
+  const int o = fp_owner(fp, W);
+  unsigned pos = atomicAdd(&h[o], 1u);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(db[o] + 16ULL * pos);
+  dst[0] = fp;
+  dst[1] = cand_val[t];
   perm[t] = pos;
 }
 
@@ -1018,9 +1027,20 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
                                                    const unsigned long long* __restrict__ recv_slot,
                                                    unsigned long long n, const unsigned long long* __restrict__ table,
                                                    unsigned long long floor, uint8_t* __restrict__ flag,
-                                                   unsigned long long* __restrict__ newcount, DevStatus* st) {
+                                                   unsigned long long* __restrict__ newcount, DevStatus* st,
+                                                   const unsigned long long* __restrict__ fbase,
+                                                   const unsigned long long* __restrict__ rseg, int W) {
   // RECV_U records per thread, their table reads issued together (as k_insert_recv)
   constexpr int U = RECV_U;
+  // fbase (shards sharing the device): the flag of record j, received from
+  // source q (rseg[q] <= j < rseg[q+1]), goes straight to the byte address
+  // fbase[q] + j in q's flag buffer
+  __shared__ unsigned long long sfb[BUCKET_MAXW], srs[BUCKET_MAXW + 1];
+  if (fbase) {
+    if (threadIdx.x < W) sfb[threadIdx.x] = fbase[threadIdx.x];
+    if (threadIdx.x <= W) srs[threadIdx.x] = rseg[threadIdx.x];
+    __syncthreads();
+  }
   const unsigned long long j0 = (unsigned long long)blockIdx.x * blockDim.x * U + threadIdx.x;
   unsigned long long rs[U], tv[U];
 #pragma unroll
@@ -1042,7 +1062,16 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
       w = fpset_won(tv[u], mine >> VAL_RANK_SHIFT, floor, mine, c);
       colls += c;
     }
-    flag[j] = w ? 1 : 0;
+    if (fbase) {
+      int lo = 0, hi = W - 1;  // source q: srs[q] <= j < srs[q+1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (srs[mid] <= j) lo = mid; else hi = mid - 1;
+      }
+      *reinterpret_cast<uint8_t*>(sfb[lo] + j) = w ? 1 : 0;
+    } else {
+      flag[j] = w ? 1 : 0;
+    }
     wins += w;
   }
   if (colls) atomicAdd(&st->hidden_coll, (unsigned long long)colls);
@@ -1135,10 +1164,10 @@ void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_
 }
 void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,
                    unsigned long long n, int W, const unsigned int* blk_off, unsigned long long* send, uint32_t* perm,
-                   hipStream_t s) {
+                   hipStream_t s, const unsigned long long* dbase) {
   if (!n) return;
   hipLaunchKernelGGL(k_bucket, dim3((unsigned)bucket_blocks(n)), dim3(256), 0, s, cand_fp, cand_val, cand_ob, n, W,
-                     blk_off, send, perm);
+                     blk_off, send, perm, dbase);
 }
 void launch_insert_recv(const unsigned long long* recv, unsigned long long n, unsigned long long* table,
                         unsigned long long mask, unsigned long long floor, unsigned long long* recv_slot, DevStatus* st,
@@ -1149,10 +1178,11 @@ void launch_insert_recv(const unsigned long long* recv, unsigned long long n, un
 }
 void launch_mark_recv(const unsigned long long* recv, const unsigned long long* recv_slot, unsigned long long n,
                       const unsigned long long* table, unsigned long long floor, uint8_t* flag,
-                      unsigned long long* newcount, DevStatus* st, hipStream_t s) {
+                      unsigned long long* newcount, DevStatus* st, hipStream_t s, const unsigned long long* fbase,
+                      const unsigned long long* rseg, int W) {
   if (!n) return;
   hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 256 * RECV_U - 1) / (256 * RECV_U))), dim3(256), 0, s, recv,
-                     recv_slot, n, table, floor, flag, newcount, st);
+                     recv_slot, n, table, floor, flag, newcount, st, fbase, rseg, W);
 }
 void launch_mark_gen(const LevelArgs& a, int moved, const uint32_t* perm, const uint8_t* flag_back,
                      unsigned long long* newcount, hipStream_t s) {

@@ -318,12 +318,13 @@ struct ShmComm : Comm {
 struct ShardBufs {
   DevBuf table, table2, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
   DevBuf send, perm, recv, rslot, rflag, sflag, stage, stp, stb, small, bcnt, boff, btmp;
-  DevBuf mpc;  // k_materialize's piece map (logical shards)
+  DevBuf mpc;   // k_materialize's piece map (logical shards)
+  DevBuf xmap;  // logical shards: record destinations (k_bucket), flag destinations + recv segments (k_mark_recv)
   GrowBuf fa, fb, trp, trb;  // frontiers and trace records grow in place
   void release() {
     for (DevBuf* b : {&table, &table2, &cfp, &cval, &cob, &cwin, &poff, &pn, &pwin, &ppos, &counters, &stbuf,
                       &scantmp, &send, &perm, &recv, &rslot, &rflag, &sflag, &stage, &stp, &stb, &small, &bcnt,
-                      &boff, &btmp, &mpc})
+                      &boff, &btmp, &mpc, &xmap})
       b->release();
     for (GrowBuf* b : {&fa, &fb, &trp, &trb}) b->release();
   }
@@ -445,6 +446,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   }
 
   std::vector<Shard> sh(NL);
+  // every shard on this device, driven by this process (logical shards)
+  const bool same_device = dynamic_cast<LocalComm*>(&comm) != nullptr;
   // the per-shard host frontier: one pinned-page pool for this process's shards
   HostPagePool pool;
   pool.page_bytes = std::max<size_t>(WD * 4, 256ULL << 20);
@@ -706,6 +709,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         message = "capacity overflow (sharded search, code " + std::to_string(e) + ")";
         break;
       }
+      std::vector<std::vector<unsigned long long>> xmaps(NL);  // (host side of xmap, alive until the round's sync)
       if (W > 1) {
         // ---- remote-owner candidates: bucket by owner (per-block histograms,
         //      owner-major scan), exchange counts
@@ -746,13 +750,38 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
           s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
           s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
+        }
+        // Shards sharing the device (logical shards): k_bucket writes each
+        // record straight into its owner's receive segment and k_mark_recv
+        // each flag straight back into its generator's flag buffer, so neither
+        // exchange step copies (the byte-address maps per shard: [0, W)
+        // record destinations by owner, [W, 2W) flag destinations by source,
+        // [2W, 3W] the receive segments).
+        if (same_device) {
+          for (int i = 0; i < NL; i++) {
+            Shard& s = sh[i];
+            std::vector<unsigned long long>& xm = xmaps[i];
+            xm.assign(3 * W + 1, 0);
+            for (int o = 0; o < W; o++) {
+              const Shard& d = sh[o];  // LocalComm: shard ids are 0..W-1 in order
+              xm[o] = (unsigned long long)d.B->recv.p + 16ULL * (d.rseg_off[s.id] - s.seg_off[o]);
+              xm[W + o] = (unsigned long long)d.B->sflag.p + (d.seg_off[s.id] - s.rseg_off[o]);
+            }
+            for (int q = 0; q <= W; q++) xm[2 * W + q] = s.rseg_off[q];
+            s.B->xmap.ensure(xm.size() * 8);
+            HIPCHK(hipMemcpyAsync(s.B->xmap.p, xm.data(), xm.size() * 8, hipMemcpyHostToDevice, stream));
+          }
+        }
+        for (int i = 0; i < NL; i++) {
+          Shard& s = sh[i];
           launch_bucket(s.B->cfp.as<unsigned long long>(), s.B->cval.as<unsigned long long>(), s.B->cob.as<uint32_t>(),
                         s.ncand, W, s.B->boff.as<unsigned int>(), s.B->send.as<unsigned long long>(),
-                        s.B->perm.as<uint32_t>(), stream);
+                        s.B->perm.as<uint32_t>(), stream,
+                        same_device ? s.B->xmap.as<unsigned long long>() : nullptr);
           HIPCHK(hipGetLastError());
         }
         // ---- (fp, key) records to their owners
-        {
+        if (!same_device) {
           std::vector<Xfer> x;
           for (int q = 0; q < W; q++)
             for (int d = 0; d < W; d++) {
@@ -777,13 +806,14 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         }
         for (Shard& s : sh) {
           unsigned long long* nc = s.B->counters.as<unsigned long long>() + 1;
+          const unsigned long long* xm = same_device ? s.B->xmap.as<unsigned long long>() : nullptr;
           launch_mark_recv(s.B->recv.as<unsigned long long>(), s.B->rslot.as<unsigned long long>(), s.nrecv,
                            s.B->table.as<unsigned long long>(), floor, s.B->rflag.as<uint8_t>(), nc,
-                           s.B->stbuf.as<DevStatus>(), stream);
+                           s.B->stbuf.as<DevStatus>(), stream, xm ? xm + W : nullptr, xm ? xm + 2 * W : nullptr, W);
           HIPCHK(hipGetLastError());
         }
         // ---- win flags back to the generators (reverse of the record exchange)
-        {
+        if (!same_device) {
           std::vector<Xfer> x;
           for (int q = 0; q < W; q++)
             for (int d = 0; d < W; d++) {
@@ -877,7 +907,6 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       // device (logical shards): then each generator's k_materialize writes
       // its winners straight into their owners' rows and trace records
       // through a piece map, and no row crosses the transport.
-      const bool same_device = dynamic_cast<LocalComm*>(&comm) != nullptr;
       std::vector<std::vector<MatPiece>> hpieces(W);  // alive until the round's stream sync
       if (same_device) {
         for (auto& pc : pcs) {
