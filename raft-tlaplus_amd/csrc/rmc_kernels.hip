@@ -131,9 +131,6 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
 #ifdef RMC_TILE_DEDUP
   const int hash_end = L.off_Hash + DEDUP * 12;
   L.bytes = o > hash_end ? o : hash_end;
-#elif defined(RMC_WAVE_DEDUP)
-  const int hash_end = L.off_Hash + 4 * WAVE * 12;  // per wave: 64 fingerprints + 64 lane ids
-  L.bytes = o > hash_end ? o : hash_end;
 #else
   L.bytes = o;
 #endif
@@ -594,88 +591,12 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     }
   }
 #endif
-#ifdef RMC_WAVE_DEDUP
-  // Wave-level dedup (FPW 1): a wave's 64 successors are consecutive in TLC
-  // order, and siblings of one tile often reach the same state (commuting
-  // actions); their inserts raced -- the losing CAS and the extra atomicMin.
-  // Per wave a 64-slot LDS table keeps each fingerprint's lowest lane (the
-  // first in TLC order, the lowest rank); only that lane probes the HBM set,
-  // the others take its slot (they carry larger ranks: their atomicMin could
-  // never change the entry, and k_mark reads the entry as if they had
-  // inserted).  No block barrier: LDS operations of one wave complete in
-  // order.
-  if constexpr (FPW == 1) {
-    if (!diag) {
-      const int lane = tid & (WAVE - 1);
-      unsigned long long* wK = reinterpret_cast<unsigned long long*>(lds + L.off_Hash) + (tid >> 6) * WAVE;
-      uint32_t* wL = reinterpret_cast<uint32_t*>(lds + L.off_Hash + 4 * WAVE * 8) + (tid >> 6) * WAVE;
-      for (int base = 0; base < total; base += 256) {  // wave-uniform trip count
-        const int idx = base + tid;
-        const bool act = idx < total;
-        unsigned long long fp = 0, val = 0, t = 0;
-        uint32_t obw = OB_ERR, local = 0;
-        bool ins = false;
-        unsigned long long slot = CAND_DUP;
-        if (act) {
-          int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
-          while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if ((int)sBase[mid] <= idx) lo = mid; else hi = mid - 1;
-          }
-          const int p = lo;
-          const int ord = select_bit(sOrd + p * ordw, idx - (int)sBase[p]);
-          const int b = sO2b[ord];
-          PState<SPEC, N> s{sS + p * L.Wp};
-          Delta d;
-          eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
-          t = gbase + (unsigned long long)idx;
-          const unsigned long long pg = pbase + p0 + p;
-          obw = ((uint32_t)d.ordinal << 16) | (uint32_t)b;
-          if (d.err) {
-            obw |= OB_ERR;
-          } else {
-            val = ((((pg + 1) << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
-                  (unsigned long long)hidden_of<SPEC>(d.hdr);
-            fp = delta_fp_sums<SPEC, N>(s, cM, d, sums1<N>(sMS[p]));
-            if (sharded && fp_owner(fp, sharded) != shard_self) {
-              slot = fp;  // a remote owner inserts it (k_insert_recv)
-              cand_val[t] = val;
-            } else {
-              ins = true;
-              if (sharded) {
-                cand_val[t] = fp;
-                local = OB_LOCAL;
-              }
-            }
-          }
-        }
-        __hip_atomic_store(&wK[lane], EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __hip_atomic_store(&wL[lane], (uint32_t)WAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        int h = 0;
-        if (ins) {
-          h = (int)((fp ^ (fp >> 29) ^ (fp >> 47)) & (WAVE - 1));
-          for (;;) {  // at most 64 keys in 64 slots: a slot is always found
-            const unsigned long long prev = atomicCAS(&wK[h], EMPTY, fp);
-            if (prev == EMPTY || prev == fp) break;
-            h = (h + 1) & (WAVE - 1);
-          }
-          atomicMin(&wL[h], (uint32_t)lane);
-        }
-        const int first = ins ? (int)__hip_atomic_load(&wL[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : lane;
-        unsigned long long raw = EMPTY;
-        if (ins && first == lane) raw = fpset_insert(table, mask, fp, val, floor, st);
-        const unsigned long long got = __shfl(raw, first, WAVE);
-        if (ins) slot = cand_word(got, val);
-        if (act) {
-          cand_slot[t] = slot;
-          cand_ob[t] = obw | local;
-        }
-      }
-      STAMP(3);
-      return;
-    }
-  }
-#endif
+  // (A wave-level dedup of equal fingerprints before the HBM probe -- a
+  // 64-slot LDS table per wave, only each key's first lane probing -- was
+  // measured and rejected: it cut the global inserts from 6.75e9 to 4.84e9,
+  // the CAS from 4.10e9 to 2.65e9 and the atomicMin from 5.29e9 to 3.37e9 per
+  // check, yet k_expand took 1,019 ms instead of 824: the LDS table costs
+  // more than the HBM operations it saves.  profiles/r04/ab_wave_dedup_r04w.txt)
   for (int idx = tid; idx < total; idx += 256) {
     int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
     while (lo < hi) {
