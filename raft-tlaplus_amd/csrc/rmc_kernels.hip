@@ -277,50 +277,9 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       // here instead of once per successor in phase C; and which messages can
       // enable an action at all (84% of DOMAIN messages cannot on the bench
       // workload: delivered, and not newer than their receiver)
-#ifdef RMC_SUMS_REG
-      // this lane's share of the parent's messages summed in registers, then
-      // one LDS atomic per nonzero word instead of ~4 per message
-      if constexpr (FPW == 1 && N <= 3) {
-        constexpr int NP = N * (N - 1);
-        uint64_t aS[NP];
-        uint32_t aSig[N], lv[LIVE_WORDS];
-#pragma unroll
-        for (int q = 0; q < NP; q++) aS[q] = 0;
-#pragma unroll
-        for (int q = 0; q < N; q++) aSig[q] = 0;
-#pragma unroll
-        for (int q = 0; q < LIVE_WORDS; q++) lv[q] = 0;
-        for (int k = tid / PB; k < nm; k += bstride) {
-          int src, dst;
-          const uint32_t w = s.msg(k);
-          if (msg_live<SPEC, N>(s, w)) {
-#pragma unroll
-            for (int q = 0; q < LIVE_WORDS; q++)
-              if ((k >> 5) == q) lv[q] |= 1u << (k & 31);
-          }
-          const uint64_t u = msg_u<SPEC>(w, src, dst);
-#pragma unroll
-          for (int q = 0; q < N; q++)
-            aSig[q] += (src == q ? (uint32_t)u : 0u) + (dst == q ? (uint32_t)(u >> 32) : 0u);
-          if (src != dst) {
-            const int pi = MsgSums<N>::pair(src, dst);
-#pragma unroll
-            for (int q = 0; q < NP; q++)
-              if (q == pi) aS[q] += u;
-          }
-        }
-        MsgSums<N>& m1 = sums1<N>(sMS[p]);
-#pragma unroll
-        for (int q = 0; q < LIVE_WORDS; q++)
-          if (lv[q]) atomicOr(&sLive[p * LIVE_WORDS + q], lv[q]);
-#pragma unroll
-        for (int q = 0; q < N; q++)
-          if (aSig[q]) atomicAdd(&m1.sig[q], aSig[q]);
-#pragma unroll
-        for (int q = 0; q < NP; q++)
-          if (aS[q]) atomicAdd((unsigned long long*)&m1.S[q], (unsigned long long)aS[q]);
-      } else
-#endif
+      // (Summing a lane's share in registers and publishing one LDS atomic
+      // per nonzero word was measured and rejected: k_expand 839 vs 827 ms
+      // per check, profiles/r04/ab_sums_reg_r04y.txt.)
       for (int k = tid / PB; k < nm; k += bstride) {
         int src, dst;
         const uint32_t w = s.msg(k);
