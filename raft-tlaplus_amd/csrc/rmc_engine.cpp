@@ -1292,6 +1292,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     hst.cap_flags = 0;
     hst.max_msgs = 0;
     hst.hidden_coll = 0;
+    hst.row_words = 0;
     HIPCHK(hipMemcpyAsync(stbuf.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(A.stmat.p, &hst, sizeof hst, hipMemcpyHostToDevice, stream));
   };
@@ -2235,6 +2236,13 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
                 "(%.3f per insert, %llu won), atomicMin %llu (%.3f per insert)\n", fs[FPS_INSERT], fs[FPS_GROUP],
                 (double)fs[FPS_GROUP] / fs[FPS_INSERT], fs[FPS_CAS], (double)fs[FPS_CAS] / fs[FPS_INSERT],
                 fs[FPS_CAS_WON], fs[FPS_MIN], (double)fs[FPS_MIN] / fs[FPS_INSERT]);
+    }
+    {  // -DRMC_ROWSTATS builds: the rows' bytes up to their last message (what the masked stores write)
+      DevStatus ms;
+      HIPCHK(hipMemcpy(&ms, A.stmat.p, sizeof ms, hipMemcpyDeviceToHost));
+      if (ms.row_words && distinct > 1)
+        fprintf(stderr, "[rmc] rows: %llu materialized, %.1f B each up to the last message (16 B units) of %zu B "
+                "fixed stride\n", distinct - 1, 4.0 * (double)ms.row_words / (double)(distinct - 1), W * 4);
     }
     fprintf(stderr, "[rmc] fingerprint set: 2^%d slots, load %.3f, %llu growths, %llu chunk redos\n",
             __builtin_ctzll(slots), (double)distinct / (double)slots, grows, redos);

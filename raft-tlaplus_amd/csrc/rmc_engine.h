@@ -15,6 +15,7 @@ struct DevStatus {
   unsigned cap_flags;              // bit e set: capacity overflow ErrCode e
   unsigned max_msgs;               // largest |DOMAIN messages| of a materialized state
   unsigned long long hidden_coll;  // same-level duplicates whose hidden variables differ from the winner's
+  unsigned long long row_words;    // -DRMC_ROWSTATS builds: words of the materialized rows up to their last message
 };
 
 // simulation mode: the first behaviour to stop the run (violation / error)

@@ -864,6 +864,9 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   __syncthreads();
   const int total = (int)sOff[np];
   int my_max = 0;  // largest |DOMAIN messages| this thread wrote (reduced per block below)
+#ifdef RMC_ROWSTATS
+  unsigned long long my_words = 0;  // diagnostic: the words this thread's rows hold (16 B units)
+#endif
   for (int r0 = 0; r0 < total; r0 += MAT_LIST) {
     if (tid == 0) sCount = 0;
     __syncthreads();
@@ -917,6 +920,9 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
       int err = apply_delta<SPEC, N>(s, cM, d, o, &nn);
       if (err) atomicOr(&st->cap_flags, 1u << err);
       my_max = nn > my_max ? nn : my_max;
+#ifdef RMC_ROWSTATS
+      my_words += (unsigned long long)((1 + 4 * N + nn + 3) & ~3);
+#endif
       const unsigned long long pg = pbase + p0 + p;
       *tp = pg;
       *tb = (uint16_t)b;
@@ -938,6 +944,11 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   // one hot address for the whole grid: only a wave that raises the max pays an atomic
   if (lane == 0 && (unsigned)my_max > __hip_atomic_load(&st->max_msgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
     atomicMax(&st->max_msgs, (unsigned)my_max);
+#ifdef RMC_ROWSTATS
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) my_words += __shfl_xor(my_words, o, WAVE);
+  if (lane == 0 && my_words) atomicAdd(&st->row_words, my_words);
+#endif
 }
 
 // ------------------------------------------------- sharded search

@@ -506,6 +506,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     s.hst.cap_flags = 0;
     s.hst.max_msgs = 0;
     s.hst.hidden_coll = 0;
+    s.hst.row_words = 0;
     HIPCHK(hipMemcpyAsync(B.stbuf.p, &s.hst, sizeof s.hst, hipMemcpyHostToDevice, stream));
   }
 

@@ -63,6 +63,7 @@ static int simulate_impl(rmc_model* m, const rmc_options* opt, unsigned long lon
     HIPCHK(hipMemcpyAsync(ssb.p, &s0, sizeof s0, hipMemcpyHostToDevice, stream));
   }
   DevStatus hst;
+  memset(&hst, 0, sizeof hst);
   hst.err_key = hst.inv_err_key = hst.viol_key = ~0ULL;
   hst.cap_flags = 0;
   hst.max_msgs = 0;
