@@ -1,0 +1,11 @@
+#!/bin/bash
+# r04 final check on the committed build: the whole -m gpu suite, smoke(),
+# and the default bench line (as the driver runs them).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=$PWD/gpurun_out/${TAG:-r04ac}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -10 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
+cut -c1-400 $O/bench.json
