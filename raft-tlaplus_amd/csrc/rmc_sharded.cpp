@@ -610,6 +610,12 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     a.cand_cap = cand_cap;
     a.st = s.B->stbuf.as<DevStatus>();
   };
+  // Capacity exhausted mid-level (host pages, HBM): the level in progress is
+  // abandoned and the check ends with status 3 and the completed levels'
+  // counts, as the single-GPU search does.  (All shards of a process see the
+  // same exception; with RCCL a rank that fails alone leaves its peers in the
+  // next collective.)
+  try {
   while (status == 0 && P > 0 && !stop) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
     if (opt->time_limit > 0) {
@@ -1100,6 +1106,15 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     if (opt->verbose && comm.local[0] == 0)
       fprintf(stderr, "[rmc] depth %u: %llu new, %llu distinct, %llu generated (%d shards)\n", depth,
               (unsigned long long)GW, (unsigned long long)distinct, (unsigned long long)generated, W);
+  }
+  } catch (OutOfHostMemory& oom) {
+    status = 3;
+    message = std::string("capacity overflow: ") + oom.what();
+    HIPCHK(hipDeviceSynchronize());
+  } catch (OutOfDeviceMemory& oom) {
+    status = 3;
+    message = std::string("capacity overflow: ") + oom.what();
+    HIPCHK(hipDeviceSynchronize());
   }
   HIPCHK(hipStreamSynchronize(stream));
   // ---- trace: walk the distributed parent records from the failing state to Init

@@ -144,3 +144,23 @@ def test_sharded_host_frontier_auto_switch(monkeypatch):
     monkeypatch.setenv("RMC_HF_HBM_FRACTION", "0.00002")
     g = SHIPPED_HF["Raft_cfg"]
     _same(_model(g).check_logical(2, host_frontier=0, chunk_parents=70000), g)
+
+
+@pytest.mark.parametrize("shards", [0, 2])
+def test_host_pages_exhausted_ends_with_the_completed_levels(monkeypatch, shards):
+    """Host pages running out mid-level (RMC_HOST_FRONTIER_GIB far below the
+    shipped Raft.cfg's levels, 1000-row pages) ends the check with status
+    "capacity" and the counts of the levels completed before it, a prefix of
+    the fixture's -- the single-GPU search and the sharded one alike."""
+    monkeypatch.setenv("RMC_HOST_FRONTIER_GIB", "0.02")
+    monkeypatch.setenv("RMC_HOST_PAGE_ROWS", "1000")
+    g = SHIPPED_HF["Raft_cfg"]
+    m = _model(g)
+    r = m.check_logical(shards, host_frontier=1) if shards else m.check(host_frontier=1)
+    assert r["status"] == "capacity", (r["status"], r.get("message"))
+    assert "host frontier pages exhausted" in r["message"]
+    k = len(r["levels"])
+    assert 3 < k < len(g["levels"])
+    assert r["levels"] == g["levels"][:k]
+    assert r["distinct"] == sum(n for _, n in g["levels"][:k])
+    assert r["generated"] == sum(x for x, _ in g["levels"][:k])
