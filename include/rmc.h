@@ -91,10 +91,15 @@ typedef struct {
 } rmc_result;
 
 /* Load M.tla + M.cfg, as TLC reads them (`tlc2.TLC -config M.cfg M.tla`; a
- * path without ".tla" gets it appended).  The .tla must exist and be the
- * reference's text of a supported module (verified by a normalised hash); the
- * module is its basename.  cfg_path NULL = M.cfg beside it.  Returns 0, or -3
- * when a file cannot be read, -2 when the spec or cfg is rejected. */
+ * path without ".tla" gets it appended; the module is its basename; cfg_path
+ * NULL = M.cfg beside it).  A .tla whose text (comments and whitespace aside)
+ * is a reference module's uses that module's action table directly; any other
+ * text goes through the TLA+ front end (rmc_tla.cpp): the module
+ * is parsed, its Next decomposed into disjuncts, and each disjunct lowered --
+ * matched by closure hash onto the action library, or compiled from its body
+ * where the front end compiles that form -- and refused, with the disjunct
+ * named, when neither applies.  Returns 0, or -3 when a file cannot be read,
+ * -2 when the spec or cfg is rejected. */
 int rmc_model_load(const char* tla_path, const char* cfg_path, rmc_model** out, char* err, size_t errlen);
 /* The built-in lowering of `module` bound to in-memory cfg text (no .tla needed). */
 int rmc_model_load_text(const char* module, const char* cfg_text, rmc_model** out, char* err, size_t errlen);
@@ -121,6 +126,11 @@ void rmc_model_free(rmc_model* m);
 void rmc_release_device_memory(void);
 const char* rmc_last_error(void);
 const char* rmc_version(void);
+/* Layout version of rmc_options / rmc_result.  2 (r04): rmc_result.message moved after `seconds` (SURVEY
+ * §8b's fields first, in its order) and device_bytes appended.  A binding built against another version must
+ * refuse the library; rmc_abi_layout gives the offsets themselves. */
+#define RMC_ABI_VERSION 2
+int rmc_abi_version(void);
 /* Fingerprint-sharded search.  One process per GPU: rank 0
  * calls rmc_comm_unique_id, the 128-byte id is broadcast out of band (e.g.
  * torch.distributed), then every rank calls rmc_check_sharded with its rank,

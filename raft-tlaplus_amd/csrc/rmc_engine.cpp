@@ -818,7 +818,9 @@ struct Arena {
   // compact host rows (per window parity): out = pack side, in = unpack side
   DevBuf hf_pack[2], hf_olen32[2], hf_olen8[2], hf_ooff[2], hf_oscan[2];
   DevBuf hf_stage[2], hf_ilen32[2], hf_ilen8[2], hf_ioff[2], hf_iscan[2];
+  DevBuf hf_flag;  // k_row_words' bound: a row whose header claims more than W words
   void release_hf() {
+    hf_flag.release();
     for (int k = 0; k < 2; k++)
       for (DevBuf* b : {&hwin_in[k], &hwin_out[k], &hf_pack[k], &hf_olen32[k], &hf_olen8[k], &hf_ooff[k], &hf_oscan[k],
                         &hf_stage[k], &hf_ilen32[k], &hf_ilen8[k], &hf_ioff[k], &hf_iscan[k]})
@@ -1221,7 +1223,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   const bool rec_host = recovering && opt->host_frontier != -1 &&
                         (opt->host_frontier == 1 ||
                          (hbm_total && (double)rc.cur_n * std::max(rc.rate, 1.0) * 1.25 * (double)(W * 4) >
-                                           0.25 * (double)hbm_total) ||
+                                           hf_hbm_fraction() * (double)hbm_total) ||
                          getenv("RMC_RECOVER_TO_HOST"));  // test hook
   if (recovering && !rec_host) fcap = std::max(fcap, rc.cur_n);
   const int maxsucc = M.nfixed + M.kmax;
@@ -1402,19 +1404,19 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   bool hf = false;
   HostPagePool pool;
   const size_t row_bytes = W * 4;
-  size_t page_rows = std::max<size_t>(1, (256ULL << 20) / row_bytes);
+  size_t page_bytes = HostPagePool::PAGE_BYTES;
   // test hooks: RMC_HOST_PAGE_ROWS (small pages: rows straddle many), and
   // RMC_HOST_FRONTIER_AT=L (auto mode moves to the host before level L's
   // second chunk) or L:grow (as if the next-level buffer's growth ran out of
   // HBM in that chunk)
-  if (const char* e = getenv("RMC_HOST_PAGE_ROWS")) page_rows = std::max<long long>(1, atoll(e));
+  if (const char* e = getenv("RMC_HOST_PAGE_ROWS")) page_bytes = (size_t)std::max<long long>(1, atoll(e)) * row_bytes;
   unsigned hf_force_level = 0;
   bool hf_force_grow = false;
   if (const char* e = getenv("RMC_HOST_FRONTIER_AT")) {
     hf_force_level = (unsigned)atoi(e);
     hf_force_grow = strstr(e, ":grow") != nullptr;
   }
-  pool.page_bytes = page_rows * row_bytes;
+  pool.page_bytes = page_bytes;
   pool.limit = host_frontier_limit();
   // pinning threads and the pages they keep ready (RMC_HF_PIN_THREADS,
   // RMC_HF_PIN_AHEAD; 0 threads = pin on demand in the BFS thread)
@@ -1481,6 +1483,14 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
                        A.hf_ilen32[k].as<uint32_t>(), (uint32_t*)dev, st);
     HIPCHK(hipGetLastError());
   };
+  bool hf_flag_ready = false;  // A.hf_flag zeroed for this check
+  auto hf_flag_init = [&]() {
+    if (hf_flag_ready) return;
+    A.hf_flag.ensure(16);
+    HIPCHK(hipMemsetAsync(A.hf_flag.p, 0, 16, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    hf_flag_ready = true;
+  };
   // n fixed rows on the device -> appended to a host level (synchronous, in slices; the switch to the host)
   auto hf_from_device = [&](HostLevel& h, const uint32_t* rows, unsigned long long n) {
     if (!n) return;
@@ -1499,16 +1509,18 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     off.ensure(S * 4);
     sc.ensure(std::max<size_t>(scan_temp_bytes(S), 16));
     std::vector<uint8_t> l;
+    hf_flag_init();
     for (unsigned long long r = 0; r < n; r += S) {
       const unsigned long long k = std::min(S, n - r);
-      launch_row_words(rows + r * W, k, (int)W, hdr_words, l32.as<uint32_t>(), l8.as<uint8_t>(), stream);
+      launch_row_words(rows + r * W, k, (int)W, hdr_words, HostRowsIO::max_words(W), l32.as<uint32_t>(),
+                       l8.as<uint8_t>(), A.hf_flag.as<unsigned>(), stream);
       launch_scan(sc.p, sc.bytes, l32.as<uint32_t>(), off.as<uint32_t>(), k, stream);
       launch_pack_rows(rows + r * W, k, (int)W, off.as<uint32_t>(), l32.as<uint32_t>(), pk.as<uint32_t>(), stream);
       HIPCHK(hipGetLastError());
       l.resize(k);
       HIPCHK(hipMemcpyAsync(l.data(), l8.p, k, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      h.append_dev(l.data(), k, pk.p, stream, pool);
+      h.append_dev(l.data(), k, pk.p, pk.bytes, stream, pool);
       HIPCHK(hipStreamSynchronize(stream));
     }
   };
@@ -1520,8 +1532,8 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     hf_ensure_out(k, n);
     HIPCHK(hipStreamWaitEvent(hs.cp, hs.mat[k], 0));  // the rows are written
     HIPCHK(hipStreamWaitEvent(hs.cp, hs.out[k], 0));  // the pack buffer's last copy-out is done
-    launch_row_words(A.hwin_out[k].as<uint32_t>(), n, (int)W, hdr_words, A.hf_olen32[k].as<uint32_t>(),
-                     A.hf_olen8[k].as<uint8_t>(), hs.cp);
+    launch_row_words(A.hwin_out[k].as<uint32_t>(), n, (int)W, hdr_words, HostRowsIO::max_words(W),
+                     A.hf_olen32[k].as<uint32_t>(), A.hf_olen8[k].as<uint8_t>(), A.hf_flag.as<unsigned>(), hs.cp);
     launch_scan(A.hf_oscan[k].p, A.hf_oscan[k].bytes, A.hf_olen32[k].as<uint32_t>(), A.hf_ooff[k].as<uint32_t>(), n,
                 hs.cp);
     launch_pack_rows(A.hwin_out[k].as<uint32_t>(), n, (int)W, A.hf_ooff[k].as<uint32_t>(),
@@ -1537,7 +1549,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     HIPCHK(hipEventSynchronize(hs.packed[hf_pend.k]));
     hf_lens_tmp.resize(hf_pend.n);
     HIPCHK(hipMemcpy(hf_lens_tmp.data(), A.hf_olen8[hf_pend.k].p, hf_pend.n, hipMemcpyDeviceToHost));
-    hnxt.append_dev(hf_lens_tmp.data(), hf_pend.n, A.hf_pack[hf_pend.k].p, hs.co, pool);
+    hnxt.append_dev(hf_lens_tmp.data(), hf_pend.n, A.hf_pack[hf_pend.k].p, A.hf_pack[hf_pend.k].bytes, hs.co, pool);
     HIPCHK(hipEventRecord(hs.out[hf_pend.k], hs.co));
   };
   auto reserve_windows = [&]() {
@@ -1550,6 +1562,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       hf_ensure_out(k, 3 * chunk);
       hf_ensure_in(k, chunk);
     }
+    hf_flag_init();
     windows = true;
   };
   auto before_growth = [&](size_t request) {  // auto mode: keep the windows' HBM available
@@ -1997,6 +2010,13 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     if (hf) {
       hf_flush();
       hs.sync();  // every new row is in its host page
+      unsigned f = 0;
+      HIPCHK(hipMemcpy(&f, A.hf_flag.p, 4, hipMemcpyDeviceToHost));
+      if (f) {  // the level that met the bound is not counted (as a capacity stop mid-level)
+        status = 3;
+        message = "capacity overflow: a row's message count exceeds the row width (a row never written)";
+        break;
+      }
     }
     const unsigned long long gen_before = generated, dist_before = distinct;
     generated += gen_lvl;
@@ -2111,6 +2131,10 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   } catch (OutOfHostMemory& oom) {
     status = 3;
     message = std::string("capacity overflow: ") + oom.what();
+    HIPCHK(hipDeviceSynchronize());
+  } catch (RowCapacity& rc) {
+    status = 3;
+    message = rc.what();
     HIPCHK(hipDeviceSynchronize());
   } catch (OutOfDeviceMemory& oom) {
     // the level in progress is abandoned; counts are those of the completed levels
@@ -2314,7 +2338,8 @@ void set_err(char* err, size_t len, const std::string& msg) {
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
-const char* rmc_version(void) { return "raftmc 0.1 (gfx950)"; }
+const char* rmc_version(void) { return "raftmc 0.5 (gfx950, abi 2)"; }
+int rmc_abi_version(void) { return RMC_ABI_VERSION; }
 
 // ABI self-description for binding checks: sizeof and every field offset of
 // rmc_options then rmc_result, in declaration order (see include/rmc.h).

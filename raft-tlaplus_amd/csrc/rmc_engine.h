@@ -74,8 +74,9 @@ void launch_rehash(const unsigned long long* old, unsigned long long nold, unsig
                    unsigned long long nmask, DevStatus* st, hipStream_t s, int ew = 2);
 
 // compact host-frontier rows (rmc_kernels.hip): words per row (1 + 4N + nmsg), pack / unpack
-void launch_row_words(const uint32_t* rows, unsigned long long n, int W, int hdr_words, uint32_t* lens32,
-                      uint8_t* lens8, hipStream_t s);
+// (a header whose length would pass max_words is clamped to it and sets *flag: a row never written)
+void launch_row_words(const uint32_t* rows, unsigned long long n, int W, int hdr_words, int max_words,
+                      uint32_t* lens32, uint8_t* lens8, unsigned* flag, hipStream_t s);
 void launch_widen_lens(const uint8_t* lens8, unsigned long long n, uint32_t* lens32, hipStream_t s);
 void launch_pack_rows(const uint32_t* rows, unsigned long long n, int W, const uint32_t* offs, const uint32_t* lens32,
                       uint32_t* out, hipStream_t s);

@@ -213,6 +213,71 @@ struct GrowBuf {
 struct OutOfHostMemory : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// A compact row longer than its fixed row (k_row_words' bound): status 3.
+struct RowCapacity : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// Registered host pages outlive a check (r05).  Each check used to pin its
+// own pages (mmap + hipHostRegister) and unregister + munmap them at its end;
+// the next check's mmap then got the same virtual addresses back and
+// registered them again.  The driver's GPU run of r04 faulted in a D2H copy
+// into host-frontier pages (an illegal address on the copy-out stream) after
+// ~30 such checks in one process, a fault no bounded kernel access explains.
+// Now (1) a process-wide cache keeps up to RMC_HF_RETAIN_GIB (default 8) of
+// registered pages for the next check, so a test process registers them once,
+// and (2) a page given up is unregistered and its address range is replaced
+// by an inaccessible reservation (PROT_NONE, no backing memory) instead of
+// unmapped, so no address that was ever registered is handed to a new
+// registration -- whatever the runtime still holds for a retired range can
+// never alias a live page.
+struct PinnedPageCache {
+  std::mutex mu;
+  size_t page_bytes = 0;
+  std::vector<void*> pages;
+  size_t retain = 0;
+  unsigned long long retired = 0;  // pages given up (address ranges quarantined)
+  static PinnedPageCache& get() {
+    static PinnedPageCache* c = [] {  // never destroyed: pages may outlive static destructors' HIP runtime
+      auto* k = new PinnedPageCache();
+      const char* e = getenv("RMC_HF_RETAIN_GIB");
+      k->retain = (size_t)((e ? atof(e) : 8.0) * 1073741824.0);
+      return k;
+    }();
+    return *c;
+  }
+  static void retire(void* p, size_t bytes) {
+    (void)hipHostUnregister(p);
+    void* q = mmap(p, bytes, PROT_NONE, MAP_FIXED | MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (q == MAP_FAILED) munmap(p, bytes);
+  }
+  void* take(size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (page_bytes != bytes || pages.empty()) return nullptr;
+    void* p = pages.back();
+    pages.pop_back();
+    return p;
+  }
+  // keep p for a later check, or retire it; returns true when kept
+  bool give(void* p, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (page_bytes != bytes) {  // another page size: the cached ones go
+        for (void* q : pages) retire(q, page_bytes);
+        retired += pages.size();
+        pages.clear();
+        page_bytes = bytes;
+      }
+      if ((pages.size() + 1) * bytes <= retain) {
+        pages.push_back(p);
+        return true;
+      }
+      retired++;
+    }
+    retire(p, bytes);
+    return false;
+  }
+};
 
 // BFS levels in pinned host memory (SURVEY.md §7 hard part 5: "page the
 // frontier to pinned host memory when a level exceeds its budget").  A level
@@ -222,6 +287,9 @@ struct OutOfHostMemory : std::runtime_error {
 // rows already consumed go back to the pool while the level is still being
 // read, so the host peak is about one level plus the growth of the next.
 struct HostPagePool {
+  // every pool pages in these units (compact rows straddle pages; tests set
+  // RMC_HOST_PAGE_ROWS for small ones), so cached pages fit every check
+  static constexpr size_t PAGE_BYTES = 256ULL << 20;
   size_t page_bytes = 0;
   size_t allocated = 0, limit = 0;  // bytes of pinned pages held / allowed (including pages being pinned)
   double alloc_s = 0;               // time the BFS thread spent pinning or waiting for a pinned page
@@ -235,12 +303,14 @@ struct HostPagePool {
   std::vector<std::thread> fillers;
   size_t ahead = 0, inflight = 0;
   bool stop = false, failed = false;
-  // One page, outside the lock; nullptr when the host refuses.  Pages are
+  // One page, outside the lock; nullptr when the host refuses.  A page the
+  // process-wide cache holds is reused as it is; otherwise pages are
   // populated by the calling thread (mmap MAP_POPULATE: the kernel zeroes them
   // in parallel across threads) and then registered with HIP, which is cheap
   // on populated memory: 15 GB/s with 4 threads against 5.8 GB/s for
   // hipHostMalloc, which serialises in the driver (profiles/r03/pin_probe.txt).
   void* pin() {
+    if (void* c = PinnedPageCache::get().take(page_bytes)) return c;
     void* p = mmap(nullptr, page_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
     if (p == MAP_FAILED) return nullptr;
     if (hipHostRegister(p, page_bytes, hipHostRegisterDefault) != hipSuccess) {
@@ -250,10 +320,7 @@ struct HostPagePool {
     }
     return p;
   }
-  void unpin(void* p) {
-    (void)hipHostUnregister(p);
-    munmap(p, page_bytes);
-  }
+  void unpin(void* p) { PinnedPageCache::get().give(p, page_bytes); }
   void start_fillers(size_t pages, int threads) {
     if (!fillers.empty() || !pages || threads < 1) return;
     ahead = pages;
@@ -386,6 +453,7 @@ struct HostLevel {
     const char* s = (const char*)dev;
     while (nb) {
       const size_t pg = b0 / page_bytes, off = b0 % page_bytes, k = std::min<unsigned long long>(nb, page_bytes - off);
+      if (pg >= pages.size() || !pages[pg]) throw std::runtime_error("host frontier: copy-out past the reserved pages");
       HIPCHK(hipMemcpyAsync((char*)pages[pg] + off, s, k, hipMemcpyDeviceToHost, stream));
       s += k;
       b0 += k;
@@ -424,10 +492,15 @@ struct HostLevel {
       nb -= k;
     }
   }
-  // append n compact rows (word counts l) whose bytes are in dev, async on stream
-  void append_dev(const uint8_t* l, unsigned long long n, const void* dev, hipStream_t stream, HostPagePool& pool) {
+  // append n compact rows (word counts l) whose bytes are in dev (dev_bytes
+  // long: the rows' bytes are checked against it), async on stream
+  void append_dev(const uint8_t* l, unsigned long long n, const void* dev, size_t dev_bytes, hipStream_t stream,
+                  HostPagePool& pool) {
     unsigned long long nb = 0;
     for (unsigned long long q = 0; q < n; q++) nb += 4ULL * l[q];
+    if (nb > dev_bytes)
+      throw std::runtime_error("host frontier: " + std::to_string(n) + " compact rows of " + std::to_string(nb) +
+                               " B exceed their " + std::to_string(dev_bytes) + " B pack buffer");
     reserve_bytes(nb, pool);
     add_rows(l, n);
     copy_out(dev, bytes, nb, stream);
@@ -481,7 +554,7 @@ struct HostLevel {
 // device rows (the sharded search's per-shard host frontier; the single-GPU
 // search pipelines the same kernels over its copy streams).
 struct HostRowsIO {
-  DevBuf pack, l32, l8, off, scan, stage, il32, il8, ioff, iscan;
+  DevBuf pack, l32, l8, off, scan, stage, il32, il8, ioff, iscan, flag;
   static size_t atleast(size_t b) { return b < 16 ? 16 : b; }
   // rows [r0, r0 + n) of h -> fixed rows at dev, in stream order on st
   void load(const HostLevel& h, unsigned long long r0, unsigned long long n, uint32_t* dev, size_t W, hipStream_t st) {
@@ -499,27 +572,52 @@ struct HostRowsIO {
     rmc::launch_unpack_rows(stage.as<uint32_t>(), n, (int)W, ioff.as<uint32_t>(), il32.as<uint32_t>(), dev, st);
     HIPCHK(hipGetLastError());
   }
-  // n fixed rows at dev -> appended to h; returns once they are in the pages
+  // n fixed rows at dev -> appended to h; returns once they are in the pages.
+  // In slices of at most 2^24 rows and 256 MiB of pack buffer (the pack
+  // offsets are 32-bit words, and a whole level would need a second copy of
+  // itself in HBM just when HBM is short: ADVICE r04).  A row whose header
+  // claims more words than W (never written) ends the check with status 3.
+  static unsigned long long slice_rows(size_t W) {
+    return std::max<unsigned long long>(1, std::min<unsigned long long>(1ULL << 24, (256ULL << 20) / (W * 4)));
+  }
   void store(HostLevel& h, const uint32_t* dev, unsigned long long n, size_t W, int hdr_words, hipStream_t st,
              HostPagePool& pool) {
     if (!n) return;
-    pack.ensure(atleast(n * W * 4));
-    l32.ensure(atleast(n * 4));
-    l8.ensure(atleast(n));
-    off.ensure(atleast(n * 4));
-    scan.ensure(atleast(rmc::scan_temp_bytes(n)));
-    rmc::launch_row_words(dev, n, (int)W, hdr_words, l32.as<uint32_t>(), l8.as<uint8_t>(), st);
-    rmc::launch_scan(scan.p, scan.bytes, l32.as<uint32_t>(), off.as<uint32_t>(), n, st);
-    rmc::launch_pack_rows(dev, n, (int)W, off.as<uint32_t>(), l32.as<uint32_t>(), pack.as<uint32_t>(), st);
-    HIPCHK(hipGetLastError());
-    std::vector<uint8_t> lens(n);
-    HIPCHK(hipMemcpyAsync(lens.data(), l8.p, n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    h.append_dev(lens.data(), n, pack.p, st, pool);
-    HIPCHK(hipStreamSynchronize(st));
+    const unsigned long long S = std::min<unsigned long long>(n, slice_rows(W));
+    pack.ensure(atleast(S * W * 4));
+    l32.ensure(atleast(S * 4));
+    l8.ensure(atleast(S));
+    off.ensure(atleast(S * 4));
+    scan.ensure(atleast(rmc::scan_temp_bytes(S)));
+    flag.ensure(16);
+    HIPCHK(hipMemsetAsync(flag.p, 0, 4, st));
+    std::vector<uint8_t> lens;
+    for (unsigned long long r = 0; r < n; r += S) {
+      const unsigned long long k = std::min(S, n - r);
+      const uint32_t* rows = dev + r * W;
+      rmc::launch_row_words(rows, k, (int)W, hdr_words, max_words(W), l32.as<uint32_t>(), l8.as<uint8_t>(),
+                            flag.as<unsigned>(), st);
+      rmc::launch_scan(scan.p, scan.bytes, l32.as<uint32_t>(), off.as<uint32_t>(), k, st);
+      rmc::launch_pack_rows(rows, k, (int)W, off.as<uint32_t>(), l32.as<uint32_t>(), pack.as<uint32_t>(), st);
+      HIPCHK(hipGetLastError());
+      lens.resize(k);
+      unsigned f = 0;
+      HIPCHK(hipMemcpyAsync(lens.data(), l8.p, k, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&f, flag.p, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (f) throw RowCapacity("capacity overflow: a row's message count exceeds the row width (a row never written)");
+      h.append_dev(lens.data(), k, pack.p, pack.bytes, st, pool);
+      HIPCHK(hipStreamSynchronize(st));
+    }
+  }
+  // the pack bound (test hook RMC_HF_ROW_MAX_WORDS lowers it to exercise the
+  // capacity report)
+  static int max_words(size_t W) {
+    if (const char* e = getenv("RMC_HF_ROW_MAX_WORDS")) return std::min<int>((int)W, atoi(e));
+    return (int)W;
   }
   void release() {
-    for (DevBuf* b : {&pack, &l32, &l8, &off, &scan, &stage, &il32, &il8, &ioff, &iscan}) b->release();
+    for (DevBuf* b : {&pack, &l32, &l8, &off, &scan, &stage, &il32, &il8, &ioff, &iscan, &flag}) b->release();
   }
 };
 

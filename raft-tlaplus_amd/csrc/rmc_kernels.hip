@@ -1335,12 +1335,22 @@ void launch_scan(void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* ou
 // cross PCIe and unpacked into fixed-stride rows in the input window, so the
 // kernels never see the compact form.  A wave per row: lane l moves word l
 // (coalesced on both sides); rows in the same wave-step are consecutive.
+// A row's length comes from its header word, so it is bounded here: a header
+// whose message count would take the row past max_words (the row width) is a
+// row that was never written -- k_materialize leaves a successor it could not
+// fit unwritten and flags the capacity -- and is clamped instead of letting
+// k_pack_rows read past the row and the copy-out past the pack buffer; the
+// flag ends the check with status 3 (the caller reads it at the level end).
 __global__ __launch_bounds__(256) void k_row_words(const uint32_t* __restrict__ rows, unsigned long long n, int W,
-                                                   int hdr_words, uint32_t* __restrict__ lens32,
-                                                   uint8_t* __restrict__ lens8) {
+                                                   int hdr_words, int max_words, uint32_t* __restrict__ lens32,
+                                                   uint8_t* __restrict__ lens8, unsigned* __restrict__ flag) {
   const unsigned long long r = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const uint32_t len = (uint32_t)hdr_words + (rows[r * (unsigned long long)W] & 0xFFu);
+  uint32_t len = (uint32_t)hdr_words + (rows[r * (unsigned long long)W] & 0xFFu);
+  if (len > (uint32_t)max_words) {
+    len = (uint32_t)max_words;
+    atomicOr(flag, 1u);
+  }
   lens32[r] = len;
   lens8[r] = (uint8_t)len;
 }
@@ -1367,7 +1377,7 @@ __global__ __launch_bounds__(256) void k_unpack_rows(const uint32_t* __restrict_
   const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x / WAVE);
   for (unsigned long long r = (unsigned long long)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; r < n;
        r += waves) {
-    const uint32_t len = lens32[r];
+    const uint32_t len = lens32[r] < (uint32_t)W ? lens32[r] : (uint32_t)W;  // host lens: never past the row
     const uint32_t* src = in + offs[r];
     uint32_t* dst = rows + r * (unsigned long long)W;
     for (uint32_t l = lane_id(); l < (uint32_t)W; l += WAVE) dst[l] = l < len ? src[l] : 0u;
@@ -1377,10 +1387,10 @@ static unsigned grid_for(unsigned long long n, unsigned per) {
   unsigned long long g = (n + per - 1) / per;
   return (unsigned)(g < 1 ? 1 : g > (1u << 20) ? (1u << 20) : g);
 }
-void launch_row_words(const uint32_t* rows, unsigned long long n, int W, int hdr_words, uint32_t* lens32,
-                      uint8_t* lens8, hipStream_t s) {
+void launch_row_words(const uint32_t* rows, unsigned long long n, int W, int hdr_words, int max_words,
+                      uint32_t* lens32, uint8_t* lens8, unsigned* flag, hipStream_t s) {
   if (!n) return;
-  k_row_words<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(rows, n, W, hdr_words, lens32, lens8);
+  k_row_words<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(rows, n, W, hdr_words, max_words, lens32, lens8, flag);
 }
 void launch_widen_lens(const uint8_t* lens8, unsigned long long n, uint32_t* lens32, hipStream_t s) {
   if (!n) return;

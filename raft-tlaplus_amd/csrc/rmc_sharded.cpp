@@ -610,11 +610,47 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     a.cand_cap = cand_cap;
     a.st = s.B->stbuf.as<DevStatus>();
   };
-  // Capacity exhausted mid-level (host pages, HBM): the level in progress is
-  // abandoned and the check ends with status 3 and the completed levels'
-  // counts, as the single-GPU search does.  (All shards of a process see the
-  // same exception; with RCCL a rank that fails alone leaves its peers in the
-  // next collective.)
+  // Capacity exhausted mid-level (host pages, HBM, a row longer than its
+  // width): the level in progress is abandoned and the check ends with
+  // status 3 and the completed levels' counts, as the single-GPU search does.
+  // Host pages and HBM are per process, so with RCCL or shm one rank usually
+  // runs out first; it must not leave the level loop while its peers wait in
+  // the next collective.  Every step that allocates runs under
+  // `guard`, which turns the exception into a local flag and skips the
+  // process's remaining guarded work; the flag travels with the next
+  // allgather (a column of the existing ones, or `agree` before a
+  // point-to-point exchange), and all ranks leave together.
+  std::string cap_local;  // this process's capacity failure, this round
+  bool abandon = false;   // the level in progress is not counted
+  auto guard = [&](auto&& f) {
+    if (!cap_local.empty()) return;
+    try {
+      f();
+    } catch (OutOfHostMemory& e) {
+      cap_local = std::string("capacity overflow: ") + e.what();
+    } catch (OutOfDeviceMemory& e) {
+      cap_local = std::string("capacity overflow: ") + e.what();
+    } catch (RowCapacity& e) {
+      cap_local = e.what();
+    }
+  };
+  // the ranks' flags, allgathered (column `col` of `all`, `ncol` per rank): true when any rank failed
+  auto any_failed = [&](int col, int ncol) {
+    bool any = false;
+    for (int r = 0; r < W; r++) any |= all[(size_t)r * ncol + col] != 0;
+    if (any) {
+      status = 3;
+      message = cap_local.empty() ? "capacity overflow on another rank (host pages or HBM)" : cap_local;
+      stop = true;
+      abandon = true;
+    }
+    return any;
+  };
+  auto agree = [&]() {
+    for (int i = 0; i < NL; i++) rows[i] = {(uint64_t)!cap_local.empty()};
+    comm.allgather(rows, all, 1);
+    return any_failed(0, 1);
+  };
   try {
   while (status == 0 && P > 0 && !stop) {
     if (opt->max_depth && (int)depth >= opt->max_depth) { status = 4; break; }
@@ -639,8 +675,12 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       comm.allgather(rows, all, 1);
       bool any = false;
       for (int r = 0; r < W; r++) any |= all[r] != 0;
-      if (any)
-        for (Shard& s : sh) shard_to_host(s);
+      if (any) {
+        guard([&] {
+          for (Shard& s : sh) shard_to_host(s);
+        });
+        if (agree()) break;
+      }
     }
     const unsigned level = depth + 1;
     if (level >= 0xFFFF) throw std::runtime_error("too many levels");
@@ -660,7 +700,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         const double r = std::max(rate, done ? (double)GW / (double)done : 0.0);
         for (Shard& s : sh) {
           s.n = s.ncur > c * CH ? std::min(CH, s.ncur - c * CH) : 0;
-          if (!opt->grow_on_overflow) table_grow(s, s.entries + (unsigned long long)((double)s.n * r * 1.25) + 1024, stream, W);
+          if (!opt->grow_on_overflow)
+            guard([&] { table_grow(s, s.entries + (unsigned long long)((double)s.n * r * 1.25) + 1024, stream, W); });
         }
       }
       // ---- expand: fp + key per candidate; the fps this shard owns are inserted here
@@ -668,10 +709,12 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         Shard& s = sh[si];
         HIPCHK(hipMemsetAsync(s.B->counters.p, 0, 64, stream));
         if (s.n && s.hf) {  // the round's block of this shard's parents, unpacked from host pages
-          s.win_in.ensure(CH * WD * 4);
-          s.io.load(s.hcur, c * CH, s.n, s.win_in.as<uint32_t>(), WD, stream);
+          guard([&] {
+            s.win_in.ensure(CH * WD * 4);
+            s.io.load(s.hcur, c * CH, s.n, s.win_in.as<uint32_t>(), WD, stream);
+          });
         }
-        if (s.n) {
+        if (s.n && cap_local.empty()) {
           LevelArgs a;
           round_args(a, s, c);
           s.expand_slots = s.slots;
@@ -687,24 +730,26 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       }
       HIPCHK(hipStreamSynchronize(stream));
       read_timers();
-      for (int i = 0; i < NL; i++) rows[i] = {sh[i].ncand, sh[i].hst.cap_flags};
-      comm.allgather(rows, all, 2);
+      for (int i = 0; i < NL; i++) rows[i] = {sh[i].ncand, sh[i].hst.cap_flags, (uint64_t)!cap_local.empty()};
+      comm.allgather(rows, all, 3);
+      if (any_failed(2, 3)) break;
       unsigned capf = 0;
-      for (int r = 0; r < W; r++) capf |= (unsigned)all[2 * r + 1];
+      for (int r = 0; r < W; r++) capf |= (unsigned)all[3 * r + 1];
       if (capf == (1u << E_CAP_TABLE)) {
         // a local insert found its owner's table full: grow the full tables and
         // redo the round on every shard (inserts are idempotent; nothing else
         // of the round has happened yet)
         for (Shard& s : sh) {
-          if (s.hst.cap_flags) table_grow(s, s.slots, stream, W);  // doubles
+          if (s.hst.cap_flags) guard([&] { table_grow(s, s.slots, stream, W); });  // doubles
           s.hst.cap_flags = 0;
           HIPCHK(hipMemcpyAsync((char*)s.B->stbuf.p + offsetof(DevStatus, cap_flags), &s.hst.cap_flags, 4,
                                 hipMemcpyHostToDevice, stream));
         }
         HIPCHK(hipStreamSynchronize(stream));
+        if (agree()) break;
         continue;
       }
-      for (int r = 0; r < W; r++) gen_lvl += all[2 * r];
+      for (int r = 0; r < W; r++) gen_lvl += all[3 * r];
       if (capf) {
         int e = 0;
         while (!((capf >> e) & 1)) e++;
@@ -724,10 +769,16 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         for (int i = 0; i < NL; i++) {
           Shard& s = sh[i];
           const unsigned long long nb = bucket_blocks(s.ncand), nbw = nb * (unsigned long long)W;
-          s.B->bcnt.ensure((nbw + 1) * 4);
-          s.B->boff.ensure((nbw + 1) * 4);
-          size_t tb = scan_temp_bytes(nbw + 1);
-          s.B->btmp.ensure(tb ? tb : 16);
+          guard([&] {
+            s.B->bcnt.ensure((nbw + 1) * 4);
+            s.B->boff.ensure((nbw + 1) * 4);
+            size_t tb = scan_temp_bytes(nbw + 1);
+            s.B->btmp.ensure(tb ? tb : 16);
+          });
+          if (!cap_local.empty()) {
+            cnts[i].assign(W + 1, 0);
+            continue;
+          }
           unsigned int* bc = s.B->bcnt.as<unsigned int>();
           HIPCHK(hipMemsetAsync(bc + nbw, 0, 4, stream));
           launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, bc, stream);
@@ -741,10 +792,18 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         }
         HIPCHK(hipStreamSynchronize(stream));
         for (int i = 0; i < NL; i++) {
-          rows[i].assign(W, 0);
+          rows[i].assign(W + 1, 0);
           for (int d = 0; d < W; d++) rows[i][d] = cnts[i][d + 1] - cnts[i][d];
+          rows[i][W] = !cap_local.empty();
         }
-        comm.allgather(rows, all, W);  // all[src*W + dst] = records src sends to dst
+        comm.allgather(rows, all, W + 1);
+        if (any_failed(W, W + 1)) break;
+        {  // all[src*W + dst] = records src sends to dst (the flag column dropped)
+          std::vector<uint64_t> a2((size_t)W * W);
+          for (int q = 0; q < W; q++)
+            for (int d = 0; d < W; d++) a2[(size_t)q * W + d] = all[(size_t)q * (W + 1) + d];
+          all.swap(a2);
+        }
         for (int i = 0; i < NL; i++) {
           Shard& s = sh[i];
           s.seg_off.assign(W + 1, 0);
@@ -752,11 +811,21 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           s.rseg_off.assign(W + 1, 0);
           for (int q = 0; q < W; q++) s.rseg_off[q + 1] = s.rseg_off[q] + all[(size_t)q * W + s.id];
           s.nrecv = s.rseg_off[W];
-          s.B->send.ensure(std::max<size_t>(16, s.seg_off[W] * 16));
-          s.B->sflag.ensure(std::max<size_t>(1, s.seg_off[W]));
-          s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
-          s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
-          s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
+          guard([&] {
+            s.B->send.ensure(std::max<size_t>(16, s.seg_off[W] * 16));
+            s.B->sflag.ensure(std::max<size_t>(1, s.seg_off[W]));
+            s.B->recv.ensure(std::max<size_t>(16, s.nrecv * 16));
+            s.B->rslot.ensure(std::max<size_t>(8, s.nrecv * 8));
+            s.B->rflag.ensure(std::max<size_t>(1, s.nrecv));
+            // exact bound for the owners' inserts below: the local candidates (inserted) and every received record new
+            table_grow(s, s.entries + s.ncand + s.nrecv, stream, W);
+          });
+        }
+        {  // the counts matrix outlives the agreement's allgather
+          std::vector<uint64_t> keep = all;
+          const bool failed = agree();
+          all.swap(keep);
+          if (failed) break;
         }
         // Shards sharing the device (logical shards): k_bucket writes each
         // record straight into its owner's receive segment and k_mark_recv
@@ -805,8 +874,6 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         }
         // ---- owners insert, then mark
         for (Shard& s : sh) {
-          // exact bound: the local candidates (inserted) and every received record new
-          table_grow(s, s.entries + s.ncand + s.nrecv, stream, W);
           launch_insert_recv(s.B->recv.as<unsigned long long>(), s.nrecv, s.B->table.as<unsigned long long>(),
                              s.slots - 1, floor, s.B->rslot.as<unsigned long long>(), s.B->stbuf.as<DevStatus>(), stream);
           HIPCHK(hipGetLastError());
@@ -884,7 +951,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           a = b;
         }
       }
-      for (Shard& s : sh) {  // capacity of the receiving side
+      for (Shard& s : sh) guard([&] {  // capacity of the receiving side
         unsigned long long need = s.next_fill;
         for (auto& pc : pcs)
           if (pc.d == s.id) need = std::max(need, pc.dl + (pc.b - pc.a));
@@ -907,7 +974,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           s.trcap = nt;
         }
         s.next_fill = need;
-      }
+      });
       // A generator whose winners all stay with it, in one local run (always
       // at W = 1), writes them straight into its next frontier; the others
       // materialize into staging and send -- unless every shard is on this
@@ -941,6 +1008,19 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
         }
         direct[q] = same_device || (ok && !first);
       }
+      for (Shard& s : sh)  // the staged generators' buffers
+        if (s.n && s.nwin && !same_device && !direct[s.id])
+          guard([&] {
+            s.B->stage.ensure(s.nwin * WD * 4);
+            s.B->stp.ensure(s.nwin * 8);
+            s.B->stb.ensure(s.nwin * 2);
+          });
+      {  // every rank has room for the round's rows before any is written or sent
+        std::vector<uint64_t> keep = all;
+        const bool failed = agree();
+        all.swap(keep);
+        if (failed) break;
+      }
       // ---- materialize winners (TLC order within the generator)
       for (int si = 0; si < NL; si++) {
         Shard& s = sh[si];
@@ -959,9 +1039,6 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
           a.tr_parent = s.B->trp.as<unsigned long long>();
           a.tr_bind = s.B->trb.as<uint16_t>();
         } else {
-          s.B->stage.ensure(s.nwin * WD * 4);
-          s.B->stp.ensure(s.nwin * 8);
-          s.B->stb.ensure(s.nwin * 2);
           a.out = s.B->stage.as<uint32_t>();
           a.out_base_global = 0;
           a.tr_parent = s.B->stp.as<unsigned long long>();
@@ -1007,22 +1084,24 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       HIPCHK(hipStreamSynchronize(stream));
       read_timers();
       for (Shard& s : sh)
-        if (s.hf) {  // the round's new rows to host pages; the round's parents are consumed
-          s.io.store(s.hnxt, s.win_out.as<uint32_t>(), s.next_fill - s.fill0, WD, hdr_words, stream, pool);
-          s.hcur.recycle_below((c + 1) * CH, pool);
-        }
+        if (s.hf)  // the round's new rows to host pages; the round's parents are consumed
+          guard([&] {
+            s.io.store(s.hnxt, s.win_out.as<uint32_t>(), s.next_fill - s.fill0, WD, hdr_words, stream, pool);
+            s.hcur.recycle_below((c + 1) * CH, pool);
+          });
       for (int i = 0; i < NL; i++)
         rows[i] = {sh[i].hst.err_key, sh[i].hst.inv_err_key, sh[i].hst.viol_key,
-                   sh[i].hst.cap_flags | ((unsigned long long)sh[i].hst.max_msgs << 32)};
-      comm.allgather(rows, all, 4);
+                   sh[i].hst.cap_flags | ((unsigned long long)sh[i].hst.max_msgs << 32), (uint64_t)!cap_local.empty()};
+      comm.allgather(rows, all, 5);
+      if (any_failed(4, 5)) break;
       unsigned long long ek = ~0ULL, iek = ~0ULL, vk = ~0ULL;
       unsigned capm = 0;
       for (int r = 0; r < W; r++) {
-        ek = std::min(ek, (unsigned long long)all[4 * r]);
-        iek = std::min(iek, (unsigned long long)all[4 * r + 1]);
-        vk = std::min(vk, (unsigned long long)all[4 * r + 2]);
-        capm |= (unsigned)all[4 * r + 3];
-        gmax_msgs = std::max(gmax_msgs, (unsigned)(all[4 * r + 3] >> 32));
+        ek = std::min(ek, (unsigned long long)all[5 * r]);
+        iek = std::min(iek, (unsigned long long)all[5 * r + 1]);
+        vk = std::min(vk, (unsigned long long)all[5 * r + 2]);
+        capm |= (unsigned)all[5 * r + 3];
+        gmax_msgs = std::max(gmax_msgs, (unsigned)(all[5 * r + 3] >> 32));
       }
       if (capm) {
         status = 3;
@@ -1085,6 +1164,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       }
       c++;
     }
+    if (abandon) break;  // a capacity failure agreed mid-level: only completed levels count
     generated += gen_lvl;
     distinct += GW;
     if (GW || gen_lvl) m->levels.push_back({gen_lvl, GW});
@@ -1114,6 +1194,10 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   } catch (OutOfDeviceMemory& oom) {
     status = 3;
     message = std::string("capacity overflow: ") + oom.what();
+    HIPCHK(hipDeviceSynchronize());
+  } catch (RowCapacity& e) {
+    status = 3;
+    message = e.what();
     HIPCHK(hipDeviceSynchronize());
   }
   HIPCHK(hipStreamSynchronize(stream));

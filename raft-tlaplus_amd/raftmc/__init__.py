@@ -55,7 +55,10 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
            "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm",
-           "rmc_abi_layout", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes"]
+           "rmc_abi_layout", "rmc_abi_version", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes"]
+
+# the rmc_options / rmc_result layout these ctypes mirrors follow (include/rmc.h RMC_ABI_VERSION)
+ABI_VERSION = 2
 
 _lib = None
 
@@ -82,6 +85,9 @@ def lib():
     L.rmc_version.restype = ctypes.c_char_p
     L.rmc_levels.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), c_int]
     L.rmc_abi_layout.argtypes = [ctypes.POINTER(ctypes.c_uint64), c_int]
+    if L.rmc_abi_version() != ABI_VERSION:
+        raise RaftmcError("librmc.so has ABI version %d; this binding mirrors version %d (rebuild one of them)"
+                          % (L.rmc_abi_version(), ABI_VERSION))
     L.rmc_model_set_next.argtypes = [P, ctypes.c_char_p]
     L.rmc_model_next.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_tla_hashes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_size_t]

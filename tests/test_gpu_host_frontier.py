@@ -130,3 +130,37 @@ def test_auto_switch_tlc_order(monkeypatch, name):
     monkeypatch.setenv("RMC_HF_HBM_FRACTION", "0.000001")
     g = ORDER[name]
     same(model(g).check(host_frontier=0, chunk_parents=333), g)
+
+
+@pytest.mark.parametrize("shards", [0, 2])
+def test_row_length_bound_reports_capacity(monkeypatch, shards):
+    """r05 regression for the r04 driver fault: a compact row's length comes
+    from its header, and k_row_words bounds it by the row width instead of
+    letting k_pack_rows and the copy-out run past their buffers.
+    RMC_HF_ROW_MAX_WORDS lowers the bound below real rows (header + 1
+    message), so the bound fires on the first level with two messages: the
+    check ends with status "capacity" and the completed levels, a prefix of
+    the fixture's, instead of faulting."""
+    g = SMALL["raft_n3v1e1"]
+    monkeypatch.setenv("RMC_HF_ROW_MAX_WORDS", str(1 + 4 * 3 + 1))
+    m = model(g)
+    r = m.check_logical(shards, host_frontier=1) if shards else m.check(host_frontier=1)
+    assert r["status"] == "capacity", (r["status"], r.get("message"))
+    assert "exceeds the row width" in r["message"]
+    k = len(r["levels"])
+    assert 1 <= k < len(g["levels"])
+    assert r["levels"] == g["levels"][:k]  # the level that met the bound is not counted
+    assert r["distinct"] == sum(n for _, n in g["levels"][:k])
+
+
+def test_back_to_back_host_checks_reuse_pinned_pages(monkeypatch):
+    """r05: pinned pages outlive a check (a process-wide cache) and a page given
+    up is never unmapped, so back-to-back host-frontier checks in one process
+    -- the GPU suite's pattern, ~30 of them, when the r04 driver run faulted in
+    a copy-out -- register no address twice."""
+    monkeypatch.setenv("RMC_HOST_PAGE_ROWS", "2000")
+    for name in ("fsync_n3v1e2_unsafe", "flex_n3v2e2_eq1"):
+        g = VIOL[name]
+        for chunk in (0, 1000, 0):
+            r = model(g).check(host_frontier=1, chunk_parents=chunk)
+            assert r["status"] == "violation" and (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])

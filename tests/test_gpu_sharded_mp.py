@@ -16,10 +16,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 pytestmark = pytest.mark.gpu
 
 
-def run_ranks(world, fx, key, chunk=0):
+def run_ranks(world, fx, key, chunk=0, extra=(), env_of=None):
+    """env_of(rank) -> extra environment variables for that rank's process."""
     name = "rmc_test_" + uuid.uuid4().hex[:12]
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "sharded_shm_rank.py"), str(r), str(world), name,
-                               fx, key, str(chunk)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                               fx, key, str(chunk)] + [str(x) for x in extra], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True, env=dict(os.environ, **(env_of(r) if env_of else {})))
              for r in range(world)]
     outs = []
     for p in procs:
@@ -60,3 +62,19 @@ def test_multiprocess_shards_violation():
         assert r["status"] == "violation" and r["violated"] == g["violated"] and r["depth"] == g["depth"]
         # TLC's counts at the failing state, summed over the ranks' blocks of the round
         assert (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])
+
+
+def test_one_rank_out_of_host_pages_stops_every_rank():
+    """host pages are per process, so one rank runs out first.  Its
+    failure is agreed through the next allgather instead of leaving its peers
+    in a collective: rank 1 gets a host-page limit far below the shipped
+    Raft.cfg's levels (1000-row pages), rank 0 none -- both ranks end with
+    status "capacity" and the same completed levels, a prefix of the fixture's."""
+    g = json.load(open(os.path.join(HERE, "golden", "shipped.json")))["Raft_cfg"]
+    env = lambda r: {"RMC_HOST_PAGE_ROWS": "1000", **({"RMC_HOST_FRONTIER_GIB": "0.01"} if r == 1 else {})}
+    outs = run_ranks(2, "shipped.json", "Raft_cfg", 20000, extra=(1,), env_of=env)
+    assert [o["status"] for o in outs] == ["capacity", "capacity"], outs
+    assert "host frontier pages exhausted" in outs[1]["message"]
+    assert "another rank" in outs[0]["message"]
+    k = len(outs[0]["levels"])
+    assert outs[1]["levels"] == outs[0]["levels"] == g["levels"][:k] and 2 < k < len(g["levels"])
