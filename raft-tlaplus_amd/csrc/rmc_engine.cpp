@@ -1145,7 +1145,18 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
   if (opt->fp_bits && opt->fp_bits != 64 && opt->fp_bits != 128)
     throw std::runtime_error("fp_bits must be 64 or 128");
-  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K : (m->kmax_user ? m->kmax_user : model_kmax(m));
+  // Rows widen in place while the levels are on the device (below: a chunk
+  // whose successors need more message slots widens the current and next
+  // level's rows and is redone), so a model checked for the first time starts
+  // with rows for N messages and grows them to the search's real maximum;
+  // a host-frontier check (whose levels re-run on an overflow) starts at the
+  // constants-based default.
+  const bool widen_ok = !opt->msg_cap_K && opt->host_frontier != 1 && !(opt->recover_dir && *opt->recover_dir);
+  uint32_t kmax = opt->msg_cap_K ? opt->msg_cap_K
+                                 : m->kmax_user ? m->kmax_user
+                                 : m->hint_kmax ? m->hint_kmax
+                                 : widen_ok     ? (uint32_t)m->M.N
+                                                : default_kmax(m->M);
   if (kmax > 120) kmax = 120;
   const bool recovering = opt->recover_dir && *opt->recover_dir;
   Ckpt rc;
@@ -1200,8 +1211,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   };
   hipEvent_t evs[3] = {matdone[0], matdone[1], ev_scan};
   MStreamGuard mguard{stream, mstream, evs};
-  const size_t W = (size_t)M.words;
-  res->state_bytes = (uint32_t)(W * 4);
+  size_t W = (size_t)M.words;  // row width (words); grows when the rows widen
   const auto t_model = std::chrono::steady_clock::now();
 
   // ---- sizing
@@ -1226,14 +1236,14 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
                                            hf_hbm_fraction() * (double)hbm_total) ||
                          getenv("RMC_RECOVER_TO_HOST"));  // test hook
   if (recovering && !rec_host) fcap = std::max(fcap, rc.cur_n);
-  const int maxsucc = M.nfixed + M.kmax;
+  int maxsucc = M.nfixed + M.kmax;
   // 8M parents per launch (bench cfg: 1.325 s per check vs 1.349 s at 4M; 4M
   // was 4% below 2M, 2M 4% below 1M), held to 2^31 candidates per launch
   unsigned long long chunk = opt->chunk_parents
                                  ? opt->chunk_parents
                                  : std::min(1ULL << 23, (1ULL << 31) / (unsigned long long)std::min(maxsucc, 256) - 1024);
   // + 1024 parents of slack: each of k_expand's 8 candidate segments must hold 1/8 of the tiles, rounded up
-  const unsigned long long cand_cap = (chunk + 1024) * (unsigned long long)std::min(maxsucc, 256);
+  unsigned long long cand_cap = (chunk + 1024) * (unsigned long long)std::min(maxsucc, 256);
   // candidate indices (par_off, k_mark, k_materialize's winner list) are 32-bit
   if (cand_cap > 0xFFFFFFFFULL)
     throw std::runtime_error("chunk_parents too large: " + std::to_string(chunk) + " parents x " +
@@ -1340,6 +1350,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   m->levels.clear();
   m->trace_states.clear();
   m->trace_actions.clear();
+  m->widenings.clear();
   unsigned long long generated = 1, distinct = 1, cur_n = 1, cur_base = 0;
   unsigned depth = 1;
   m->levels.push_back({1, 1});
@@ -1403,7 +1414,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   const int hf_opt = opt->host_frontier;
   bool hf = false;
   HostPagePool pool;
-  const size_t row_bytes = W * 4;
+  size_t row_bytes = W * 4;
   size_t page_bytes = HostPagePool::PAGE_BYTES;
   // test hooks: RMC_HOST_PAGE_ROWS (small pages: rows straddle many), and
   // RMC_HOST_FRONTIER_AT=L (auto mode moves to the host before level L's
@@ -1443,7 +1454,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   // driver (a hipMalloc right after hipMemRelease of the frontiers failed on
   // the GPU box; profiles/r03/vmm_release_probe.txt), so the windows must not
   // depend on it.
-  const size_t win_in_bytes = chunk * W * 4, win_out_bytes = 3 * chunk * W * 4;
+  size_t win_in_bytes = chunk * W * 4, win_out_bytes = 3 * chunk * W * 4;
   bool windows = false;
   struct WindowsGuard {  // every exit path (an E_CAP_MSG re-run, a throw, auto mode that never switched)
     Arena& A;
@@ -1692,6 +1703,78 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     a.cand_cap = cand_cap;
     a.st = stbuf.as<DevStatus>();
   };
+  // ---- widening the rows (device frontiers): chunk [c0, c0 + n) of the
+  // current level met a successor with more messages than the rows hold.
+  // The chunk is redone at a row width for `need` messages: its claimed
+  // ranks go back to unclaimed (the message bindings' TLC ordinals depend on
+  // the slot count: k_reset_ranks), the current level's rows and the next
+  // level's rows so far are restrided (from the last row down, a slice at a
+  // time through the candidate buffer, which the redo rewrites anyway), the
+  // model's binding tables are rebuilt for the new slot count, and the
+  // chunk's status goes back to the last kept chunk's.  Widenings per check:
+  // a handful at small levels on a first check (rows start at N slots), none
+  // when the model was checked before (its last maximum is the hint).
+  unsigned widenings = 0;
+  double widen_s = 0;
+  auto widen = [&](unsigned need, unsigned long long c0, unsigned long long n) {
+    auto tw0 = now();
+    HIPCHK(hipStreamSynchronize(stream));
+    if (mstream != stream) HIPCHK(hipStreamSynchronize(mstream));
+    launch_reset_ranks(table.as<unsigned long long>(), slots, ew, (cur_base + c0 + 1) << 10,
+                       (cur_base + c0 + n + 1) << 10, stream);
+    HIPCHK(hipGetLastError());
+    const size_t Wo = W;
+    finalize_model(m, std::min(120u, need));
+    M.fpw = opt->fp_bits == 128 ? 2 : 1;
+    HIPCHK(upload_model(M));
+    W = (size_t)M.words;
+    auto restride = [&](uint32_t* rows, unsigned long long nr) {
+      const unsigned long long slice = std::max<unsigned long long>(1, cslot.bytes / (Wo * 4));
+      for (unsigned long long r1 = nr; r1 > 0;) {
+        const unsigned long long r0 = r1 > slice ? r1 - slice : 0;
+        HIPCHK(hipMemcpyAsync(cslot.p, rows + r0 * Wo, (r1 - r0) * Wo * 4, hipMemcpyDeviceToDevice, stream));
+        launch_restride(cslot.as<uint32_t>(), r1 - r0, (int)Wo, (int)W, rows + r0 * W, stream);
+        HIPCHK(hipGetLastError());
+        r1 = r0;
+      }
+    };
+    const bool cur_is_a = cur == fa.as<uint32_t>();
+    GrowBuf& gc = cur_is_a ? fa : fb;
+    GrowBuf& gn = cur_is_a ? fb : fa;
+    gc.ensure(std::max<unsigned long long>(cur_n, 1) * W * 4);
+    gn.ensure(std::max<unsigned long long>(lvl_next_n, 1) * W * 4);
+    cur = gc.as<uint32_t>();
+    nxt = gn.as<uint32_t>();
+    restride(cur, cur_n);
+    restride(nxt, lvl_next_n);
+    maxsucc = M.nfixed + M.kmax;
+    cand_cap = (chunk + 1024) * (unsigned long long)std::min(maxsucc, 256);
+    if (cand_cap > 0xFFFFFFFFULL) throw std::runtime_error("widened rows: more than 2^32 candidates per launch");
+    HIPCHK(hipStreamSynchronize(stream));  // the candidate buffer served as the slice buffer
+    cslot.ensure(cand_cap * 8);
+    cob.ensure(cand_cap * 4);
+    cwin.ensure(cand_cap * 2);
+    if (pipe) {
+      A.cslot2.ensure(cand_cap * 8);
+      A.cob2.ensure(cand_cap * 4);
+      A.cwin2.ensure(cand_cap * 2);
+    }
+    row_bytes = W * 4;
+    win_in_bytes = chunk * W * 4;
+    win_out_bytes = 3 * chunk * W * 4;
+    const unsigned zero = 0;
+    const unsigned long long none = ~0ULL;
+    HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, cap_flags), &zero, 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync((char*)stbuf.p + offsetof(DevStatus, err_key), &none, 8, hipMemcpyHostToDevice, stream));
+    restore_coll();
+    HIPCHK(hipStreamSynchronize(stream));
+    widenings++;
+    m->widenings.push_back({(unsigned long long)depth, c0, (unsigned long long)M.kmax});
+    widen_s += secs(tw0, now());
+    if (opt->verbose)
+      fprintf(stderr, "[rmc] rows widened to %zu words (%d message slots) at depth %u, chunk at %llu (%.3fs)\n", W,
+              M.kmax, depth, c0, secs(tw0, now()));
+  };
   try {
   if (rec_host) {  // the snapshot's level goes straight to host pages
     auto th0 = std::chrono::steady_clock::now();
@@ -1894,9 +1977,15 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
       if (hst.cap_flags) {
         int e = 0;
         while (!((hst.cap_flags >> e) & 1)) e++;
+        const unsigned redoable = (1u << E_CAP_MSG) | (1u << E_CAP_TABLE) | (1u << E_RETRY);
+        if (e == E_CAP_MSG && !opt->msg_cap_K && M.kmax < 120 && !hf && widen_ok && !(hst.cap_flags & ~redoable)) {
+          widen(std::max(hst.max_msgs, (unsigned)M.kmax + 1), c0, n);
+          redos++;
+          continue;
+        }
         if (e == E_CAP_MSG && !opt->msg_cap_K && M.kmax < 120) {
           // the caller re-runs with a larger message capacity
-          m->kmax_user = std::min(120u, (uint32_t)M.kmax * 2);
+          m->kmax_user = std::min(120u, std::max((uint32_t)M.kmax * 2, default_kmax(M)));
           HIPCHK(hipStreamDestroy(stream));
           return 1;
         }
@@ -2286,6 +2375,9 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   if (!opt->hash_slots) m->hint_slots = slots;
   if (!opt->frontier_cap && !hf) m->hint_fcap = fcap;
   m->hint_trcap = trcap;
+  res->state_bytes = (uint32_t)(W * 4);
+  if (opt->verbose && widenings)
+    fprintf(stderr, "[rmc] rows widened %u times (%.3fs), to %zu words\n", widenings, widen_s, W);
   res->generated = generated;
   res->distinct = distinct;
   res->left_on_queue = (status == 0) ? 0 : cur_n;
@@ -2653,6 +2745,15 @@ void rmc_release_device_memory(void) {
 // that level's first chunk stopped after each phase (diag 4: staging, 3:
 // bindings, 2: successor deltas, 1: fingerprints, no insert; 0: the real
 // launch).  Fills (diag, ms) pairs; returns how many.
+// TEST HOOK: the last check's row widenings, 3 values each (depth, first
+// parent of the redone chunk within its level, message slots after); returns
+// how many there were.
+int rmc_selftest_widenings(const rmc_model* m, uint64_t* out, int cap) {
+  const int n = (int)m->widenings.size();
+  for (int k = 0; k < n && 3 * k + 2 < cap; k++)
+    for (int j = 0; j < 3; j++) out[3 * k + j] = m->widenings[k][j];
+  return n;
+}
 int rmc_selftest_profile_expand(rmc_model* m, const rmc_options* o, int level, double* out, int cap) {
   if (!m || !o || level < 2) { g_last_error = "bad argument"; return -1; }
   if (!diag_build()) { g_last_error = "librmc was not built with -DRMC_DIAG"; return -1; }

@@ -82,6 +82,10 @@ void launch_pack_rows(const uint32_t* rows, unsigned long long n, int W, const u
                       uint32_t* out, hipStream_t s);
 void launch_unpack_rows(const uint32_t* in, unsigned long long n, int W, const uint32_t* offs, const uint32_t* lens32,
                         uint32_t* rows, hipStream_t s);
+// widening the rows mid-check (rmc_kernels.hip): reset the chunk's claimed ranks, restride rows
+void launch_reset_ranks(unsigned long long* table, unsigned long long slots, int ew, unsigned long long lo,
+                        unsigned long long hi, hipStream_t s);
+void launch_restride(const uint32_t* src, unsigned long long n, int Wo, int Wn, uint32_t* dst, hipStream_t s);
 // batched device-to-device copies (one launch for a whole exchange step)
 struct CopyDesc {
   const void* src;

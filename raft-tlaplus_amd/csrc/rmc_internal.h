@@ -7,6 +7,7 @@
 #include <string>
 #include <utility>
 #include <vector>
+#include <array>
 #include <algorithm>
 #include <sys/mman.h>
 #include <chrono>
@@ -52,6 +53,8 @@ struct rmc_model {
   // first chunk of this level; (diag, ms) pairs of the last check
   unsigned profile_level = 0;
   std::vector<std::pair<int, double>> profile_ms;
+  // the last check's row widenings (depth, first parent of the redone chunk, new message slots)
+  std::vector<std::array<unsigned long long, 3>> widenings;
 };
 
 

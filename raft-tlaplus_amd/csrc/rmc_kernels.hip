@@ -307,7 +307,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
         int adds = 0;
 #pragma unroll
         for (int q = 0; q < MAXOPS; q++) adds += (q < d.nops && d.opk[q] < 0);
-        if (h_nmsg(sS[pp * L.Wp]) + adds > cM.kmax) atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
+        const int nn = h_nmsg(sS[pp * L.Wp]) + adds;
+        if (nn > cM.kmax) {  // the row needs more message slots: the driver widens the rows (rmc_engine.cpp)
+          atomicOr(&st->cap_flags, 1u << E_CAP_MSG);
+          atomicMax(&st->max_msgs, (unsigned)nn);
+        }
       }
       atomicOr(&sOrd[pp * ordw + (d.ordinal >> 5)], 1u << (d.ordinal & 31));
     };
@@ -1405,6 +1409,47 @@ void launch_unpack_rows(const uint32_t* in, unsigned long long n, int W, const u
                         uint32_t* rows, hipStream_t s) {
   if (!n) return;
   k_unpack_rows<<<grid_for(n, 4), 256, 0, s>>>(in, n, W, offs, lens32, rows);
+}
+
+// ------------------------------------------------ widening the rows mid-check
+// A successor that needs more message slots than the rows have (E_CAP_MSG in
+// k_expand) widens every row of the current level and of the next level so
+// far, and the chunk is redone (rmc_engine.cpp).  The TLC ordinals of the
+// message bindings depend on the slot count, so the chunk's first attempt
+// left ranks of the old numbering in the entries it claimed: every entry
+// whose rank lies in the chunk's parents' range [lo, hi) goes back to the
+// value of a freshly claimed entry (~0), and the redo's atomicMin sets it
+// anew.  (Entries of earlier chunks hold other parents' ranks: TLC order
+// between them is decided by the parent, not the ordinal.)
+__global__ __launch_bounds__(256) void k_reset_ranks(unsigned long long* __restrict__ T, unsigned long long slots,
+                                                     int ew, unsigned long long lo, unsigned long long hi) {
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < slots;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    unsigned long long* v = T + (unsigned long long)ew * i + (ew >> 1);
+    const unsigned long long r = *v >> VAL_RANK_SHIFT;
+    if (*v != EMPTY && r >= lo && r < hi) *v = EMPTY;
+  }
+}
+// rows of Wo words (src, contiguous) -> rows of Wn >= Wo words at dst, zero-padded; a wave per row
+__global__ __launch_bounds__(256) void k_restride(const uint32_t* __restrict__ src, unsigned long long n, int Wo, int Wn,
+                                                  uint32_t* __restrict__ dst) {
+  const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x / WAVE);
+  for (unsigned long long r = (unsigned long long)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; r < n;
+       r += waves) {
+    const uint32_t* s = src + r * (unsigned long long)Wo;
+    uint32_t* d = dst + r * (unsigned long long)Wn;
+    for (int l = lane_id(); l < Wn; l += WAVE) d[l] = l < Wo ? s[l] : 0u;
+  }
+}
+void launch_reset_ranks(unsigned long long* table, unsigned long long slots, int ew, unsigned long long lo,
+                        unsigned long long hi, hipStream_t s) {
+  unsigned long long blocks = (slots + 255) / 256;
+  if (blocks > (1ULL << 20)) blocks = 1ULL << 20;
+  k_reset_ranks<<<(unsigned)blocks, 256, 0, s>>>(table, slots, ew, lo, hi);
+}
+void launch_restride(const uint32_t* src, unsigned long long n, int Wo, int Wn, uint32_t* dst, hipStream_t s) {
+  if (!n) return;
+  k_restride<<<grid_for(n, 4), 256, 0, s>>>(src, n, Wo, Wn, dst);
 }
 
 // ------------------------------------------------ batched device copies

@@ -106,6 +106,7 @@ def lib():
     L.rmc_trace_json.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_selftest_random_trace.argtypes = [P, ctypes.c_uint64, c_int]
     L.rmc_selftest_set_hint_kmax.argtypes = [P, ctypes.c_uint32]
+    L.rmc_selftest_widenings.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), c_int]
     L.rmc_selftest_profile_expand.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(ctypes.c_double), c_int]
     L.rmc_selftest_encode_msg.argtypes = [c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
     L.rmc_selftest_encode_kmsg.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]
@@ -298,6 +299,13 @@ class Model:
         if n < 0:
             raise RaftmcError(lib().rmc_last_error().decode())
         return [(int(buf[2 * k]), buf[2 * k + 1]) for k in range(n)]
+
+    def selftest_widenings(self):
+        """TEST HOOK: the last check's row widenings, [(depth, first parent of the
+        redone chunk within its level, message slots after), ...]."""
+        buf = (ctypes.c_uint64 * 3072)()
+        n = lib().rmc_selftest_widenings(self._h, buf, 3072)
+        return [tuple(buf[3 * k:3 * k + 3]) for k in range(min(n, 1024))]
 
     def selftest_set_hint_kmax(self, k):
         """TEST HOOK: pretend the last check saw at most k messages per state, so the

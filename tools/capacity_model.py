@@ -11,7 +11,7 @@ tests/golden/exhausted.json): cut each at the same depth as config 2's known
 prefix, predict, and compare the prediction with the true total, peak level
 and depth.  The validation errors give the band applied to config 2.
 
-    python tools/capacity_model.py > profiles/r04/capacity_model.txt
+    python tools/capacity_model.py > profiles/r05/capacity_model.txt
 """
 import json
 import math
@@ -66,24 +66,36 @@ def extrapolate(levels, window, kind):
     return sum(n), n[peak], peak + 1, len(n)
 
 
-def known_config2():
-    """Config 2 per-level new states from the compact host-frontier ladder (depth 31 reached)."""
-    txt = open(os.path.join(ROOT, "profiles", "r04", "ladder_Raft_n3v2e3_hf1_compact.txt")).read()
+def ladder(path):
+    """Per-level new states from a verbose ladder log ("[rmc] depth d: n new, ...")."""
+    txt = open(os.path.join(ROOT, path)).read()
     lv = {1: 1}
     for d, new in re.findall(r"depth (\d+): (\d+) new", txt):
         lv[int(d)] = int(new)
     return [lv[d] for d in range(1, max(lv) + 1)]
 
 
+# The BASELINE configs and rungs that do NOT exhaust on one GPU, with the
+# deepest prefix measured (the ladder logs under profiles/).
+TARGETS = [
+    ("config 2: Raft N=3 V=2 E=3 R=0 (configs/Raft_n3v2e3.cfg)",
+     "profiles/r04/ladder_Raft_n3v2e3_hf1_compact.txt", 112),
+    ("config 3: FlexibleRaft.cfg verbatim, N=5 EQ=3 RQ=4 V=2 E=2 (configs/FlexibleRaft.cfg)",
+     "profiles/r03/ladder_FlexibleRaft_hf1.txt", 160),
+    ("config 5 rung: RaftFsync N=3 V=2 E=2 R=1 (configs/RaftFsync_n3v2e2r1.cfg)",
+     "profiles/r03/ladder_RaftFsync_n3v2e2r1_hf1.txt", 112),
+    ("config 5 scaled: RaftFsync N=3 V=2 E=3 R=1 (configs/RaftFsync_n3v2e3r1.cfg)",
+     "profiles/r02/ladder_RaftFsync_n3v2e3r1.txt", 112),
+]
+EXTRA = os.environ.get("CAPACITY_EXTRA", "")  # "label|path|row_bytes;..." rungs measured later
+
+
 def main():
     ex = json.load(open(os.path.join(ROOT, "tests", "golden", "exhausted.json")))
-    c2 = known_config2()
-    cut0 = len(c2)
     cuts = (25, 27, 29, 31, 33)
     windows = (4, 6, 8, 10, 14)
     print("Capacity model (tools/capacity_model.py): linear fit of the level growth ratio r_k = n_{k+1}/n_k")
-    print("on the last W known levels, extended until r <= 0 or a level falls below one state.  Config 2 is known")
-    print("to depth %d (profiles/r04/ladder_Raft_n3v2e3_hf1_compact.txt: %d distinct states)." % (cut0, sum(c2)))
+    print("on the last W known levels, extended until r <= 0 or a level falls below one state.")
     print("(A quadratic fit of r_k was tried too: on these prefixes it curves back up and diverges -- unusable.)")
     print()
     print("Validation on the two rungs that exhaust (tests/golden/exhausted.json), cut at depths %s:" % (cuts,))
@@ -106,29 +118,38 @@ def main():
     lo, hi = min(errs[best]), max(errs[best])
     print("Best window on the validation rungs: W=%d, predicted/actual total within x%.2f .. x%.2f over %d cuts." %
           (best, lo, hi, len(errs[best])))
-    print()
-    print("Config 2 (Raft_n3v2e3), known to depth %d:" % cut0)
-    for W in windows:
-        tot, pk, pd, last = extrapolate(c2, W, "linear")
-        print("  W=%-2d: %.3e distinct, peak level %.3e at depth %d, depth %d%s" %
-              (W, tot, pk, pd, last, "  <- validated best" if W == best else ""))
-    tot, pk, pd, last = extrapolate(c2, best, "linear")
-    band = (tot / hi, tot / lo)  # truth = prediction / (predicted/actual)
-    mid = math.sqrt(band[0] * band[1])
-    print()
-    print("Estimate: config 2 has ~%.1e distinct states (band %.1e .. %.1e: the W=%d prediction %.2e divided by the "
-          "validation's predicted/actual range), a peak level of ~%.1e states near depth %d, depth ~%d." %
-          (mid, band[0], band[1], best, tot, pk / math.sqrt(lo * hi), pd, last))
     hbm = 288e9
-    for entry in (16, 8):
-        cap1 = hbm / entry * 0.75
-        print("  fingerprint set, %2d B per entry at 0.75 load: 1 GPU holds %.2e states, 8 GPUs %.2e -> config 2 "
-              "needs %.0f..%.0f GPUs' HBM for the set alone" % (entry, cap1, 8 * cap1, band[0] / cap1, band[1] / cap1))
-    for S in (192.0, 112.0):
-        print("  the peak level alone at %3.0f B per row: %.1f TB (8 x 288 GB of HBM = 2.3 TB; host pages: 8 x 270 GiB)"
-              % (S, pk / math.sqrt(lo * hi) * S / 1e12))
-    print("Conclusion: config 2 (MaxElections=3) is out of reach of one MI355X and of an 8-GPU node, by a factor of "
-          "%.0f or more in fingerprint-set capacity alone at 8 B per entry." % (band[0] / (8 * hbm / 8 * 0.75)))
+    cap = {e: hbm / e * 0.75 for e in (16, 8)}
+    print("One MI355X's fingerprint set (288 GB at 0.75 load): %.2e states at 16 B per entry, %.2e at 8 B; "
+          "an 8-GPU node: %.2e / %.2e." % (cap[16], cap[8], 8 * cap[16], 8 * cap[8]))
+    targets = list(TARGETS)
+    for item in filter(None, EXTRA.split(";")):
+        label, path, rb = item.split("|")
+        targets.append((label, path, int(rb)))
+    for label, path, row_bytes in targets:
+        lv = ladder(path)
+        print()
+        print("%s, known to depth %d (%s: %d distinct states):" % (label, len(lv), path, sum(lv)))
+        for W in windows:
+            tot, pk, pd, last = extrapolate(lv, W, "linear")
+            print("  W=%-2d: %.3e distinct, peak level %.3e at depth %d, depth %d%s" %
+                  (W, tot, pk, pd, last, "  <- validated best" if W == best else ""))
+        tot, pk, pd, last = extrapolate(lv, best, "linear")
+        band = (tot / hi, tot / lo)  # truth = prediction / (predicted/actual)
+        mid = math.sqrt(band[0] * band[1])
+        peak = pk / math.sqrt(lo * hi)
+        print("  Estimate: ~%.1e distinct states (band %.1e .. %.1e), a peak level of ~%.1e states near depth %d, "
+              "depth ~%d." % (mid, band[0], band[1], peak, pd, last))
+        for e in (16, 8):
+            print("    fingerprint set at %2d B per entry: needs %.1f..%.1f GPUs' HBM (an 8-GPU node holds %.2e)"
+                  % (e, band[0] / cap[e], band[1] / cap[e], 8 * cap[e]))
+        print("    the peak level at %d B per compact row: %.2f TB (8 x 288 GB of HBM = 2.3 TB; host pages 8 x 270 GiB = "
+              "2.3 TB)" % (row_bytes, peak * row_bytes / 1e12))
+        fits = band[1] <= 8 * cap[8]
+        print("    -> %s" % ("fits an 8-GPU node's fingerprint sets (8 B entries) even at the band's top" if fits else
+                            "fits an 8-GPU node only if the truth is near the band's bottom" if band[0] <= 8 * cap[8]
+                            else "out of reach of an 8-GPU node by a factor of %.0f at the band's bottom (8 B entries)"
+                            % (band[0] / (8 * cap[8]))))
 
 
 if __name__ == "__main__":
