@@ -571,6 +571,9 @@ struct Hasher {
   const Module& m;
   std::map<std::string, uint64_t> memo;
   std::set<std::string> active;
+  // identifiers and applied operators that are neither bound, nor defined in
+  // the module, nor declared: they must be standard-module operators (lower())
+  std::set<std::string> unresolved;
   // innermost last: (name, is_local_def, local def hash)
   struct Ent { std::string name; bool def; uint64_t h; size_t nparams; };
   std::vector<Ent> env;
@@ -647,6 +650,7 @@ struct Hasher {
         bool d;
         if (lookup(n->s, r, d)) return d ? hcomb(hstr("ldef"), r) : r;
         if (!is_declared(n->s) && m.find(n->s)) return hcomb(hstr("ref"), def_hash(n->s));
+        if (!is_declared(n->s)) unresolved.insert(n->s);
         return hcomb(hstr("name"), hstr(n->s));
       }
       case N_APP: {
@@ -654,7 +658,10 @@ struct Hasher {
         bool d;
         if (lookup(n->s, r, d) && d) h = hcomb(hstr("lapp"), r);
         else if (m.find(n->s) && !is_declared(n->s)) h = hcomb(hstr("app"), def_hash(n->s));
-        else h = hcomb(hstr("builtin"), hstr(n->s));
+        else {
+          if (!is_declared(n->s)) unresolved.insert(n->s);
+          h = hcomb(hstr("builtin"), hstr(n->s));
+        }
         for (auto& c : n->k) h = hcomb(h, node(c));
         return h;
       }
@@ -790,6 +797,7 @@ Module parse_module(const std::string& text) {
       continue;
     }
     // ASSUME, THEOREM, INSTANCE, ...: skipped to the next unit
+    if (x.k == T_ID) m.skipped.push_back({x.s, x.line});
     i++;
     while (i < t.size() && !unit_start(t, i)) i++;
   }
@@ -930,9 +938,33 @@ std::string action_name(int spec, int act) {
   return "?";
 }
 
+// The standard modules a lowered spec may EXTEND, and the operators they (and
+// the TLA+ core) give an identifier that no definition of the module binds.
+// An identifier outside this list is an operator the hashing cannot see into
+// (a user module's, a LOCAL or INSTANCE'd one): an edit to it would leave the
+// action hashes unchanged, so the lowering refuses it.
+static const std::set<std::string> kStdModules = {"Naturals", "Integers", "Sequences", "FiniteSets", "TLC", "Bags"};
+static const std::set<std::string> kStdOps = {
+    "TRUE", "FALSE", "BOOLEAN", "STRING", "Nat", "Int",                                  // core, Naturals, Integers
+    "Seq", "Len", "Append", "Head", "Tail", "SubSeq", "SelectSeq",                         // Sequences
+    "IsFiniteSet", "Cardinality",                                                           // FiniteSets
+    "Print", "PrintT", "Assert", "JavaTime", "TLCGet", "TLCSet", "Permutations", "SortSeq",  // TLC
+    "RandomElement", "Any", "ToString", "TLCEval",
+    "IsABag", "BagToSet", "SetToBag", "BagIn", "EmptyBag", "CopiesIn", "BagCup", "BagDiff",  // Bags
+    "BagUnion", "SubBag", "BagOfAll", "BagCardinality"};
+
 Lowering lower(const std::string& text, const std::string& next, const std::string& view,
                const std::string& symmetry, const std::vector<std::string>& invariants) {
   Module m = parse_module(text);
+  for (const std::string& e : m.extends)
+    if (!kStdModules.count(e))
+      throw std::runtime_error("module " + m.name + " EXTENDS " + e + ": the lowering reads a module's own text and "
+                               "the standard modules (Naturals, Integers, Sequences, FiniteSets, TLC, Bags) only");
+  for (auto& u : m.skipped)
+    if (u.first == "LOCAL" || u.first == "INSTANCE" || u.first == "RECURSIVE")
+      throw std::runtime_error("module " + m.name + ": " + u.first + " (line " + std::to_string(u.second) +
+                               ") is not supported by the lowering (its operators would not be seen by the closure "
+                               "hashes)");
   Hasher H(m);
   auto hash_of = [&](const std::string& name) -> uint64_t {
     if (!m.find(name)) throw std::runtime_error("module " + m.name + " defines no " + name);
@@ -956,7 +988,19 @@ Lowering lower(const std::string& text, const std::string& next, const std::stri
       if (k.spec == L.spec && k.role == role && k.hash == h) return &k;
     return nullptr;
   };
-  for (const Disjunct& dj : next_disjuncts(m, next)) {
+  const std::vector<Disjunct> djs = next_disjuncts(m, next);
+  {  // hash everything the cfg names first: an unresolved identifier is reported as such
+    for (const Disjunct& dj : djs) (void)hash_of(dj.op);
+    for (const std::string& inv : invariants)
+      if (m.find(inv)) (void)hash_of(inv);
+    if (!view.empty()) (void)hash_of(view);
+    if (!symmetry.empty()) (void)hash_of(symmetry);
+    for (const std::string& u : H.unresolved)
+      if (!kStdOps.count(u))
+        throw std::runtime_error("module " + m.name + " uses " + u + ", which it neither defines nor declares and no "
+                                 "standard module the lowering knows defines");
+  }
+  for (const Disjunct& dj : djs) {
     const uint64_t h = hash_of(dj.op);
     const Known* k = find(R_ACTION, h);
     if (!k)

@@ -143,7 +143,7 @@ def load(tmp_path, text, cfg, module="Raft"):
 def add_unused(text):
     """A semantics-preserving edit that changes the file's hash: the module
     then goes through the front end instead of the verbatim-text check."""
-    i = text.rindex("====")
+    i = text.rindex("\n====") + 1  # before the closing line (rindex("====") lands inside a longer rule)
     return text[:i] + "\nFrontEndProbe == 42\n" + text[i:]
 
 
@@ -235,3 +235,42 @@ def test_changed_binding_is_refused(tmp_path):
     cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
     with pytest.raises(raftmc.RaftmcError, match="form the lowering does not bind"):
         load(tmp_path, text, cfg)
+
+
+def _raft_cfg():
+    return open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
+
+
+@needs_ref
+def test_nonstandard_extends_is_refused(tmp_path):
+    """an operator taken from a user module in EXTENDS is invisible
+    to the closure hashes, so such a module is refused, not checked with the
+    built-in lowering's semantics."""
+    text = ref_text("Raft").replace("EXTENDS Naturals, FiniteSets, Sequences, TLC",
+                                    "EXTENDS Naturals, FiniteSets, Sequences, TLC, MyHelpers")
+    assert text != ref_text("Raft")
+    with pytest.raises(raftmc.RaftmcError, match="EXTENDS MyHelpers"):
+        load(tmp_path, text, _raft_cfg())
+
+
+@needs_ref
+@pytest.mark.parametrize("unit", ["LOCAL LocalQuorum == {i \\in SUBSET(Server) : Cardinality(i) * 2 > Cardinality(Server)}",
+                                  "INSTANCE Naturals"])
+def test_local_and_instance_units_are_refused(tmp_path, unit):
+    text = add_unused(ref_text("Raft"))
+    i = text.rindex("\n====") + 1
+    text = text[:i] + "\n" + unit + "\n" + text[i:]
+    with pytest.raises(raftmc.RaftmcError, match="LOCAL|INSTANCE"):
+        load(tmp_path, text, _raft_cfg())
+
+
+@needs_ref
+def test_unresolved_identifier_is_refused(tmp_path):
+    """An action that calls an operator the module neither defines nor declares
+    (and no standard module defines) is refused, naming it."""
+    text = ref_text("Raft")
+    k = text.index("RequestVote(i) ==")
+    j = text.index("electionCtr < MaxElections", k)
+    text = text[:j] + "ElectionBudget(electionCtr)" + text[j + len("electionCtr < MaxElections"):]
+    with pytest.raises(raftmc.RaftmcError, match="ElectionBudget"):
+        load(tmp_path, text, _raft_cfg())
