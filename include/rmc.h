@@ -177,6 +177,16 @@ int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
  * rmc_last_error()).  rmc_model_next writes the model's current Next the same
  * way and returns its length. */
 int rmc_model_set_next(rmc_model* m, const char* disjuncts);
+/* The guard of one of Next's simple actions (Restart, RequestVote, Timeout,
+ * BecomeLeader, ClientRequest) as TLA+ expression text over the state
+ * variables, the cfg's constants and the action's parameters (`params`, e.g.
+ * "i" or "i, v"), with the family's Quorum and LastTerm in scope -- what a
+ * module whose action keeps the reference body but states another guard
+ * lowers to through the TLA+ front end (the reference's effect runs behind
+ * the compiled guard; rmc_guard.cpp).  E.g. rmc_model_set_guard(m,
+ * "RequestVote", "i", "electionCtr <= MaxElections /\ state[i] = Follower").
+ * Returns 0, or a negative value (rmc_last_error()). */
+int rmc_model_set_guard(rmc_model* m, const char* action, const char* params, const char* expr);
 int rmc_model_next(const rmc_model* m, char* out, size_t len);
 /* The TLA+ front end's structural hashes of a module's definitions (the
  * closure hashes the lowering matches against its action library; used by

@@ -13,7 +13,7 @@ from .cfg import load_cfg, parse_cfg
 from .tlc import bfs, EvalError
 
 
-def make_spec(module, cfg, next_order=None):
+def make_spec(module, cfg, next_order=None, guards=None):
     from .raft import RaftSpec
     from .variants import FlexibleRaftSpec, RaftFsyncSpec, PullRaftSpec, PullRaftVariant2Spec
     from .kraft import KRaftSpec
@@ -22,6 +22,11 @@ def make_spec(module, cfg, next_order=None):
              "PullRaftVariant2": PullRaftVariant2Spec, "KRaft": KRaftSpec}
     if module not in table:
         raise ValueError("oracle: unsupported module %r" % module)
+    kw = {}
     if next_order:
-        return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]), next_order=next_order)
-    return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]))
+        kw["next_order"] = next_order
+    if guards:
+        if module == "KRaft":
+            raise ValueError("oracle: guard overrides are not offered for KRaft")
+        kw["guards"] = guards
+    return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]), **kw)

@@ -30,7 +30,12 @@ class RaftSpec:
     # view == <<messages, serverVars, candidateVars, leaderVars, logVars>> (Raft.tla:115)
     hidden_vars = ("acked", "electionCtr", "restartCtr")
 
-    def __init__(self, consts, invariants=("LeaderHasAllAckedValues", "NoLogDivergence"), next_order=None):
+    def __init__(self, consts, invariants=("LeaderHasAllAckedValues", "NoLogDivergence"), next_order=None,
+                 guards=None):
+        # guards: {action name: g(spec, s, *args) -> bool} replacing the
+        # reference's guard of that action (its effect unchanged): the oracle
+        # side of the front end's compiled guards (rmc_guard.cpp)
+        self.guards = dict(guards or {})
         # next_order: Next's disjuncts by operator name, in order (default: the
         # module's own Next); may drop disjuncts or add the network actions the
         # module defines but leaves commented out of Next (Raft.tla:540-541)
@@ -54,6 +59,11 @@ class RaftSpec:
 
     def setup(self, consts):
         pass
+
+    def _guard(self, name, s, args, reference):
+        """The action's guard: an override from `guards`, else the reference's (a thunk)."""
+        g = self.guards.get(name)
+        return g(self, s, *args) if g is not None else reference()
 
     # ---------------------------------------------------------------- helpers
     def IsQuorum(self, s):
@@ -151,7 +161,7 @@ class RaftSpec:
     # ---------------------------------------------------------------- actions
     def Restart(self, s, i):
         # Raft.tla:226-235
-        if not s["restartCtr"] < self.MaxRestarts:
+        if not self._guard("Restart", s, (i,), lambda: s["restartCtr"] < self.MaxRestarts):
             return
         N = self.N
         t = dict(s)
@@ -166,9 +176,8 @@ class RaftSpec:
 
     def RequestVote(self, s, i):
         # Raft.tla:242-257
-        if not s["electionCtr"] < self.MaxElections:
-            return
-        if s["state"][i] not in (FOLLOWER, CANDIDATE):
+        if not self._guard("RequestVote", s, (i,), lambda: s["electionCtr"] < self.MaxElections and
+                           s["state"][i] in (FOLLOWER, CANDIDATE)):
             return
         term = s["currentTerm"][i] + 1
         ms = [Rec(mtype=RVREQ, mterm=term, mlastLogTerm=self.LastTerm(s["log"][i]),
@@ -212,7 +221,8 @@ class RaftSpec:
 
     def BecomeLeader(self, s, i):
         # Raft.tla:289-300
-        if s["state"][i] != CANDIDATE or not self.IsQuorum(s["votesGranted"][i]):
+        if not self._guard("BecomeLeader", s, (i,), lambda: s["state"][i] == CANDIDATE and
+                           self.IsQuorum(s["votesGranted"][i])):
             return
         N = self.N
         t = dict(s)
@@ -224,7 +234,7 @@ class RaftSpec:
 
     def ClientRequest(self, s, i, v):
         # Raft.tla:304-313
-        if s["state"][i] != LEADER or s["acked"][v] != NIL:
+        if not self._guard("ClientRequest", s, (i, v), lambda: s["state"][i] == LEADER and s["acked"][v] == NIL):
             return
         entry = Rec(term=s["currentTerm"][i], value=v)
         t = dict(s)

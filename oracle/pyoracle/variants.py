@@ -62,7 +62,7 @@ class FlexibleRaftSpec(_SendOnceOnly, RaftSpec):
 
     def Restart(self, s, i):
         # FlexibleRaft.tla:200-208
-        if not s["restartCtr"] < self.MaxRestarts:
+        if not self._guard("Restart", s, (i,), lambda: s["restartCtr"] < self.MaxRestarts):
             return
         N = self.N
         t = dict(s)
@@ -101,7 +101,8 @@ class FlexibleRaftSpec(_SendOnceOnly, RaftSpec):
 
     def BecomeLeader(self, s, i):
         # FlexibleRaft.tla:260-269: Cardinality(votesGranted[i]) >= ElectionQuorumSize
-        if s["state"][i] != CANDIDATE or not len(s["votesGranted"][i]) >= self.ElectionQuorumSize:
+        if not self._guard("BecomeLeader", s, (i,), lambda: s["state"][i] == CANDIDATE and
+                           len(s["votesGranted"][i]) >= self.ElectionQuorumSize):
             return
         N = self.N
         t = dict(s)
@@ -138,7 +139,7 @@ class RaftFsyncSpec(_SendOnceOnly, RaftSpec):
 
     def Restart(self, s, i):
         # RaftFsync.tla:203-218
-        if not s["restartCtr"] < self.MaxRestarts:
+        if not self._guard("Restart", s, (i,), lambda: s["restartCtr"] < self.MaxRestarts):
             return
         N = self.N
         t = dict(s)
@@ -160,9 +161,8 @@ class RaftFsyncSpec(_SendOnceOnly, RaftSpec):
 
     def Timeout(self, s, i):
         # RaftFsync.tla:222-230
-        if not s["electionCtr"] < self.MaxElections:
-            return
-        if s["state"][i] not in (FOLLOWER, CANDIDATE):
+        if not self._guard("Timeout", s, (i,), lambda: s["electionCtr"] < self.MaxElections and
+                           s["state"][i] in (FOLLOWER, CANDIDATE)):
             return
         t = dict(s)
         t["state"] = fset(s["state"], i, CANDIDATE)
@@ -174,7 +174,7 @@ class RaftFsyncSpec(_SendOnceOnly, RaftSpec):
 
     def RequestVoteIJ(self, s, i, j):
         # RaftFsync.tla:234-243
-        if s["state"][i] != CANDIDATE or i == j:
+        if not self._guard("RequestVote", s, (i, j), lambda: s["state"][i] == CANDIDATE and i != j):
             return
         m = Rec(mtype=RVREQ, mterm=s["currentTerm"][i], mlastLogTerm=self.LastTerm(s["log"][i]),
                 mlastLogIndex=len(s["log"][i]), msource=i, mdest=j)
@@ -195,7 +195,8 @@ class RaftFsyncSpec(_SendOnceOnly, RaftSpec):
 
     def BecomeLeader(self, s, i):
         # RaftFsync.tla:276-285
-        if s["state"][i] != CANDIDATE or not self.IsQuorum(s["votesGranted"][i]):
+        if not self._guard("BecomeLeader", s, (i,), lambda: s["state"][i] == CANDIDATE and
+                           self.IsQuorum(s["votesGranted"][i])):
             return
         N = self.N
         t = dict(s)
@@ -343,7 +344,7 @@ class PullRaftSpec(RaftSpec):
 
     def Restart(self, s, i):
         # PullRaft.tla:258-265
-        if not s["restartCtr"] < self.MaxRestarts:
+        if not self._guard("Restart", s, (i,), lambda: s["restartCtr"] < self.MaxRestarts):
             return
         t = dict(s)
         t["state"] = fset(s["state"], i, FOLLOWER)
@@ -366,9 +367,8 @@ class PullRaftSpec(RaftSpec):
 
     def RequestVote(self, s, i):
         # PullRaft.tla:283-298
-        if not s["electionCtr"] < self.MaxElections:
-            return
-        if s["state"][i] not in (FOLLOWER, CANDIDATE):
+        if not self._guard("RequestVote", s, (i,), lambda: s["electionCtr"] < self.MaxElections and
+                           s["state"][i] in (FOLLOWER, CANDIDATE)):
             return
         term = s["currentTerm"][i] + 1
         ms = [Rec(mtype=RVREQ, mterm=term, mlastLogTerm=self.LastTerm(s["log"][i]),
@@ -413,7 +413,8 @@ class PullRaftSpec(RaftSpec):
 
     def BecomeLeader(self, s, i):
         # PullRaft.tla:354-366
-        if s["state"][i] != CANDIDATE or not self.IsQuorum(s["votesGranted"][i]):
+        if not self._guard("BecomeLeader", s, (i,), lambda: s["state"][i] == CANDIDATE and
+                           self.IsQuorum(s["votesGranted"][i])):
             return
         ms = [Rec(mtype=LNREQ, mterm=s["currentTerm"][i], msource=i, mdest=j)
               for j in self.Server if j not in s["votesGranted"][i]]
@@ -619,7 +620,7 @@ class PullRaftVariant2Spec(PullRaftSpec):
 
     def Restart(self, s, i):
         # PullRaftVariant2.tla:251-260
-        if not s["restartCtr"] < self.MaxRestarts:
+        if not self._guard("Restart", s, (i,), lambda: s["restartCtr"] < self.MaxRestarts):
             return
         t = dict(s)
         t["state"] = fset(s["state"], i, FOLLOWER)
@@ -645,9 +646,8 @@ class PullRaftVariant2Spec(PullRaftSpec):
 
     def RequestVote(self, s, i):
         # PullRaftVariant2.tla:279-295
-        if not s["electionCtr"] < self.MaxElections:
-            return
-        if s["state"][i] not in (FOLLOWER, CANDIDATE):
+        if not self._guard("RequestVote", s, (i,), lambda: s["electionCtr"] < self.MaxElections and
+                           s["state"][i] in (FOLLOWER, CANDIDATE)):
             return
         term = s["currentTerm"][i] + 1
         ms = [Rec(mtype=RVREQ, mterm=term, mlastLogTerm=self.LastTerm(s["log"][i]),
@@ -709,7 +709,8 @@ class PullRaftVariant2Spec(PullRaftSpec):
     def BecomeLeader(self, s, i):
         # PullRaftVariant2.tla:361-379: notify every other server, with the last
         # common entry for the voters whose last entry is known
-        if s["state"][i] != CANDIDATE or not self.IsQuorum(s["votesGranted"][i]):
+        if not self._guard("BecomeLeader", s, (i,), lambda: s["state"][i] == CANDIDATE and
+                           self.IsQuorum(s["votesGranted"][i])):
             return
         ms = []
         for j in self.Server:

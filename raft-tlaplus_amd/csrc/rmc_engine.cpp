@@ -347,6 +347,42 @@ static bool defines_operator(const std::string& tla, const std::string& name) {
   return false;
 }
 
+// Compile the guards the front end lowered onto library effects (rmc_guard.cpp)
+// against this model's constants, into Model::gcode / gstart (all of them:
+// gs replaces the model's compiled guards).
+void install_guards(rmc_model* m, const std::vector<rmc::tla::GuardSrc>& gs) {
+  Model& M = m->M;
+  rmc::tla::GuardEnv env;
+  env.spec = M.spec;
+  env.N = M.N;
+  env.V = M.V;
+  env.servers = m->server_names;
+  env.values = m->value_names;
+  for (auto& kv : m->int_consts) env.ints.insert(kv);
+  std::vector<uint32_t> code;
+  std::vector<std::pair<int, int>> starts;
+  for (const auto& g : gs) {
+    const int kind = g.act == A_CLIENT ? K_IV : g.act == A_RVIJ ? K_IJ : K_I;
+    const std::vector<int> types = kind == K_IV ? std::vector<int>{0, 1} : kind == K_IJ ? std::vector<int>{0, 0}
+                                                                                         : std::vector<int>{0};
+    if (g.params.size() != types.size())
+      throw std::runtime_error("guard of " + g.op + ": " + std::to_string(g.params.size()) +
+                               " parameters, the action binds " + std::to_string(types.size()));
+    std::vector<uint32_t> c = rmc::tla::compile_guard(*g.mod, g.params, types, g.conjuncts, env, g.op);
+    starts.push_back({g.act, (int)code.size()});
+    code.insert(code.end(), c.begin(), c.end());
+  }
+  if (code.size() > (size_t)MAXGCODE)
+    throw std::runtime_error("compiled guards take " + std::to_string(code.size()) + " words (at most " +
+                             std::to_string(MAXGCODE) + ")");
+  for (int a = 0; a < A_NUM; a++) M.gstart[a] = -1;
+  memset(M.gcode, 0, sizeof M.gcode);
+  for (size_t q = 0; q < code.size(); q++) M.gcode[q] = code[q];
+  for (auto& s2 : starts) M.gstart[s2.first] = (int16_t)s2.second;
+  M.gany = starts.empty() ? 0 : 1;
+  m->guard_srcs = gs;
+}
+
 rmc_model* load_model(const std::string& module, const std::string& cfg_text, const std::string& tla_text) {
   auto m = new rmc_model();
   try {
@@ -390,6 +426,7 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     };
     Model& M = m->M;
     memset(&M, 0, sizeof M);
+    for (int a = 0; a < A_NUM; a++) M.gstart[a] = -1;  // the library's guards
     M.spec = spec;
     CfgVal& S = need("Server");
     CfgVal& Vv = need("Value");
@@ -399,6 +436,7 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     for (auto& kv : c.consts) {
       const CfgVal& v = kv.second;
       std::string t;
+      if (v.kind == CfgVal::INT) m->int_consts[kv.first] = v.i;
       switch (v.kind) {
         case CfgVal::INT: t = std::to_string(v.i); break;
         case CfgVal::BOOL: t = v.b ? "TRUE" : "FALSE"; break;
@@ -503,6 +541,7 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
                         "leader", "pendingFetch", "log", "highWatermark", "votesGranted", "endOffset"};
         break;
     }
+    if (!low.guards.empty()) install_guards(m, low.guards);
   } catch (std::exception& e) {
     delete m;
     throw;
@@ -945,6 +984,9 @@ unsigned long long model_signature(const rmc_model* m) {
   for (int q = 0; q < M.ninv; q++) s += "|inv" + std::to_string(M.inv[q]);
   for (auto& n : m->server_names) s += "|s:" + n;
   for (auto& n : m->value_names) s += "|v:" + n;
+  for (int a = 0; a < A_NUM; a++)  // compiled guards (rmc_guard.cpp) are part of the model
+    if (M.gstart[a] >= 0) s += "|g" + std::to_string(a) + ":" + std::to_string(M.gstart[a]);
+  for (int q = 0; q < MAXGCODE && M.gcode[q]; q++) s += "," + std::to_string(M.gcode[q]);
   return fnv1a64(s);
 }
 static void ckpt_write(const std::string& path, const void* dev, size_t bytes, void* stage, size_t stage_bytes) {
@@ -1145,6 +1187,8 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   if (opt->deadlock_check) throw std::runtime_error("deadlock checking is not supported; run with -deadlock (README.md:6)");
   if (opt->fp_bits && opt->fp_bits != 64 && opt->fp_bits != 128)
     throw std::runtime_error("fp_bits must be 64 or 128");
+  if (opt->fp_bits == 128 && m->M.gany)
+    throw std::runtime_error("a model with compiled guards is checked with 64-bit fingerprints");
   // Rows widen in place while the levels are on the device (below: a chunk
   // whose successors need more message slots widens the current and next
   // level's rows and is redone), so a model checked for the first time starts
@@ -2481,6 +2525,50 @@ int rmc_model_set_next(rmc_model* m, const char* disjuncts) {
     if (names.empty()) throw std::runtime_error("empty Next");
     m->lowered_actions = rmc::tla::actions_by_name(m->M.spec, names);
     m->lowered_labels = names;
+    m->hint_slots = m->hint_fcap = m->hint_trcap = 0;
+    m->hint_kmax = 0;
+    return 0;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -2;
+  }
+}
+
+int rmc_model_set_guard(rmc_model* m, const char* action, const char* params, const char* expr) {
+  if (!m || !action || !params || !expr) { g_last_error = "null argument"; return -1; }
+  try {
+    const int spec = m->M.spec;
+    if (spec == KRAFT) throw std::runtime_error("compiled guards are not offered for KRaft");
+    const int act = rmc::tla::actions_by_name(spec, {std::string(action)})[0].first;
+    if (act != A_RESTART && act != A_REQUESTVOTE && act != A_TIMEOUT && act != A_RVIJ && act != A_BECOMELEADER &&
+        act != A_CLIENT)
+      throw std::runtime_error(std::string("the guard of ") + action + " is not one the front end compiles (Restart, "
+                               "RequestVote, Timeout, BecomeLeader, ClientRequest)");
+    std::vector<std::string> ps;
+    std::string cur;
+    for (const char* p = params;; p++) {
+      if (*p == ',' || *p == 0) {
+        while (!cur.empty() && cur.back() == ' ') cur.pop_back();
+        if (!cur.empty()) ps.push_back(cur);
+        cur.clear();
+        if (!*p) break;
+      } else if (!(cur.empty() && *p == ' ')) {
+        cur += *p;
+      }
+    }
+    std::vector<rmc::tla::GuardSrc> all;
+    for (auto& g : m->guard_srcs)
+      if (g.act != act) all.push_back(g);
+    all.push_back(rmc::tla::parse_guard(spec, act, action, ps, expr));
+    const Model saved = m->M;
+    const std::vector<rmc::tla::GuardSrc> saved_srcs = m->guard_srcs;
+    try {
+      install_guards(m, all);
+    } catch (...) {
+      m->M = saved;
+      m->guard_srcs = saved_srcs;
+      throw;
+    }
     m->hint_slots = m->hint_fcap = m->hint_trcap = 0;
     m->hint_kmax = 0;
     return 0;

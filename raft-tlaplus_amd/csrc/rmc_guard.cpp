@@ -1,0 +1,578 @@
+// rmc_guard.cpp — the TLA+ front end's guard compiler.
+//
+// A Next disjunct whose operator differs from every library action, but whose
+// EFFECT -- the conjuncts that prime a variable, say UNCHANGED or call an
+// operator that does -- is a library action's effect exactly (same effect
+// hash, rmc_tla.cpp effect_hash), is checked with the library's effect run
+// unguarded behind ITS OWN guard, compiled here from the module's guard
+// conjuncts into the stack-machine code rmc_spec.h guard_vm runs on the
+// device (and in the CPU engine: the same code).  E.g. Raft.tla:242-257's
+// RequestVote with `electionCtr <= MaxElections`, or a BecomeLeader
+// (Raft.tla:289-300) that wants every vote.
+//
+// The guard language is the specs' expression subset over the state, typed
+// as the packed layout stores it: per-server variables (state, currentTerm,
+// votedFor / leader, commitIndex, fsyncIndex, votesGranted, Len(log[x]),
+// log[x][k].term / .value, nextIndex / matchIndex / pendingResponse rows),
+// electionCtr, restartCtr, acked[v]; the cfg's constants and model values;
+// integers (+ - *, comparisons), booleans (/\ \/ ~ => short-circuit, as TLC
+// evaluates them), sets of servers / values / states as bitmasks (\in,
+// \notin, \subseteq, \cup, \cap, \, Cardinality, SUBSET, set filters such as
+// Quorum), IF/THEN/ELSE, LET, \E / \A over constant sets (unrolled), and the
+// module's own operators (inlined).  Anything else is refused, naming it.
+#include <functional>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rmc_spec.h"
+#include "rmc_tla.h"
+
+namespace rmc {
+namespace tla {
+namespace {
+
+enum Ty { T_INT, T_BOOL, T_SRV, T_VAL, T_STATE, T_ACK, T_SET_SRV, T_SET_VAL, T_SET_STATE, T_NIL, T_TRUE, T_FALSE };
+
+const char* ty_name(Ty t) {
+  static const char* n[] = {"an integer", "a boolean", "a server", "a value", "a server state", "an acked value",
+                            "a set of servers", "a set of values", "a set of states", "Nil", "TRUE", "FALSE"};
+  return n[t];
+}
+
+struct Compiler;
+
+// A name in scope: an action parameter (ARG n), a constant of an unrolled
+// quantifier, or a macro (an operator of the module / LET, inlined at use).
+struct Binding {
+  enum K { ARG, CONSTV, MACRO } k = ARG;
+  int v = 0;
+  Ty ty = T_INT;
+  const Def* def = nullptr;  // MACRO: its definition
+  // MACRO arguments bound to expressions in the caller's scope
+  std::vector<std::pair<std::string, std::pair<NodeP, std::shared_ptr<struct Scope>>>> args;
+};
+struct Scope {
+  std::map<std::string, Binding> names;
+  std::shared_ptr<Scope> up;
+  const Binding* find(const std::string& n) const {
+    for (const Scope* s = this; s; s = s->up.get()) {
+      auto it = s->names.find(n);
+      if (it != s->names.end()) return &it->second;
+    }
+    return nullptr;
+  }
+};
+using ScopeP = std::shared_ptr<Scope>;
+
+// An expression argument of an inlined operator, evaluated in its caller's scope.
+struct Arg {
+  NodeP n;
+  ScopeP sc;
+};
+
+struct Compiler {
+  const Module& m;
+  const GuardEnv& env;
+  std::vector<uint32_t> code;
+  std::string where;  // the action, for messages
+  // parameters of inlined operators: name -> argument (innermost last)
+  std::vector<std::pair<std::string, Arg>> params;
+  int depth = 0;
+
+  Compiler(const Module& mod, const GuardEnv& e) : m(mod), env(e) {}
+
+  [[noreturn]] void fail(const NodeP& n, const std::string& what) {
+    throw std::runtime_error("guard of " + where + " (line " + std::to_string(n ? n->line : 0) + "): " + what);
+  }
+  void emit(uint32_t op, int imm = 0) { code.push_back(g_ins(op, imm)); }
+  size_t jump(uint32_t op) {
+    code.push_back(g_ins(op, 0));
+    return code.size() - 1;
+  }
+  void patch(size_t at) { code[at] = (code[at] & 0xFFu) | ((uint32_t)((int)(code.size() - at - 1)) << 8); }
+
+  const Arg* param(const std::string& s) const {
+    for (size_t q = params.size(); q-- > 0;)
+      if (params[q].first == s) return &params[q].second;
+    return nullptr;
+  }
+
+  // emit code for a symbolic constant (Nil / TRUE / FALSE) compared with a value of type t
+  int sym_code(Ty sym, Ty t, const NodeP& n) {
+    if (sym == T_NIL) {
+      if (t == T_SRV) return NILS;
+      if (t == T_ACK) return 0;
+      fail(n, std::string("Nil compared with ") + ty_name(t));
+    }
+    if (t == T_ACK) return sym == T_TRUE ? 2 : 1;
+    if (t == T_BOOL) return sym == T_TRUE ? 1 : 0;
+    fail(n, std::string("TRUE/FALSE compared with ") + ty_name(t));
+  }
+  static bool is_sym(Ty t) { return t == T_NIL || t == T_TRUE || t == T_FALSE; }
+  // a symbolic constant where a value is needed on its own (a boolean TRUE/FALSE)
+  Ty concrete(Ty t, const NodeP& n) {
+    if (t == T_TRUE || t == T_FALSE) {
+      emit(G_CONST, t == T_TRUE);
+      return T_BOOL;
+    }
+    if (t == T_NIL) fail(n, "Nil outside a comparison");
+    return t;
+  }
+  Ty elem_of(Ty set, const NodeP& n) {
+    if (set == T_SET_SRV) return T_SRV;
+    if (set == T_SET_VAL) return T_VAL;
+    if (set == T_SET_STATE) return T_STATE;
+    fail(n, std::string("membership in ") + ty_name(set));
+  }
+  Ty set_of(Ty e, const NodeP& n) {
+    if (e == T_SRV) return T_SET_SRV;
+    if (e == T_VAL) return T_SET_VAL;
+    if (e == T_STATE) return T_SET_STATE;
+    fail(n, std::string("a set of ") + ty_name(e));
+  }
+
+  // variables indexed by one server: the load op and the value type
+  bool server_var(const std::string& v, uint32_t& op, Ty& ty) {
+    const int spec = env.spec;
+    if (v == "state") { op = G_ST; ty = T_STATE; return true; }
+    if (v == "currentTerm") { op = G_TERM; ty = T_INT; return true; }
+    if (v == "commitIndex") { op = G_COMMIT; ty = T_INT; return true; }
+    if (v == "fsyncIndex" && spec == FSYNC) { op = G_FSYNC; ty = T_INT; return true; }
+    if (v == "votesGranted") { op = G_VOTES; ty = T_SET_SRV; return true; }
+    if (v == "votedFor" && spec != PULL) { op = spec == PULL2 ? G_VOTED2 : G_VOTED; ty = T_SRV; return true; }
+    if (v == "leader" && pullish(spec)) { op = G_VOTED; ty = T_SRV; return true; }
+    return false;
+  }
+  bool pair_var(const std::string& v, uint32_t& op, Ty& ty) {
+    if (v == "nextIndex" && !pullish(env.spec)) { op = G_NEXT; ty = T_INT; return true; }
+    if (v == "matchIndex") { op = G_MATCH; ty = T_INT; return true; }
+    if (v == "pendingResponse" && env.spec == RAFT) { op = G_PEND; ty = T_BOOL; return true; }
+    return false;
+  }
+
+  // log[x] as an operand of Len / indexing: the server expression
+  bool log_of(const NodeP& n, ScopeP sc, Arg& x) {
+    if (n->kind == N_ID) {
+      if (const Arg* a = param(n->s)) return log_of(a->n, a->sc, x);
+      if (sc->find(n->s)) return false;
+    }
+    if (n->kind == N_FAPP && n->k.size() == 2 && n->k[0]->kind == N_ID && n->k[0]->s == "log" && !sc->find("log")) {
+      x = {n->k[1], sc};
+      return true;
+    }
+    return false;
+  }
+
+  Ty sub(const Arg& a) { return expr(a.n, a.sc); }
+
+  Ty bin_int(const NodeP& n, ScopeP sc, uint32_t op) {
+    Ty a = concrete(expr(n->k[0], sc), n), b = concrete(expr(n->k[1], sc), n);
+    if (a != T_INT || b != T_INT) fail(n, "arithmetic on " + std::string(ty_name(a)) + " and " + ty_name(b));
+    emit(op);
+    return T_INT;
+  }
+  Ty compare(const NodeP& n, ScopeP sc, const std::string& op) {
+    // a symbolic operand takes its code from the other side's type
+    const size_t mark = code.size();
+    Ty a = expr(n->k[0], sc);
+    Ty b;
+    if (is_sym(a)) {
+      code.resize(mark);
+      b = concrete(expr(n->k[1], sc), n);
+      emit(G_CONST, sym_code(a, b, n));
+      if (op == "<" || op == ">" || op == "<=" || op == ">=") fail(n, "order comparison with a symbolic constant");
+      a = b;
+    } else {
+      b = expr(n->k[1], sc);
+      if (is_sym(b)) {
+        emit(G_CONST, sym_code(b, a, n));
+        b = a;
+      }
+    }
+    a = concrete(a, n);
+    b = concrete(b, n);
+    if (a != b && !(a == T_INT && b == T_INT)) fail(n, std::string("comparison of ") + ty_name(a) + " and " + ty_name(b));
+    if ((op == "<" || op == ">" || op == "<=" || op == ">=") && a != T_INT) fail(n, "order comparison of non-integers");
+    if (op == "=") emit(G_EQ);
+    else if (op == "/=" || op == "#") emit(G_NE);
+    else if (op == "<") emit(G_LT);
+    else if (op == "<=" || op == "=<" || op == "\\leq") emit(G_LE);
+    else if (op == ">") { emit(G_LE); emit(G_NOT); }
+    else if (op == ">=" || op == "\\geq") { emit(G_LT); emit(G_NOT); }
+    return T_BOOL;
+  }
+
+  // x \in S: filters and SUBSET are rewritten (e \in {y \in S : P} is e \in S /\ P[y := e])
+  Ty member(const NodeP& n, const NodeP& e, const NodeP& set, ScopeP sc, ScopeP esc) {
+    NodeP S = set;
+    ScopeP ssc = sc;
+    // unfold names of the module / parameters until the set's own form shows
+    for (int guard = 0; guard < 16; guard++) {
+      if (S->kind == N_ID) {
+        if (const Arg* a = param(S->s)) { S = a->n; ssc = a->sc; continue; }
+        if (!ssc->find(S->s) && S->s != "Server" && S->s != "Value") {
+          const Def* d = m.find(S->s);
+          if (d && d->params.empty() && !d->error.empty()) fail(n, "definition " + S->s + " does not parse");
+          if (d && d->params.empty()) { S = d->body; ssc = std::make_shared<Scope>(); continue; }
+        }
+      }
+      break;
+    }
+    if (S->kind == N_SETFILTER && S->bounds.size() == 1 && S->bounds[0].vars.size() == 1) {
+      // e \in S' /\ P[y := e]
+      NodeP inner = S->bounds[0].set;
+      Ty t = member(n, e, inner, ssc, esc);
+      (void)t;
+      const size_t j = jump(G_JZ);
+      params.push_back({S->bounds[0].vars[0], Arg{e, esc}});
+      Ty p = concrete(expr(S->k[0], ssc), n);
+      params.pop_back();
+      if (p != T_BOOL) fail(n, "set filter predicate is not a boolean");
+      const size_t k = jump(G_JMP);
+      patch(j);
+      emit(G_CONST, 0);
+      patch(k);
+      return T_BOOL;
+    }
+    if (S->kind == N_UNARY && S->s == "SUBSET") {  // e \subseteq S
+      Ty a = concrete(expr(e, esc), n);
+      Ty b = concrete(expr(S->k[0], ssc), n);
+      if (a != b || (a != T_SET_SRV && a != T_SET_VAL && a != T_SET_STATE)) fail(n, "SUBSET membership of mismatched sets");
+      emit(G_SUBSETEQ);
+      return T_BOOL;
+    }
+    Ty a = concrete(expr(e, esc), n);
+    Ty b = concrete(expr(S, ssc), n);
+    if (elem_of(b, n) != a) fail(n, std::string(ty_name(a)) + " \\in " + ty_name(b));
+    emit(G_BIT);
+    return T_BOOL;
+  }
+
+  Ty junction(const std::vector<NodeP>& items, ScopeP sc, bool conj, const NodeP& n) {
+    // /\: the first false item ends it with 0; \/: the first true one with 1 (TLC's short circuit)
+    std::vector<size_t> exits;
+    for (size_t q = 0; q < items.size(); q++) {
+      Ty t = concrete(expr(items[q], sc), n);
+      if (t != T_BOOL) fail(items[q], std::string("junction item is ") + ty_name(t));
+      if (q + 1 < items.size()) exits.push_back(jump(conj ? G_JZ : G_JNZ));
+    }
+    if (exits.empty()) return T_BOOL;
+    const size_t done = jump(G_JMP);
+    for (size_t x : exits) patch(x);
+    emit(G_CONST, conj ? 0 : 1);
+    patch(done);
+    return T_BOOL;
+  }
+  void flatten(const NodeP& n, const std::string& op, std::vector<NodeP>& out) {
+    if ((n->kind == N_JUNCT || n->kind == N_BIN) && n->s == op) {
+      for (auto& c : n->k) flatten(c, op, out);
+    } else {
+      out.push_back(n);
+    }
+  }
+
+  // the elements of a constant set (for unrolled quantifiers)
+  std::vector<int> const_set(const NodeP& S, ScopeP sc, Ty& elem) {
+    if (S->kind == N_ID && !sc->find(S->s) && !param(S->s)) {
+      if (S->s == "Server") { elem = T_SRV; std::vector<int> v; for (int x = 0; x < env.N; x++) v.push_back(x); return v; }
+      if (S->s == "Value") { elem = T_VAL; std::vector<int> v; for (int x = 0; x < env.V; x++) v.push_back(x); return v; }
+    }
+    fail(S, "quantifier over a set other than Server or Value");
+  }
+
+  Ty quant(const NodeP& n, ScopeP sc) {
+    const bool ex = n->s == "\\E";
+    std::vector<std::pair<std::string, std::vector<int>>> vars;
+    std::vector<Ty> tys;
+    for (auto& b : n->bounds) {
+      if (!b.set) fail(n, "unbounded quantifier");
+      Ty et;
+      std::vector<int> els = const_set(b.set, sc, et);
+      for (auto& v : b.vars) { vars.push_back({v, els}); tys.push_back(et); }
+    }
+    // all combinations, first variable fastest
+    std::vector<size_t> idx(vars.size(), 0);
+    std::vector<size_t> exits;
+    bool any = false;
+    for (;;) {
+      for (size_t q = 0; q < vars.size(); q++)
+        if (vars[q].second.empty()) goto done;
+      {
+        auto s2 = std::make_shared<Scope>();
+        s2->up = sc;
+        for (size_t q = 0; q < vars.size(); q++) {
+          Binding b;
+          b.k = Binding::CONSTV;
+          b.v = vars[q].second[idx[q]];
+          b.ty = tys[q];
+          s2->names[vars[q].first] = b;
+        }
+        Ty t = concrete(expr(n->k[0], s2), n);
+        if (t != T_BOOL) fail(n, "quantified body is not a boolean");
+        exits.push_back(jump(ex ? G_JNZ : G_JZ));  // \E: a true instance decides; \A: a false one
+        any = true;
+      }
+      {
+        size_t q = 0;
+        while (q < vars.size() && ++idx[q] == vars[q].second.size()) idx[q++] = 0;
+        if (q == vars.size()) break;
+      }
+    }
+  done:
+    emit(G_CONST, ex ? 0 : 1);
+    const size_t end = jump(G_JMP);
+    for (size_t x : exits) patch(x);
+    emit(G_CONST, ex ? 1 : 0);
+    patch(end);
+    (void)any;
+    return T_BOOL;
+  }
+
+  Ty expr(const NodeP& n, ScopeP sc) {
+    if (++depth > 200) fail(n, "expression nested too deeply (a recursive operator?)");
+    struct D { int& d; ~D() { d--; } } dd{depth};
+    switch (n->kind) {
+      case N_NUM: emit(G_CONST, std::stoi(n->s)); return T_INT;
+      case N_ID: {
+        const std::string& s = n->s;
+        if (const Binding* b = sc->find(s)) {
+          if (b->k == Binding::ARG) { emit(G_ARG, b->v); return b->ty; }
+          if (b->k == Binding::CONSTV) { emit(G_CONST, b->v); return b->ty; }
+          return inline_def(n, b->def, {}, sc);
+        }
+        if (const Arg* a = param(s)) {
+          // evaluate the argument in its own scope, without the parameters bound after it
+          std::vector<std::pair<std::string, Arg>> save = params;
+          while (!params.empty() && &params.back().second != a) params.pop_back();
+          params.pop_back();
+          Ty t = sub(*a);
+          params = save;
+          return t;
+        }
+        if (s == "TRUE") return T_TRUE;
+        if (s == "FALSE") return T_FALSE;
+        if (s == "Nil") return T_NIL;
+        if (s == "Follower") { emit(G_CONST, FOLLOWER); return T_STATE; }
+        if (s == "Candidate") { emit(G_CONST, CANDIDATE); return T_STATE; }
+        if (s == "Leader") { emit(G_CONST, LEADER); return T_STATE; }
+        if (s == "Server") { emit(G_CONST, (1 << env.N) - 1); return T_SET_SRV; }
+        if (s == "Value") { emit(G_CONST, (1 << env.V) - 1); return T_SET_VAL; }
+        if (s == "electionCtr") { emit(G_ECTR); return T_INT; }
+        if (s == "restartCtr") { emit(G_RCTR); return T_INT; }
+        for (size_t q = 0; q < env.servers.size(); q++)
+          if (env.servers[q] == s) { emit(G_CONST, (int)q); return T_SRV; }
+        for (size_t q = 0; q < env.values.size(); q++)
+          if (env.values[q] == s) { emit(G_CONST, (int)q); return T_VAL; }
+        auto ci = env.ints.find(s);
+        if (ci != env.ints.end()) { emit(G_CONST, (int)ci->second); return T_INT; }
+        if (const Def* d = m.find(s)) return inline_def(n, d, {}, sc);
+        fail(n, "'" + s + "' is not a state variable, constant or operator the guard compiler knows");
+      }
+      case N_APP: {
+        const std::string& s = n->s;
+        if (const Binding* b = sc->find(s))
+          if (b->k == Binding::MACRO) return inline_def(n, b->def, n->k, sc);
+        if (!m.find(s) || sc->find(s)) {
+          if (s == "Len" && n->k.size() == 1) {
+            Arg x;
+            if (!log_of(n->k[0], sc, x)) fail(n, "Len of something other than log[x]");
+            if (sub(x) != T_SRV) fail(n, "log indexed by a non-server");
+            emit(G_LEN);
+            return T_INT;
+          }
+          if (s == "Cardinality" && n->k.size() == 1) {
+            Ty t = concrete(expr(n->k[0], sc), n);
+            if (t != T_SET_SRV && t != T_SET_VAL && t != T_SET_STATE) fail(n, "Cardinality of a non-set");
+            emit(G_POPC);
+            return T_INT;
+          }
+          fail(n, "operator '" + s + "' is not one the guard compiler knows");
+        }
+        return inline_def(n, m.find(s), n->k, sc);
+      }
+      case N_FAPP: {
+        if (n->k.size() != 2) fail(n, "function application with several arguments");
+        const NodeP& f = n->k[0];
+        if (f->kind == N_ID && !sc->find(f->s) && !param(f->s)) {
+          uint32_t op;
+          Ty ty;
+          if (server_var(f->s, op, ty)) {
+            if (concrete(expr(n->k[1], sc), n) != T_SRV) fail(n, f->s + " indexed by a non-server");
+            emit(op);
+            return ty;
+          }
+          if (f->s == "acked") {
+            if (concrete(expr(n->k[1], sc), n) != T_VAL) fail(n, "acked indexed by a non-value");
+            emit(G_ACKED);
+            return T_ACK;
+          }
+        }
+        if (f->kind == N_FAPP && f->k.size() == 2 && f->k[0]->kind == N_ID && !sc->find(f->k[0]->s)) {
+          uint32_t op;
+          Ty ty;
+          if (pair_var(f->k[0]->s, op, ty)) {
+            if (concrete(expr(f->k[1], sc), n) != T_SRV || concrete(expr(n->k[1], sc), n) != T_SRV)
+              fail(n, f->k[0]->s + " indexed by a non-server");
+            emit(op);
+            return ty;
+          }
+        }
+        fail(n, "this function application (only the state variables' own indexing is compiled)");
+      }
+      case N_FIELD: {  // log[x][k].term / .value
+        const NodeP& e = n->k[0];
+        if (e->kind == N_FAPP && e->k.size() == 2 && (n->s == "term" || n->s == "value")) {
+          Arg x;
+          if (log_of(e->k[0], sc, x)) {
+            if (sub(x) != T_SRV) fail(n, "log indexed by a non-server");
+            if (concrete(expr(e->k[1], sc), n) != T_INT) fail(n, "log index is not an integer");
+            emit(n->s == "term" ? G_LOGTERM : G_LOGVAL);
+            return n->s == "term" ? T_INT : T_VAL;
+          }
+        }
+        fail(n, "field access other than log[x][k].term / .value");
+      }
+      case N_UNARY: {
+        if (n->s == "~" || n->s == "\\lnot" || n->s == "\\neg") {
+          if (concrete(expr(n->k[0], sc), n) != T_BOOL) fail(n, "~ of a non-boolean");
+          emit(G_NOT);
+          return T_BOOL;
+        }
+        if (n->s == "-") {
+          if (concrete(expr(n->k[0], sc), n) != T_INT) fail(n, "- of a non-integer");
+          emit(G_NEG);
+          return T_INT;
+        }
+        fail(n, "unary " + n->s);
+      }
+      case N_JUNCT:
+      case N_BIN: {
+        const std::string& op = n->s;
+        if (op == "/\\" || op == "\\/" || op == "\\land" || op == "\\lor") {
+          const bool conj = op == "/\\" || op == "\\land";
+          std::vector<NodeP> items;
+          flatten(n, op, items);
+          return junction(items, sc, conj, n);
+        }
+        if (op == "=>") {  // ~a \/ b
+          if (concrete(expr(n->k[0], sc), n) != T_BOOL) fail(n, "=> of a non-boolean");
+          const size_t j = jump(G_JZ);
+          if (concrete(expr(n->k[1], sc), n) != T_BOOL) fail(n, "=> of a non-boolean");
+          const size_t e = jump(G_JMP);
+          patch(j);
+          emit(G_CONST, 1);
+          patch(e);
+          return T_BOOL;
+        }
+        if (op == "+") return bin_int(n, sc, G_ADD);
+        if (op == "-") return bin_int(n, sc, G_SUB);
+        if (op == "*") return bin_int(n, sc, G_MUL);
+        if (op == "=" || op == "/=" || op == "#" || op == "<" || op == ">" || op == "<=" || op == "=<" ||
+            op == ">=" || op == "\\leq" || op == "\\geq")
+          return compare(n, sc, op);
+        if (op == "\\in") return member(n, n->k[0], n->k[1], sc, sc);
+        if (op == "\\notin") {
+          member(n, n->k[0], n->k[1], sc, sc);
+          emit(G_NOT);
+          return T_BOOL;
+        }
+        if (op == "\\subseteq") {
+          Ty a = concrete(expr(n->k[0], sc), n), b = concrete(expr(n->k[1], sc), n);
+          if (a != b || (a != T_SET_SRV && a != T_SET_VAL && a != T_SET_STATE)) fail(n, "\\subseteq of mismatched sets");
+          emit(G_SUBSETEQ);
+          return T_BOOL;
+        }
+        if (op == "\\cup" || op == "\\union" || op == "\\cap" || op == "\\intersect" || op == "\\") {
+          Ty a = concrete(expr(n->k[0], sc), n), b = concrete(expr(n->k[1], sc), n);
+          if (a != b || (a != T_SET_SRV && a != T_SET_VAL && a != T_SET_STATE)) fail(n, op + " of mismatched sets");
+          emit(op == "\\cup" || op == "\\union" ? G_BOR : op == "\\" ? G_BDIFF : G_BAND);
+          return a;
+        }
+        fail(n, "operator " + op);
+      }
+      case N_SETENUM: {
+        emit(G_CONST, 0);
+        Ty et = T_SRV;
+        bool first = true;
+        for (auto& c : n->k) {
+          Ty t = concrete(expr(c, sc), n);
+          if (!first && t != et) fail(n, "set literal of mixed types");
+          et = t;
+          first = false;
+          emit(G_SETADD);
+        }
+        if (first) fail(n, "empty set literal (its type is not known)");
+        return set_of(et, n);
+      }
+      case N_IF: {
+        if (concrete(expr(n->k[0], sc), n) != T_BOOL) fail(n, "IF condition is not a boolean");
+        const size_t j = jump(G_JZ);
+        Ty a = concrete(expr(n->k[1], sc), n);
+        const size_t e = jump(G_JMP);
+        patch(j);
+        Ty b = concrete(expr(n->k[2], sc), n);
+        patch(e);
+        if (a != b) fail(n, "IF branches of different types");
+        return a;
+      }
+      case N_LET: {
+        auto s2 = std::make_shared<Scope>();
+        s2->up = sc;
+        for (auto& d : n->defs) {
+          Binding b;
+          b.k = Binding::MACRO;
+          b.def = &d;
+          s2->names[d.name] = b;
+        }
+        return expr(n->k[0], s2);
+      }
+      case N_QUANT: return quant(n, sc);
+      default: break;
+    }
+    fail(n, "this construct");
+  }
+
+  Ty inline_def(const NodeP& at, const Def* d, const std::vector<NodeP>& args, ScopeP sc) {
+    if (!d->error.empty()) fail(at, "definition " + d->name + " does not parse: " + d->error);
+    if (d->params.size() != args.size()) fail(at, "operator " + d->name + " applied to the wrong number of arguments");
+    const size_t base = params.size();
+    for (size_t q = 0; q < args.size(); q++) params.push_back({d->params[q], Arg{args[q], sc}});
+    // the body sees only its parameters (and the module), not the caller's bound names
+    auto s2 = std::make_shared<Scope>();
+    Ty t = expr(d->body, s2);
+    params.resize(base);
+    return t;
+  }
+};
+
+}  // namespace
+
+std::vector<uint32_t> compile_guard(const Module& m, const std::vector<std::string>& action_params,
+                                    const std::vector<int>& param_types, const std::vector<NodeP>& conjuncts,
+                                    const GuardEnv& env, const std::string& where) {
+  Compiler c(m, env);
+  c.where = where;
+  auto sc = std::make_shared<Scope>();
+  for (size_t q = 0; q < action_params.size(); q++) {
+    Binding b;
+    b.k = Binding::ARG;
+    b.v = (int)q;
+    b.ty = param_types[q] == 1 ? T_VAL : T_SRV;
+    sc->names[action_params[q]] = b;
+  }
+  if (conjuncts.empty()) {
+    c.emit(G_CONST, 1);
+  } else {
+    NodeP root = conjuncts[0];
+    Ty t = c.junction(conjuncts, sc, true, root);
+    if (t != T_BOOL) c.fail(root, "the guard is not a boolean");
+  }
+  c.emit(G_END);
+  return c.code;
+}
+
+}  // namespace tla
+}  // namespace rmc

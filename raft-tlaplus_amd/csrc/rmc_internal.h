@@ -16,6 +16,8 @@
 #include <thread>
 #include "../../include/rmc.h"
 #include "rmc_engine.h"
+#include "rmc_tla.h"
+#include <map>
 
 #define HIPCHK(x)                                                                   \
   do {                                                                              \
@@ -53,6 +55,10 @@ struct rmc_model {
   // first chunk of this level; (diag, ms) pairs of the last check
   unsigned profile_level = 0;
   std::vector<std::pair<int, double>> profile_ms;
+  // the cfg's integer constants (the guard compiler's environment) and the
+  // guards compiled onto library effects (rmc_guard.cpp)
+  std::map<std::string, long long> int_consts;
+  std::vector<rmc::tla::GuardSrc> guard_srcs;
   // the last check's row widenings (depth, first parent of the redone chunk, new message slots)
   std::vector<std::array<unsigned long long, 3>> widenings;
 };

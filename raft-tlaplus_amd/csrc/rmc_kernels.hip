@@ -194,9 +194,10 @@ template <int N>
 __device__ __forceinline__ MsgSums<N>& sums1(MsgSums<N>& m) { return m; }
 template <int N>
 __device__ __forceinline__ MsgSums<N>& sums1(MsgSums2<N>& m) { return m.m; }
-template <int SPEC, int N, int FPW>
+template <int SPEC, int N, int FPW, bool G = false>
 // waves per SIMD: as many as fit without scratch spills (N >= 4 and 128-bit
 // fingerprints need more registers; a spill costs a scratch store per binding)
+// G: the instantiation for models with compiled guards (rmc_guard.cpp)
 __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW == 2 ? 3 : 4) : FPW == 2 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                 unsigned long long pbase, unsigned long long floor, int sharded,
                                                 int shard_self,
@@ -326,7 +327,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       bool g = false;
       if (p < np) {
         PState<SPEC, N> s{sS + p * L.Wp};
-        g = may_enable<SPEC, N>(s, cM, b);
+        g = may_enable<SPEC, N, G>(s, cM, b);
       }
       const unsigned long long m = __ballot(g);
       if (p == 0) sMask[b] = m;
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           const int pp = select_bit64(sMask[lo], g - (int)sBOff[lo]);
           PState<SPEC, N> s{sS + pp * L.Wp};
           Delta d;
-          if (eval_fixed<SPEC, N>(s, cM, a, cM.fb_x[lo], d)) record(pp, lo, d);
+          if (eval_fixed<SPEC, N, G>(s, cM, a, cM.fb_x[lo], d)) record(pp, lo, d);
         }
       }
     }
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       const int b = sO2b[ord];
       PState<SPEC, N> s{sS + p * L.Wp};
       Delta d;
-      eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
+      eval_known<SPEC, N, G>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
       if constexpr (FPW == 2) {
         if (!d.err) acc ^= delta_fp_sums2<SPEC, N>(s, cM, d, sMS[p]).b;
       } else {
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           const int b = sO2b[ord];
           PState<SPEC, N> s{sS + p * L.Wp};
           Delta d;
-          eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
+          eval_known<SPEC, N, G>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
           obw = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : 0u);
           if (diag == 2) fp = (unsigned long long)d.hdr ^ d.w[0] ^ d.opc[0];  // the delta only
           else if (!d.err) {
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     const int b = sO2b[ord];
     PState<SPEC, N> s{sS + p * L.Wp};
     Delta d;
-    eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
+    eval_known<SPEC, N, G>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
     const unsigned long long t = gbase + (unsigned long long)idx;
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = CAND_DUP;
@@ -824,7 +825,7 @@ constexpr int MAT_LIST = RMC_MAT_LIST;
 #endif
 constexpr int MAT_T = RMC_MAT_THREADS;
 static_assert(MAT_T % 64 == 0 && MAT_T >= 64, "one thread per tile parent");
-template <int SPEC, int N>
+template <int SPEC, int N, bool G = false>
 __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                      unsigned long long pbase, const uint32_t* __restrict__ cand_ob,
                                                      const uint16_t* __restrict__ cand_win,
@@ -903,7 +904,7 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
       const int rank = (int)(sList[e] >> 16);
       PState<SPEC, N> s{sS + p * Wp};
       Delta d;
-      eval_known<SPEC, N>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, (int)(ob >> 16), d);
+      eval_known<SPEC, N, G>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, (int)(ob >> 16), d);
       const unsigned long long dst = (unsigned long long)sPos[p] + rank;
       uint32_t* o;
       unsigned long long* tp;
@@ -1221,17 +1222,23 @@ int host_fp_owner(unsigned long long fp, int W) { return fp_owner(fp, W); }
 struct Launch {
   template <int SPEC, int N>
   static void expand(const LevelArgs& a, hipStream_t s) {
+    if constexpr (SPEC != KRAFT) {
+      if (a.model->gany) {  // compiled guards: 64-bit fingerprints only (rmc_engine.cpp checks)
+        if (a.model->fpw == 2) throw std::runtime_error("compiled guards need 64-bit fingerprints");
+        return expand_w<SPEC, N, 1, true>(a, s);
+      }
+    }
     if (a.model->fpw == 2) return expand_w<SPEC, N, 2>(a, s);
     return expand_w<SPEC, N, 1>(a, s);
   }
-  template <int SPEC, int N, int FPW>
+  template <int SPEC, int N, int FPW, bool G = false>
   static void expand_w(const LevelArgs& a, hipStream_t s) {
     constexpr int PB = Tile<N>::PB;
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
     ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T), M.nfixed,
                              M.ordinal_limit);
-    hipLaunchKernelGGL((k_expand<SPEC, N, FPW>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
+    hipLaunchKernelGGL((k_expand<SPEC, N, FPW, G>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.floor, a.sharded, a.shard_self, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val
 #ifdef RMC_DIAG
@@ -1244,6 +1251,14 @@ struct Launch {
     constexpr int PB = Tile<N>::PB;  // must be k_expand's tile: a tile's candidates are contiguous only within one expand tile
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     size_t lds_bytes = (size_t)PB * (a.model->words | 1) * 4;
+    if constexpr (SPEC != KRAFT) {
+      if (a.model->gany) {
+        hipLaunchKernelGGL((k_materialize<SPEC, N, true>), dim3((unsigned)blocks), dim3(MAT_T), lds_bytes, s, a.frontier,
+                           a.nparents, a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out,
+                           a.out_base_global, a.tr_parent, a.tr_bind, a.pieces, a.npieces, a.st);
+        return;
+      }
+    }
     hipLaunchKernelGGL((k_materialize<SPEC, N>), dim3((unsigned)blocks), dim3(MAT_T), lds_bytes, s, a.frontier, a.nparents,
                        a.pbase, a.cand_ob, a.cand_win, a.par_off, a.par_n, a.par_pos, a.out, a.out_base_global,
                        a.tr_parent, a.tr_bind, a.pieces, a.npieces, a.st);
@@ -1548,14 +1563,14 @@ __global__ __launch_bounds__(SIM_BLOCK) void k_simulate(const uint32_t* __restri
     int cnt = 0;
     for (int b = 0; b < B; b++) {
       Delta d;
-      if (eval_binding<SPEC, N>(s, cM, b, d)) cnt++;
+      if (eval_binding<SPEC, N, SPEC != KRAFT>(s, cM, b, d)) cnt++;
     }
     if (!cnt) break;  // no successor: the behaviour ends (-deadlock)
     int r = (int)(splitmix(rng) % (unsigned long long)cnt);
     Delta d;
     int b = 0;
     for (; b < B; b++)
-      if (eval_binding<SPEC, N>(s, cM, b, d) && r-- == 0) break;
+      if (eval_binding<SPEC, N, SPEC != KRAFT>(s, cM, b, d) && r-- == 0) break;
     binds[w * depth + steps] = (uint16_t)b;
     if (d.err) {  // an evaluation error in Next (TLC stops with an error)
       atomicMin(&ss->key, (w << 20) | ((unsigned long long)(steps + 1) << 2) | 2ULL);

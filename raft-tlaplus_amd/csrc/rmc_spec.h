@@ -43,6 +43,15 @@
 #else
 #define RMC_HD static inline
 #endif
+// Compiled guards (guard_vm) are evaluated only in code instantiated for them:
+// the device kernels take them as a template flag, launched with it only for a
+// model that has one (inlining the machine into every kernel costs the library
+// actions registers and spills); host code always has it.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RMC_G_DEFAULT false
+#else
+#define RMC_G_DEFAULT true
+#endif
 
 namespace rmc {
 
@@ -83,6 +92,7 @@ enum ErrCode {
 };
 constexpr int NILS = 7;
 constexpr int MAXN = 7, MAXV = 4, MAXLOG = 5, MAXOPS = 7, MAXPERM = 120, MAXACT = 16, MAXFIXED = 192;
+constexpr int MAXGCODE = 512;  // words of compiled guard code (Model::gcode)
 
 struct Model {
   int spec, N, V, E, R, EQ, RQ, lfae, lfiq, ffbr;
@@ -105,6 +115,13 @@ struct Model {
   int fpw;                    // fingerprint width in 64-bit words (1: 64-bit, 2: 128-bit)
   int bind_words, ord_words;  // u32 words of a per-parent bitmask over bindings / over ordinals
   uint16_t ord2b[1024];       // TLC ordinal -> binding (fixed bindings; message actions: nfixed + DOMAIN index)
+  // Compiled guards (the TLA+ front end, rmc_tla.cpp compile_guard): an action
+  // whose module text keeps the library action's effect but states its own
+  // guard runs the library effect unguarded, behind this program.  gstart[a]
+  // = first word of action id a's program in gcode, -1 = the library guard.
+  int16_t gstart[A_NUM];
+  int gany;  // some action has a compiled guard
+  uint32_t gcode[MAXGCODE];
 };
 
 // ------------------------------------------------------------- bit helpers
@@ -946,10 +963,126 @@ RMC_HD bool kr_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& d
 // Each returns true iff the action is enabled for the binding; d receives the
 // successor.  Citations are to /root/reference/specifications/.
 
+// ------------------------------------------------------- compiled guards
+// A stack machine over the packed state for the guards the TLA+ front end
+// compiles (rmc_tla.cpp compile_guard): one 32-bit word per instruction, op in
+// the low 8 bits, a signed 24-bit operand above.  Values are ints: booleans
+// 0/1, sets of servers / values / states as bitmasks, Nil and the record
+// values in the packed state's own codes (the compiler types every operand).
+// Jumps are relative to the next instruction (short-circuit /\ and \/, IF).
+// Returns 1 (enabled), 0, or -1: a TLC evaluation error (a sequence indexed
+// outside its domain).  Only models with a compiled guard reach it.
+enum GOp : uint32_t {
+  G_END = 0,   // return the top of the stack
+  G_CONST,     // push imm
+  G_ARG,       // push bound variable imm (0: i, 1: j or v)
+  G_ST,        // x -> state[x]
+  G_TERM,      // x -> currentTerm[x]
+  G_VOTED,     // x -> votedFor[x] (Pull: leader[x]); Nil = 7
+  G_VOTED2,    // x -> PullRaftVariant2 votedFor[x]
+  G_LEN,       // x -> Len(log[x])
+  G_COMMIT,    // x -> commitIndex[x]
+  G_FSYNC,     // x -> fsyncIndex[x]
+  G_VOTES,     // x -> votesGranted[x] (server bitmask)
+  G_NEXT,      // x y -> nextIndex[x][y]
+  G_MATCH,     // x y -> matchIndex[x][y]
+  G_PEND,      // x y -> pendingResponse[x][y]
+  G_LOGTERM,   // x k -> log[x][k].term   (error outside 1..Len)
+  G_LOGVAL,    // x k -> log[x][k].value  (error outside 1..Len)
+  G_ECTR,      // -> electionCtr
+  G_RCTR,      // -> restartCtr
+  G_ACKED,     // v -> acked[v] (0 Nil, 1 FALSE, 2 TRUE)
+  G_ADD, G_SUB, G_MUL, G_NEG,
+  G_EQ, G_NE, G_LT, G_LE, G_NOT,
+  G_BIT,       // x S -> (S >> x) & 1   (x \in S)
+  G_SETADD,    // S x -> S | 1 << x
+  G_POPC,      // S -> Cardinality(S)
+  G_SUBSETEQ,  // A B -> (A & ~B) == 0
+  G_BOR, G_BAND, G_BDIFF,  // A B -> A | B, A & B, A & ~B (set union, intersection, difference)
+  G_JZ,        // pop; jump imm if 0
+  G_JNZ,       // pop; jump imm if not 0
+  G_JMP,       // jump imm
+  G_POP,
+  G_ERR,       // evaluation error
+  G_NUM
+};
+RMC_HD uint32_t g_ins(uint32_t op, int imm = 0) { return op | ((uint32_t)imm << 8); }
+// The stack lives in eight registers, shifted on push and pop (a dynamically
+// indexed array would put it in scratch memory, and a real call would make
+// every kernel that can reach it save its live registers around it: the
+// kernels' register budgets are set for the library actions).  The compiler
+// refuses a guard deeper than that (rmc_guard.cpp).
 template <int SPEC, int N>
-RMC_HD bool act_restart(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {
+RMC_HD int guard_vm(const uint32_t* S, const Model& M, int pc, int i, int jv) {
+  int t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0, t6 = 0, t7 = 0;
+  const PState<SPEC, N> s{S};
+#define GPUSH(x) do { const int x_ = (x); t7 = t6; t6 = t5; t5 = t4; t4 = t3; t3 = t2; t2 = t1; t1 = t0; t0 = x_; } while (0)
+#define GPOP() do { t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = t5; t5 = t6; t6 = t7; } while (0)
+#define GBIN(e) do { const int a_ = t1, b_ = t0; GPOP(); t0 = (e); } while (0)
+  for (int steps = 0; steps < MAXGCODE; steps++) {
+    const uint32_t w = M.gcode[pc++];
+    const int op = (int)(w & 0xFFu), imm = (int)w >> 8;
+    switch (op) {
+      case G_END: return t0 ? 1 : 0;
+      case G_CONST: GPUSH(imm); break;
+      case G_ARG: GPUSH(imm ? jv : i); break;
+      case G_ST: t0 = s.st(t0 & 7); break;
+      case G_TERM: t0 = s.term(t0 & 7); break;
+      case G_VOTED: t0 = a_voted(s.A(t0 & 7)); break;
+      case G_VOTED2: t0 = a_votedfor2(s.A(t0 & 7)); break;
+      case G_LEN: t0 = s.len(t0 & 7); break;
+      case G_COMMIT: t0 = a_commit(s.A(t0 & 7)); break;
+      case G_FSYNC: t0 = a_fsync(s.A(t0 & 7)); break;
+      case G_VOTES: t0 = a_votes(s.A(t0 & 7)); break;
+      case G_NEXT: GBIN(row_get(s.Cw(a_ & 7), b_ & 7)); break;
+      case G_MATCH: GBIN(row_get(s.Dw(a_ & 7), b_ & 7)); break;
+      case G_PEND: GBIN((a_pending(s.A(a_ & 7)) >> (b_ & 7)) & 1); break;
+      case G_LOGTERM:
+      case G_LOGVAL: {
+        const int x = t1 & 7, k = t0;
+        const uint32_t a = s.A(x), b = s.B(x);
+        if (k < 1 || k > a_len(a)) return -1;
+        GPOP();
+        t0 = op == G_LOGTERM ? e_term(b, k - 1) : e_value(b, k - 1);
+        break;
+      }
+      case G_ECTR: GPUSH(h_ectr(s.hdr())); break;
+      case G_RCTR: GPUSH(h_rctr(s.hdr())); break;
+      case G_ACKED: t0 = h_acked(s.hdr(), t0 & 3); break;
+      case G_ADD: GBIN(a_ + b_); break;
+      case G_SUB: GBIN(a_ - b_); break;
+      case G_MUL: GBIN(a_ * b_); break;
+      case G_NEG: t0 = -t0; break;
+      case G_EQ: GBIN(a_ == b_); break;
+      case G_NE: GBIN(a_ != b_); break;
+      case G_LT: GBIN(a_ < b_); break;
+      case G_LE: GBIN(a_ <= b_); break;
+      case G_NOT: t0 = !t0; break;
+      case G_BIT: GBIN((b_ >> (a_ & 31)) & 1); break;
+      case G_SETADD: GBIN(a_ | (1 << (b_ & 31))); break;
+      case G_POPC: t0 = popc7((uint32_t)t0); break;
+      case G_SUBSETEQ: GBIN((a_ & ~b_) == 0); break;
+      case G_BOR: GBIN(a_ | b_); break;
+      case G_BAND: GBIN(a_ & b_); break;
+      case G_BDIFF: GBIN(a_ & ~b_); break;
+      case G_JZ: { const int c_ = t0; GPOP(); if (!c_) pc += imm; break; }
+      case G_JNZ: { const int c_ = t0; GPOP(); if (c_) pc += imm; break; }
+      case G_JMP: pc += imm; break;
+      case G_POP: GPOP(); break;
+      default: return -1;  // G_ERR
+    }
+  }
+#undef GPUSH
+#undef GPOP
+#undef GBIN
+  return -1;
+}
+
+template <int SPEC, int N>
+RMC_HD bool act_restart(const PState<SPEC, N>& s, const Model& M, int i, Delta& d, bool ug = false) {
   // Raft.tla:226-235; FlexibleRaft.tla:200-208; RaftFsync.tla:203-218; PullRaft.tla:258-265
-  if (!(h_rctr(s.hdr()) < M.R)) return false;
+  // (ug: a compiled guard stands in for the reference's, guard_vm)
+  if (!ug && !(h_rctr(s.hdr()) < M.R)) return false;
   begin_srv(s, d, i);
   uint32_t a = d.w[0];
   a = setb(a, 4, 2, FOLLOWER);
@@ -975,12 +1108,12 @@ RMC_HD bool act_restart(const PState<SPEC, N>& s, const Model& M, int i, Delta& 
 }
 
 template <int SPEC, int N>
-RMC_HD bool act_requestvote(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {
+RMC_HD bool act_requestvote(const PState<SPEC, N>& s, const Model& M, int i, Delta& d, bool ug = false) {
   // Raft.tla:242-257 (FlexibleRaft.tla:215-230; PullRaft.tla:283-298 sets leader[i])
   int ec = h_ectr(s.hdr());
-  if (!(ec < M.E)) return false;
   int st = s.st(i);
-  if (!(st == FOLLOWER || st == CANDIDATE)) return false;
+  if (!ug && !(ec < M.E && (st == FOLLOWER || st == CANDIDATE))) return false;
+  if (ec + 1 > 15) { d.err = E_CAP_FIELD; return true; }
   int t1 = s.term(i) + 1;
   if (t1 > 15) { d.err = E_CAP_TERM; return true; }
   uint32_t a = s.A(i), b = s.B(i);
@@ -1007,11 +1140,11 @@ RMC_HD bool act_requestvote(const PState<SPEC, N>& s, const Model& M, int i, Del
 }
 
 template <int SPEC, int N>
-RMC_HD bool act_timeout(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {  // RaftFsync.tla:222-230
+RMC_HD bool act_timeout(const PState<SPEC, N>& s, const Model& M, int i, Delta& d, bool ug = false) {  // RaftFsync.tla:222-230
   int ec = h_ectr(s.hdr());
-  if (!(ec < M.E)) return false;
   int st = s.st(i);
-  if (!(st == FOLLOWER || st == CANDIDATE)) return false;
+  if (!ug && !(ec < M.E && (st == FOLLOWER || st == CANDIDATE))) return false;
+  if (ec + 1 > 15) { d.err = E_CAP_FIELD; return true; }
   int t1 = s.term(i) + 1;
   if (t1 > 15) { d.err = E_CAP_TERM; return true; }
   begin_srv(s, d, i);
@@ -1026,8 +1159,8 @@ RMC_HD bool act_timeout(const PState<SPEC, N>& s, const Model& M, int i, Delta& 
 }
 
 template <int SPEC, int N>
-RMC_HD bool act_rvij(const PState<SPEC, N>& s, const Model& M, int i, int j, Delta& d) {  // RaftFsync.tla:234-243
-  if (s.st(i) != CANDIDATE || i == j) return false;
+RMC_HD bool act_rvij(const PState<SPEC, N>& s, const Model& M, int i, int j, Delta& d, bool ug = false) {  // RaftFsync.tla:234-243
+  if (!ug && (s.st(i) != CANDIDATE || i == j)) return false;
   uint32_t a = s.A(i), b = s.B(i);
   MsgF m = msg_zero();
   m.type = RVREQ; m.term = a_term(a); m.llt = last_term(a, b); m.lli = a_len(a); m.src = i; m.dst = j; m.count = 1;
@@ -1069,13 +1202,13 @@ RMC_HD bool act_appendentries(const PState<SPEC, N>& s, const Model& M, int i, i
 }
 
 template <int SPEC, int N>
-RMC_HD bool act_becomeleader(const PState<SPEC, N>& s, const Model& M, int i, Delta& d) {
+RMC_HD bool act_becomeleader(const PState<SPEC, N>& s, const Model& M, int i, Delta& d, bool ug = false) {
   // Raft.tla:289-300; FlexibleRaft.tla:260-269; RaftFsync.tla:276-285; PullRaft.tla:354-366
-  if (s.st(i) != CANDIDATE) return false;
+  if (!ug && s.st(i) != CANDIDATE) return false;
   uint32_t a = s.A(i);
   int vg = a_votes(a);
   bool q = SPEC == FLEX ? popc7((uint32_t)vg) >= M.EQ : popc7((uint32_t)vg) * 2 > N;
-  if (!q) return false;
+  if (!ug && !q) return false;
   if (SPEC == PULL) {
     MsgF m = msg_zero();
     m.type = LNREQ; m.term = a_term(a); m.src = i; m.count = 1;
@@ -1115,8 +1248,8 @@ RMC_HD bool act_becomeleader(const PState<SPEC, N>& s, const Model& M, int i, De
 }
 
 template <int SPEC, int N>
-RMC_HD bool act_client(const PState<SPEC, N>& s, const Model& M, int i, int v, Delta& d) {  // Raft.tla:304-313
-  if (s.st(i) != LEADER || h_acked(s.hdr(), v) != 0) return false;
+RMC_HD bool act_client(const PState<SPEC, N>& s, const Model& M, int i, int v, Delta& d, bool ug = false) {  // Raft.tla:304-313
+  if (!ug && (s.st(i) != LEADER || h_acked(s.hdr(), v) != 0)) return false;
   begin_srv(s, d, i);
   log_append(d.w[0], d.w[1], s.term(i), v, d.err);
   d.hdr = setb(s.hdr(), 16 + 2 * v, 2, 1);  // acked[v] = FALSE
@@ -1380,7 +1513,7 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
 // A fixed binding given as (action id, its bound server i, its second bound
 // variable jv) with its TLC ordinal already known: no table lookups, so a lane
 // with its own binding issues no dependent loads before the action's guard.
-template <int SPEC, int N>
+template <int SPEC, int N, bool G = RMC_G_DEFAULT>
 RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int i, int jv, int ordinal, Delta& d) {
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   d.act = act;
@@ -1401,13 +1534,22 @@ RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int
     return true;
   }
   if (SPEC == KRAFT) return kr_fixed(s, M, act, i, jv, d);
+  bool ug = false;
+  if constexpr (G) {
+    if (M.gstart[act] >= 0) {  // a compiled guard (rmc_guard.cpp) instead of the library's
+      const int g = guard_vm<SPEC, N>(s.S, M, M.gstart[act], i, jv);
+      if (g < 0) { d.err = E_DOMAIN; return true; }
+      if (!g) return false;
+      ug = true;
+    }
+  }
   switch (act) {
-    case A_RESTART: return act_restart(s, M, i, d);
-    case A_REQUESTVOTE: return act_requestvote(s, M, i, d);
-    case A_TIMEOUT: return act_timeout(s, M, i, d);
-    case A_RVIJ: return act_rvij(s, M, i, jv, d);
-    case A_BECOMELEADER: return act_becomeleader(s, M, i, d);
-    case A_CLIENT: return act_client(s, M, i, jv, d);
+    case A_RESTART: return act_restart(s, M, i, d, ug);
+    case A_REQUESTVOTE: return act_requestvote(s, M, i, d, ug);
+    case A_TIMEOUT: return act_timeout(s, M, i, d, ug);
+    case A_RVIJ: return act_rvij(s, M, i, jv, d, ug);
+    case A_BECOMELEADER: return act_becomeleader(s, M, i, d, ug);
+    case A_CLIENT: return act_client(s, M, i, jv, d, ug);
     case A_ADVCOMMIT: return act_advcommit(s, M, i, d);
     case A_APPENDENTRIES: return act_appendentries(s, M, i, jv, d);
     case A_ADVFSYNC: return act_advfsync(s, M, i, d);
@@ -1417,17 +1559,18 @@ RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int
 }
 // A fixed binding: action slot `slot` (a K_I / K_IV / K_IJ action of Next)
 // with bound-variable index x (first bound variable fastest).
-template <int SPEC, int N>
+template <int SPEC, int N, bool G = RMC_G_DEFAULT>
 RMC_HD bool eval_fixed(const PState<SPEC, N>& s, const Model& M, int slot, int x, Delta& d) {
-  if (M.act_kind[slot] == K_M) return eval_fixed_id(s, M, M.act_id[slot], x & 15, x >> 4, M.act_off[slot] + x, d);
-  return eval_fixed_id(s, M, M.act_id[slot], x % N, x / N, M.act_off[slot] + x, d);
+  if (M.act_kind[slot] == K_M) return eval_fixed_id<SPEC, N, G>(s, M, M.act_id[slot], x & 15, x >> 4, M.act_off[slot] + x, d);
+  return eval_fixed_id<SPEC, N, G>(s, M, M.act_id[slot], x % N, x / N, M.act_off[slot] + x, d);
 }
 // Binding b whose TLC ordinal is known (k_expand phase C, k_materialize):
 // desc = M.fb_desc[b] for a fixed binding (staged in LDS by the kernels).
-template <int SPEC, int N>
+template <int SPEC, int N, bool G = RMC_G_DEFAULT>
 RMC_HD bool eval_known(const PState<SPEC, N>& s, const Model& M, int b, uint32_t desc, int ordinal, Delta& d) {
   if (b < M.nfixed)
-    return eval_fixed_id(s, M, (int)((desc >> 16) & 0xFFu), (int)((desc >> 24) & 15u), (int)(desc >> 28), ordinal, d);
+    return eval_fixed_id<SPEC, N, G>(s, M, (int)((desc >> 16) & 0xFFu), (int)((desc >> 24) & 15u), (int)(desc >> 28),
+                                     ordinal, d);
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   d.act = -1;
   const bool en = act_message(s, M, b - M.nfixed, d);
@@ -1436,9 +1579,9 @@ RMC_HD bool eval_known(const PState<SPEC, N>& s, const Model& M, int b, uint32_t
 }
 
 // Evaluate binding b (fixed bindings first, then one per DOMAIN element).
-template <int SPEC, int N>
+template <int SPEC, int N, bool G = RMC_G_DEFAULT>
 RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta& d) {
-  if (b < M.nfixed) return eval_fixed(s, M, M.fb_act[b], M.fb_x[b], d);
+  if (b < M.nfixed) return eval_fixed<SPEC, N, G>(s, M, M.fb_act[b], M.fb_x[b], d);
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   int k = b - M.nfixed;
   d.act = -1;
@@ -1452,7 +1595,7 @@ RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta&
 // one header field or one server's state word.  may_enable false implies
 // eval_binding returns false without an error, so k_expand evaluates only the
 // (parent, binding) pairs that pass it.
-template <int SPEC, int N>
+template <int SPEC, int N, bool G = RMC_G_DEFAULT>
 RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
   const uint32_t desc = M.fb_desc[b];
   const int i = (int)((desc >> 24) & 15u), jv = (int)(desc >> 28);
@@ -1462,6 +1605,9 @@ RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
       const int k = i | (jv << 4);
       return k < s.nmsg() && (act == A_DUP || msg_count(s.msg(k)) > 0);
     }
+  }
+  if constexpr (G) {
+    if (M.gstart[(desc >> 16) & 0xFFu] >= 0) return true;  // a compiled guard: no prefilter
   }
   const uint32_t a = s.A(i);
   const int st = a_st(a);

@@ -735,6 +735,82 @@ struct Hasher {
     }
     return h;
   }
+
+  // Does n change the state: a primed variable, UNCHANGED, or an operator of
+  // the module whose body does (Send, Reply, ...)?  Bound names shadow
+  // definitions.
+  std::map<std::string, bool> eff_memo;
+  bool has_effect(const NodeP& n, std::set<std::string>& bound) {
+    if (!n) return false;
+    if (n->kind == N_PRIME) return true;
+    if (n->kind == N_UNARY && n->s == "UNCHANGED") return true;
+    if ((n->kind == N_ID || n->kind == N_APP) && !bound.count(n->s)) {
+      const Def* d = m.find(n->s);
+      if (d && !is_declared(n->s)) {
+        auto it = eff_memo.find(n->s);
+        bool e;
+        if (it != eff_memo.end()) {
+          e = it->second;
+        } else {
+          eff_memo[n->s] = false;  // (recursion guard)
+          std::set<std::string> b2(d->params.begin(), d->params.end());
+          e = d->error.empty() ? has_effect(d->body, b2) : true;
+          eff_memo[n->s] = e;
+        }
+        if (e) return true;
+      }
+    }
+    std::vector<std::string> added;
+    auto bind = [&](const std::string& v) {
+      if (bound.insert(v).second) added.push_back(v);
+    };
+    for (auto& b : n->bounds) {
+      if (has_effect(b.set, bound)) return true;
+      for (auto& v : b.vars) bind(v);
+    }
+    bool e = false;
+    for (auto& d : n->defs) {
+      std::set<std::string> b2 = bound;
+      for (auto& p : d.params) b2.insert(p);
+      if (has_effect(d.body, b2)) e = true;
+      bind(d.name);
+    }
+    for (auto& c : n->k)
+      if (!e && has_effect(c, bound)) e = true;
+    for (auto& path : n->paths)
+      for (auto& st : path)
+        for (auto& a : st.args)
+          if (!e && has_effect(a, bound)) e = true;
+    for (auto& v : added) bound.erase(v);
+    return e;
+  }
+  // The top-level conjuncts of definition `name`: guards (no effect) and effects.
+  bool split(const std::string& name, std::vector<NodeP>& guards, std::vector<NodeP>& effects) {
+    const Def* d = m.find(name);
+    if (!d || !d->error.empty() || !d->body) return false;
+    std::vector<NodeP> items;
+    flatten(d->body, "/\\", items);
+    std::set<std::string> bound(d->params.begin(), d->params.end());
+    for (auto& c : items) (has_effect(c, bound) ? effects : guards).push_back(c);
+    return !effects.empty();
+  }
+  // Hash of an action's EFFECT: its effect conjuncts in order, parameters
+  // bound by position as in def_hash.  Two actions with equal effect hashes
+  // differ at most in their guards.
+  bool effect_hash(const std::string& name, uint64_t& out, std::vector<NodeP>* guards_out = nullptr) {
+    std::vector<NodeP> g, e;
+    if (!split(name, g, e)) return false;
+    const Def* d = m.find(name);
+    std::vector<Ent> save;
+    save.swap(env);
+    for (auto& p : d->params) env.push_back({p, false, 0, 0});
+    uint64_t h = hcomb(hstr("effect"), d->params.size());
+    for (auto& c : e) h = hcomb(h, node(c));
+    env.swap(save);
+    out = h;
+    if (guards_out) *guards_out = g;
+    return true;
+  }
 };
 
 }  // namespace
@@ -881,7 +957,7 @@ std::vector<Disjunct> next_disjuncts(const Module& m, const std::string& next) {
 
 // ------------------------------------------------------------------ lowering
 namespace {
-enum Role { R_INIT = 0, R_ACTION = 1, R_INV = 2, R_VIEW = 3, R_SYMM = 4, R_VARS = 5 };
+enum Role { R_INIT = 0, R_ACTION = 1, R_INV = 2, R_VIEW = 3, R_SYMM = 4, R_VARS = 5, R_EFFECT = 6 };
 struct Known {
   int spec, role, id, kind;
   unsigned long long hash;
@@ -914,6 +990,19 @@ std::string hash_report(const std::string& text) {
   for (auto& kv : closure_hashes(m)) {
     snprintf(b, sizeof b, "%016llx", (unsigned long long)kv.second);
     o += kv.first + " " + b + "\n";
+  }
+  {  // "effect:name hash": the effect hash of each action-shaped definition
+    Hasher H(m);
+    for (auto& d : m.defs) {
+      uint64_t h = 0;
+      try {
+        if (!H.effect_hash(d.name, h)) continue;
+      } catch (std::exception&) {
+        continue;
+      }
+      snprintf(b, sizeof b, "%016llx", (unsigned long long)h);
+      o += "effect:" + d.name + " " + b + "\n";
+    }
   }
   for (auto& d : m.defs)
     if (!d.error.empty()) o += "#unparsed " + d.name + " " + d.error + "\n";
@@ -955,7 +1044,8 @@ static const std::set<std::string> kStdOps = {
 
 Lowering lower(const std::string& text, const std::string& next, const std::string& view,
                const std::string& symmetry, const std::vector<std::string>& invariants) {
-  Module m = parse_module(text);
+  auto mp = std::make_shared<Module>(parse_module(text));
+  Module& m = *mp;
   for (const std::string& e : m.extends)
     if (!kStdModules.count(e))
       throw std::runtime_error("module " + m.name + " EXTENDS " + e + ": the lowering reads a module's own text and "
@@ -1000,13 +1090,35 @@ Lowering lower(const std::string& text, const std::string& next, const std::stri
         throw std::runtime_error("module " + m.name + " uses " + u + ", which it neither defines nor declares and no "
                                  "standard module the lowering knows defines");
   }
+  L.module = mp;
   for (const Disjunct& dj : djs) {
     const uint64_t h = hash_of(dj.op);
     const Known* k = find(R_ACTION, h);
+    if (!k) {
+      // the library's effect behind the module's own guard (rmc_guard.cpp)?
+      uint64_t eh = 0;
+      std::vector<NodeP> g;
+      if (H.effect_hash(dj.op, eh, &g)) k = find(R_EFFECT, eh);
+      if (k) {
+        for (const GuardSrc& q : L.guards)
+          if (q.act == k->id)
+            throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") and " + q.op +
+                                     " both guard the library's " + k->name + " effect: one guard per action");
+        GuardSrc gs;
+        gs.act = k->id;
+        gs.op = dj.op;
+        gs.params = m.find(dj.op)->params;
+        gs.conjuncts = g;
+        gs.mod = mp;
+        L.guards.push_back(gs);
+      }
+    }
     if (!k)
       throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") computes an action "
                                "the " + spec_name(L.spec) + " lowering does not have (its definition differs from "
-                               "every lowered action of the spec family); adding it needs a lowering in rmc_spec.h");
+                               "every lowered action of the spec family, and its effect -- the conjuncts that change "
+                               "the state -- from every effect whose guard the front end compiles); adding it needs a "
+                               "lowering in rmc_spec.h");
     static const int form_of_kind[] = {B_I, B_IV, B_IJ, B_MSG, B_M};
     if (form_of_kind[k->kind] != dj.form)
       throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) +
@@ -1032,6 +1144,29 @@ Lowering lower(const std::string& text, const std::string& next, const std::stri
     L.symmetry_ok = true;
   }
   return L;
+}
+
+GuardSrc parse_guard(int spec, int act, const std::string& op, const std::vector<std::string>& params,
+                     const std::string& expr) {
+  // the family's standard helpers, restated (Raft.tla:123 Quorum, :126 LastTerm)
+  std::string ps;
+  for (size_t q = 0; q < params.size(); q++) ps += (q ? ", " : "") + params[q];
+  const std::string text = "---- MODULE GuardText ----\n"
+                           "Quorum == {i \\in SUBSET(Server) : Cardinality(i) * 2 > Cardinality(Server)}\n"
+                           "LastTerm(xlog) == IF Len(xlog) = 0 THEN 0 ELSE xlog[Len(xlog)].term\n"
+                           "GuardOf" + op + (params.empty() ? "" : "(" + ps + ")") + " ==\n    " + expr + "\n====\n";
+  auto helpers = std::make_shared<Module>(parse_module(text));
+  const Def* d = helpers->find("GuardOf" + op);
+  if (!d) throw ParseError("guard text did not parse");
+  if (!d->error.empty()) throw ParseError("guard text: " + d->error);
+  (void)spec;
+  GuardSrc g;
+  g.act = act;
+  g.op = op;
+  g.params = params;
+  g.conjuncts = {d->body};
+  g.mod = helpers;
+  return g;
 }
 
 }  // namespace tla

@@ -60,19 +60,28 @@ INVARIANTS = {"LeaderHasAllAckedValues": 0, "NoLogDivergence": 1, "CommittedEntr
               "NeverTwoLeadersInSameEpoch": 3, "NoIllegalState": 4}
 
 
+# Actions whose guard the front end may replace (rmc_guard.cpp): their library
+# functions check exactly the reference's effect-free conjuncts and run the
+# rest unguarded when a compiled guard stands in (rmc_spec.h `ug`).
+GUARDED = {"Restart", "RequestVote", "Timeout", "BecomeLeader", "ClientRequest"}
+
+
 def hashes(lib, text):
     buf = ctypes.create_string_buffer(1 << 20)
     n = lib.rmc_tla_hashes(text.encode(), buf, len(buf))
     if n < 0:
         raise SystemExit(buf.value.decode())
-    out, vars_h = {}, None
+    out, vars_h, effects = {}, None, {}
     for line in buf.value.decode().splitlines():
         if line.startswith("#vars "):
             vars_h = line.split()[1]
+        elif line.startswith("effect:"):
+            name, h = line[len("effect:"):].split()
+            effects[name] = h
         elif not line.startswith("#"):
             name, h = line.split()
             out[name] = h
-    return out, vars_h
+    return out, vars_h, effects
 
 
 def main():
@@ -80,7 +89,7 @@ def main():
     rows = ["// Generated by tools/gen_tla_known.py from the reference modules (closure hashes only, no spec text).",
             "// {spec, role, id, binding form, closure hash, reference definition}"]
     for module, kind, rel in MODULES:
-        h, vh = hashes(lib, open(os.path.join(REF, rel)).read())
+        h, vh, eff = hashes(lib, open(os.path.join(REF, rel)).read())
         rows.append("// %s (specifications/%s)" % (module, rel))
         rows.append("{%s, R_VARS, 0, 0, 0x%sULL, \"VARIABLES\"}," % (kind, vh))
         rows.append("{%s, R_INIT, 0, 0, 0x%sULL, \"Init\"}," % (kind, h["Init"]))
@@ -93,6 +102,8 @@ def main():
                     continue
                 raise SystemExit("%s: no hash for %s" % (module, name))
             rows.append("{%s, R_ACTION, %s, %s, 0x%sULL, \"%s\"}," % (kind, act, form, h[name], name))
+            if name in GUARDED and name in eff and kind != "KRAFT":
+                rows.append("{%s, R_EFFECT, %s, %s, 0x%sULL, \"%s\"}," % (kind, act, form, eff[name], name))
         for name, iid in INVARIANTS.items():
             if name in h:
                 rows.append("{%s, R_INV, %d, 0, 0x%sULL, \"%s\"}," % (kind, iid, h[name], name))
