@@ -194,6 +194,11 @@ int rmc_model_next(const rmc_model* m, char* out, size_t len);
  * "name <hash>" line per definition into out and returns the text length,
  * or a negative value with the parse error in out. */
 int rmc_tla_hashes(const char* tla_text, char* out, size_t len);
+/* "<hash>:<file>,<file>,...": the first 32 hex digits of the SHA-256 of the
+ * listed source files (paths relative to raft-tlaplus_amd/), concatenated in
+ * that order, as the library was built from them.  A binding compares it with
+ * the tree's sources to refuse a stale build (raftmc.lib()). */
+const char* rmc_source_id(void);
 /* ABI self-description for binding checks (ctypes, JNA): fills up to cap values -- sizeof(rmc_options),
  * the offset of each of its fields in declaration order, then sizeof(rmc_result) and its field offsets --
  * and returns how many there are. */

@@ -530,6 +530,27 @@ struct Compiler {
         return expr(n->k[0], s2);
       }
       case N_QUANT: return quant(n, sc);
+      case N_SETFILTER: {  // {y \in S : P} over a constant set: the bitmask of the elements P holds for
+        if (n->bounds.size() != 1 || n->bounds[0].vars.size() != 1) fail(n, "set filter over several variables");
+        Ty et;
+        const std::vector<int> els = const_set(n->bounds[0].set, sc, et);
+        emit(G_CONST, 0);
+        for (int e : els) {
+          auto s2 = std::make_shared<Scope>();
+          s2->up = sc;
+          Binding b;
+          b.k = Binding::CONSTV;
+          b.v = e;
+          b.ty = et;
+          s2->names[n->bounds[0].vars[0]] = b;
+          if (concrete(expr(n->k[0], s2), n) != T_BOOL) fail(n, "set filter predicate is not a boolean");
+          const size_t skip = jump(G_JZ);
+          emit(G_CONST, e);
+          emit(G_SETADD);
+          patch(skip);
+        }
+        return set_of(et, n);
+      }
       default: break;
     }
     fail(n, "this construct");
@@ -571,6 +592,43 @@ std::vector<uint32_t> compile_guard(const Module& m, const std::vector<std::stri
     if (t != T_BOOL) c.fail(root, "the guard is not a boolean");
   }
   c.emit(G_END);
+  // guard_vm keeps its stack in eight registers: check every path's depth
+  // (the code is structured, so each instruction has one depth on all paths)
+  const std::vector<uint32_t>& code = c.code;
+  std::vector<int> at(code.size() + 1, -1);
+  std::vector<size_t> work{0};
+  at[0] = 0;
+  auto flow = [&](size_t to, int d) {
+    if (to > code.size()) throw std::runtime_error("guard of " + where + ": a jump leaves the code (compiler bug)");
+    if (at[to] < 0) { at[to] = d; work.push_back(to); }
+    else if (at[to] != d) throw std::runtime_error("guard of " + where + ": stack depths disagree at a join (compiler bug)");
+  };
+  while (!work.empty()) {
+    const size_t pc = work.back();
+    work.pop_back();
+    if (pc == code.size()) continue;
+    const uint32_t op = code[pc] & 0xFFu;
+    const int imm = (int)code[pc] >> 8;
+    int d = at[pc], need = 0, delta = 0;
+    switch (op) {
+      case G_END: if (d < 1) throw std::runtime_error("guard of " + where + ": empty stack at the end"); continue;
+      case G_CONST: case G_ARG: case G_ECTR: case G_RCTR: delta = 1; break;
+      case G_ST: case G_TERM: case G_VOTED: case G_VOTED2: case G_LEN: case G_COMMIT: case G_FSYNC: case G_VOTES:
+      case G_ACKED: case G_NEG: case G_NOT: case G_POPC: need = 1; break;
+      case G_JZ: case G_JNZ: need = 1; delta = -1; break;
+      case G_JMP: break;
+      case G_POP: need = 1; delta = -1; break;
+      default: need = 2; delta = -1; break;  // binary operators
+    }
+    if (d < need) throw std::runtime_error("guard of " + where + ": stack underflow (compiler bug)");
+    d += delta;
+    if (d > 8)
+      throw std::runtime_error("guard of " + where + " nests deeper than the guard machine's 8-value stack: split it "
+                               "into helper conjuncts");
+    if (op == G_JMP) { flow(pc + 1 + imm, d); continue; }
+    if (op == G_JZ || op == G_JNZ) flow(pc + 1 + imm, d);
+    flow(pc + 1, d);
+  }
   return c.code;
 }
 

@@ -11,6 +11,7 @@ The HIP path is the only path: if librmc.so is missing or no GPU is present,
 calls fail loudly (RaftmcError); there is no CPU fallback.
 """
 import ctypes
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -55,12 +56,28 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_model_free", "rmc_last_error", "rmc_version", "rmc_levels",
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
            "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm",
-           "rmc_abi_layout", "rmc_abi_version", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes"]
+           "rmc_abi_layout", "rmc_abi_version", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes",
+           "rmc_model_set_guard", "rmc_source_id"]
 
 # the rmc_options / rmc_result layout these ctypes mirrors follow (include/rmc.h RMC_ABI_VERSION)
 ABI_VERSION = 2
 
 _lib = None
+
+
+def source_mismatch(source_id):
+    """Compare a library's rmc_source_id with the tree's sources: None when they
+    match, else a short reason (the sources are raft-tlaplus_amd/-relative)."""
+    digest, _, files = source_id.partition(":")
+    h = hashlib.sha256()
+    base = os.path.dirname(_HERE)
+    for f in files.split(","):
+        try:
+            with open(os.path.join(base, f), "rb") as fh:
+                h.update(fh.read())
+        except OSError:
+            return "source %s is missing" % f
+    return None if h.hexdigest()[:32] == digest else "source hash %s, tree %s" % (digest, h.hexdigest()[:32])
 
 
 def lib():
@@ -88,7 +105,17 @@ def lib():
     if L.rmc_abi_version() != ABI_VERSION:
         raise RaftmcError("librmc.so has ABI version %d; this binding mirrors version %d (rebuild one of them)"
                           % (L.rmc_abi_version(), ABI_VERSION))
+    L.rmc_source_id.restype = ctypes.c_char_p
+    stale = source_mismatch(L.rmc_source_id().decode())
+    if stale and "RAFTMC_BUILD" in os.environ:
+        raise RaftmcError("%s was built from other sources than the tree's (%s): rebuild it "
+                          "(make -C raft-tlaplus_amd OUT=%s)" % (LIB_PATH, stale, os.environ["RAFTMC_BUILD"]))
+    if stale:
+        import warnings
+        warnings.warn("%s was built from other sources than the tree's (%s): run make -C raft-tlaplus_amd"
+                      % (LIB_PATH, stale))
     L.rmc_model_set_next.argtypes = [P, ctypes.c_char_p]
+    L.rmc_model_set_guard.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
     L.rmc_model_next.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_tla_hashes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_size_t]
     L.rmc_comm_unique_id.argtypes = [ctypes.c_char_p]
@@ -193,6 +220,17 @@ class Model:
         """Next as operator names of the spec family's definitions, in order
         (rmc_model_set_next: the TLA+ front end's lowering of such a Next)."""
         if lib().rmc_model_set_next(self._h, ",".join(disjuncts).encode()) != 0:
+            raise RaftmcError(lib().rmc_last_error().decode())
+
+    def set_guard(self, action, params, expr):
+        """Replace the guard of one of Next's simple actions (Restart,
+        RequestVote, Timeout, BecomeLeader, ClientRequest) by TLA+ expression
+        text over the state, the cfg's constants and the action's parameters
+        (rmc_model_set_guard: the front end's compiled guard, rmc_guard.cpp);
+        e.g. set_guard("RequestVote", "i", "electionCtr <= MaxElections")."""
+        if isinstance(params, (list, tuple)):
+            params = ", ".join(params)
+        if lib().rmc_model_set_guard(self._h, action.encode(), params.encode(), expr.encode()) != 0:
             raise RaftmcError(lib().rmc_last_error().decode())
 
     def next(self):

@@ -235,3 +235,47 @@ FRONTEND = [
     ("pull_dup_n3v1e1", "PullRaft", dict(n=3, v=1, E=1), NEXT_PULL + ("DuplicateMessage",), 8),
     ("pull2_drop_reversed_n3v1e1", "PullRaftVariant2", dict(n=3, v=1, E=1), tuple(reversed(NEXT_PULL)) + ("DropMessage",), 0),
 ]
+
+
+# (name, module, kwargs, [(action, params, TLA+ guard)], max_depth): Next with
+# actions behind a guard other than the reference's -- what a module whose
+# action keeps the reference's effect but states another guard lowers to
+# through the TLA+ front end (rmc_guard.cpp; rmc_model_set_guard is the same
+# table).  The Python side of each guard is make_golden.GUARD_PY[name].
+GUARDS = [
+    # Raft.tla:242-257 RequestVote with `electionCtr <= MaxElections`: one more election
+    ("raft_rv_le_n2v1e1", "Raft", dict(n=2, v=1, E=1),
+     [("RequestVote", "i", "electionCtr <= MaxElections /\\ state[i] \\in {Follower, Candidate}")], 0),
+    # Raft.tla:289-300 BecomeLeader that wants every vote
+    ("raft_bl_all_n3v1e1", "Raft", dict(n=3, v=1, E=1),
+     [("BecomeLeader", "i", "state[i] = Candidate /\\ votesGranted[i] = Server")], 0),
+    # Raft.tla:226-235 Restart only of a non-leader
+    ("raft_restart_nonleader_n2v1e2r1", "Raft", dict(n=2, v=1, E=2, R=1),
+     [("Restart", "i", "restartCtr < MaxRestarts /\\ state[i] /= Leader")], 0),
+    # Raft.tla:304-313 ClientRequest only while the leader has no entry of its own term
+    ("raft_client_lastterm_n2v2e2", "Raft", dict(n=2, v=2, E=2),
+     [("ClientRequest", "i, v",
+       "/\\ state[i] = Leader\n    /\\ acked[v] = Nil\n    /\\ LastTerm(log[i]) < currentTerm[i]")], 0),
+    # quantifiers, IF/LET and a set filter, two guards at once
+    ("raft_quant_n2v1e2", "Raft", dict(n=2, v=1, E=2),
+     [("BecomeLeader", "i",
+       "state[i] = Candidate /\\ votesGranted[i] \\in Quorum /\\ \\A j \\in Server : currentTerm[j] <= currentTerm[i]"),
+      ("RequestVote", "i",
+       "LET busy == \\E j \\in Server : state[j] = Leader IN "
+       "electionCtr < MaxElections /\\ state[i] \\in {Follower, Candidate} /\\ "
+       "IF busy THEN Cardinality({j \\in Server : currentTerm[j] > currentTerm[i]}) > 0 ELSE TRUE")], 0),
+    # FlexibleRaft.tla BecomeLeader at a fixed election quorum of 3 of 3
+    ("flex_bl_card_n3v1e1", "FlexibleRaft", dict(n=3, v=1, E=1, ElectionQuorumSize=2, ReplicationQuorumSize=2),
+     [("BecomeLeader", "i", "state[i] = Candidate /\\ Cardinality(votesGranted[i]) >= 3")], 0),
+    # RaftFsync.tla Timeout only of a follower, RequestVote(i, j) only to a server at a term <= i's
+    ("fsync_timeout_rvij_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1),
+     [("Timeout", "i", "electionCtr < MaxElections /\\ state[i] = Follower"),
+      ("RequestVote", "i, j", "state[i] = Candidate /\\ i /= j /\\ currentTerm[j] <= currentTerm[i]")], 0),
+    # PullRaft.tla:283-298 RequestVote only with no known leader
+    ("pull_rv_noleader_n2v1e2r1", "PullRaft", dict(n=2, v=1, E=2, R=1),
+     [("RequestVote", "i", "electionCtr < MaxElections /\\ state[i] \\in {Follower, Candidate} /\\ leader[i] = Nil")],
+     0),
+    # PullRaftVariant2 Restart gated on an empty log
+    ("pull2_restart_emptylog_n2v1e2r1", "PullRaftVariant2", dict(n=2, v=1, E=2, R=1),
+     [("Restart", "i", "restartCtr < MaxRestarts /\\ Len(log[i]) = 0")], 0),
+]

@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import (EXTRAS, FLEX_RESTART, FRONTEND, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
+from cfgs import (EXTRAS, FLEX_RESTART, FRONTEND, GUARDS, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
                   VARIANT2_N5, VARIANT2_SMALL, cfg_text)
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
@@ -263,7 +263,63 @@ def frontend():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def _guard_py():
+    """The Python side of every cfgs.GUARDS guard: {case: {action: g(spec, s, *args)}}."""
+    from oracle.pyoracle.raft import CANDIDATE, FOLLOWER, LEADER
+    from oracle.pyoracle.tlc import NIL
+    st, term = (lambda s, i: s["state"][i]), (lambda s, i: s["currentTerm"][i])
+
+    def quant_rv(sp, s, i):
+        busy = any(st(s, j) == LEADER for j in sp.Server)
+        return (s["electionCtr"] < sp.MaxElections and st(s, i) in (FOLLOWER, CANDIDATE) and
+                (len([j for j in sp.Server if term(s, j) > term(s, i)]) > 0 if busy else True))
+    return {
+        "raft_rv_le_n2v1e1": {"RequestVote": lambda sp, s, i: s["electionCtr"] <= sp.MaxElections and
+                              st(s, i) in (FOLLOWER, CANDIDATE)},
+        "raft_bl_all_n3v1e1": {"BecomeLeader": lambda sp, s, i: st(s, i) == CANDIDATE and
+                               s["votesGranted"][i] == frozenset(sp.Server)},
+        "raft_restart_nonleader_n2v1e2r1": {"Restart": lambda sp, s, i: s["restartCtr"] < sp.MaxRestarts and
+                                            st(s, i) != LEADER},
+        "raft_client_lastterm_n2v2e2": {"ClientRequest": lambda sp, s, i, v: st(s, i) == LEADER and
+                                        s["acked"][v] == NIL and sp.LastTerm(s["log"][i]) < term(s, i)},
+        "raft_quant_n2v1e2": {"BecomeLeader": lambda sp, s, i: st(s, i) == CANDIDATE and
+                              sp.IsQuorum(s["votesGranted"][i]) and all(term(s, j) <= term(s, i) for j in sp.Server),
+                              "RequestVote": quant_rv},
+        "flex_bl_card_n3v1e1": {"BecomeLeader": lambda sp, s, i: st(s, i) == CANDIDATE and
+                                len(s["votesGranted"][i]) >= 3},
+        "fsync_timeout_rvij_n2v1e2r1": {"Timeout": lambda sp, s, i: s["electionCtr"] < sp.MaxElections and
+                                        st(s, i) == FOLLOWER,
+                                        "RequestVote": lambda sp, s, i, j: st(s, i) == CANDIDATE and i != j and
+                                        term(s, j) <= term(s, i)},
+        "pull_rv_noleader_n2v1e2r1": {"RequestVote": lambda sp, s, i: s["electionCtr"] < sp.MaxElections and
+                                    st(s, i) in (FOLLOWER, CANDIDATE) and s["leader"][i] == NIL},
+        "pull2_restart_emptylog_n2v1e2r1": {"Restart": lambda sp, s, i: s["restartCtr"] < sp.MaxRestarts and
+                                            len(s["log"][i]) == 0},
+    }
+
+
+def guards():
+    """--guards: actions behind a guard other than the reference's (cfgs.GUARDS),
+    by the Python oracle with the same guard (_guard_py, written here by hand
+    from each TLA+ guard).  The C oracle has no configurable guards, so these
+    are pinned by the Python oracle alone."""
+    py = _guard_py()
+    out = {}
+    for name, module, kw, gs, md in GUARDS:
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        p = bfs(make_spec(module, cfg, guards=py[name]), max_depth=md or None)
+        out[name] = dict(module=module, cfg=txt, guards=[list(g) for g in gs], max_depth=md, generated=p.generated,
+                         distinct=p.distinct, depth=p.depth, status=p.status, levels=[list(x) for x in p.levels],
+                         hidden_same_level=p.hidden_same_level, max_msgs=p.max_msgs, pinned_by="pyoracle")
+        print(name, p.generated, p.distinct, p.depth, p.status, p.hidden_same_level, "%.1fs" % p.seconds, flush=True)
+    with open(os.path.join(HERE, "guards.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--guards" in sys.argv:
+        return guards()
     if "--frontend" in sys.argv:
         return frontend()
     if "--extras" in sys.argv:

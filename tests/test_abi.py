@@ -108,3 +108,14 @@ def test_result_prefix_is_survey_8b():
     for f, _ in Survey8b._fields_:
         assert getattr(raftmc.Result, f).offset == getattr(Survey8b, f).offset, f
     assert raftmc.Result.message.offset >= ctypes.sizeof(Survey8b)
+
+
+def test_source_id_matches_the_tree():
+    """rmc_source_id hashes the sources the library was built from; a variant
+    build made from other sources is refused at load (RAFTMC_BUILD)."""
+    sid = raftmc.lib().rmc_source_id().decode()
+    assert raftmc.source_mismatch(sid) is None
+    digest, _, files = sid.partition(":")
+    assert "csrc/rmc_kernels.hip" in files.split(",")
+    assert raftmc.source_mismatch("0" * 32 + ":" + files).startswith("source hash")
+    assert "missing" in raftmc.source_mismatch(digest + ":csrc/no_such_file.cpp")

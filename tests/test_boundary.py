@@ -42,18 +42,31 @@ def test_reference_cfg_same_first_levels(name):
 
 
 def test_edited_spec_is_refused(tmp_path):
-    """Raft with an action whose body computes something else (Restart gated
-    on restartCtr <= MaxRestarts instead of <, Raft.tla:227) is a different
-    spec: refused with a message naming the action, not checked as the
-    built-in one.  (Re-enabling the commented-out DuplicateMessage disjunct,
-    Raft.tla:540, is lowered instead: tests/test_frontend.py.)"""
+    """Raft with an action whose EFFECT computes something else (Restart
+    counting two restarts, Raft.tla:234) is a different spec: refused with a
+    message naming the action, not checked as the built-in one.  (An edited
+    GUARD -- Restart on restartCtr <= MaxRestarts, Raft.tla:227 -- is compiled
+    instead: tests/test_guards.py; re-enabling the commented-out
+    DuplicateMessage disjunct, Raft.tla:540, is lowered: tests/test_frontend.py.)"""
     txt = open(ref("Raft", ".tla")).read()
-    edited = txt.replace("    /\\ restartCtr < MaxRestarts\n", "    /\\ restartCtr <= MaxRestarts\n")
+    edited = txt.replace("    /\\ restartCtr'      = restartCtr + 1\n", "    /\\ restartCtr'      = restartCtr + 2\n")
     assert edited != txt
     p = tmp_path / "Raft.tla"
     p.write_text(edited)
     with pytest.raises(raftmc.RaftmcError, match="Next disjunct Restart"):
         raftmc.Model(str(p), ref("Raft", ".cfg"))
+
+
+def test_edited_guard_is_lowered(tmp_path):
+    """Restart gated on restartCtr <= MaxRestarts instead of < (Raft.tla:227):
+    the library's Restart effect behind the compiled guard (rmc_guard.cpp)."""
+    txt = open(ref("Raft", ".tla")).read()
+    edited = txt.replace("    /\\ restartCtr < MaxRestarts\n", "    /\\ restartCtr <= MaxRestarts\n")
+    assert edited != txt
+    p = tmp_path / "Raft.tla"
+    p.write_text(edited)
+    m = raftmc.Model(str(p), ref("Raft", ".cfg"))
+    assert m.next() == raftmc.Model(module="Raft", cfg_path=ref("Raft", ".cfg")).next()
 
 
 def test_comment_and_layout_edits_pass(tmp_path):

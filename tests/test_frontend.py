@@ -220,7 +220,8 @@ def test_renamed_helpers_and_module_are_accepted(tmp_path):
 @needs_ref
 def test_changed_action_is_refused_by_name(tmp_path):
     text = ref_text("Raft")
-    edited = text.replace("    /\\ electionCtr < MaxElections \n", "    /\\ electionCtr <= MaxElections \n")
+    # the effect edited (an edited guard is compiled instead: tests/test_guards.py)
+    edited = text.replace("    /\\ votedFor' = [votedFor EXCEPT ![i] = i]", "    /\\ votedFor' = [votedFor EXCEPT ![i] = Nil]")
     assert edited != text
     cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
     with pytest.raises(raftmc.RaftmcError, match="RequestVote"):
