@@ -163,6 +163,8 @@ LADDERS = [
     # largest exhausted rung), pinned by the oracles on their first levels
     ("raft_n3v2e2_bench", "Raft", "configs/Raft_n3v2e2.cfg", 20000000, 20000),
     ("fsync_n3v1e2r1_rung", "RaftFsync", "configs/RaftFsync_n3v1e2r1.cfg", 20000000, 20000),
+    # BASELINE config 3 verbatim (FlexibleRaft.cfg: N=5, EQ=3, RQ=4, V=2, E=2)
+    ("flex_cfg3", "FlexibleRaft", "configs/FlexibleRaft.cfg", 10000000, 3000),
 ]
 
 # FlexibleRaft's Restart (FlexibleRaft.tla:200-208) with MaxRestarts >= 1:

@@ -165,8 +165,12 @@ def ladders():
     """--ladders: BASELINE configs 2 and 5 at their scaled bounds (cfgs.LADDERS),
     level-truncated: the C oracle to the first level boundary past max_distinct,
     the Python oracle on a shorter prefix that must agree level by level."""
-    out = {}
+    only = sys.argv[sys.argv.index("--ladder-one") + 1] if "--ladder-one" in sys.argv else None
+    lp = os.path.join(HERE, "ladders.json")
+    out = json.load(open(lp)) if only and os.path.exists(lp) else {}
     for name, module, path, c_max, py_max in LADDERS:
+        if only and name != only:
+            continue
         with open(os.path.join(ROOT, path)) as fh:
             txt = fh.read()
         cfg = parse_cfg(txt)
@@ -324,7 +328,7 @@ def main():
         return frontend()
     if "--extras" in sys.argv:
         return extras()
-    if "--ladders" in sys.argv:
+    if "--ladders" in sys.argv or "--ladder-one" in sys.argv:
         return ladders()
     if "--flex-restart" in sys.argv:
         return flex_restart()

@@ -10,7 +10,10 @@ rungs below them.
   first level boundary past 2*10^7 distinct states, its first 12 levels also
   reproduced by the literal Python oracle.  The GPU runs exactly that many
   levels (max_depth) and must match every (generated, new) pair and the
-  hidden-variable collisions, single-shard and with 2 logical shards.
+  hidden-variable collisions, single-shard, with 2 logical shards, and with 4
+  logical shards each keeping its levels in host pages.  Config 3
+  (FlexibleRaft.cfg verbatim, N = 5) likewise, to the first level boundary
+  past 10^7 distinct states.
 * The exhaustible rungs -- the bench workload Raft_n3v2e2 (1.885 * 10^9
   distinct) and RaftFsync_n3v1e2r1 (6.3 * 10^8) -- are checked in full:
   counts equal to the committed record (tests/golden/exhausted.json, made by
@@ -29,7 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LAD = json.load(open(os.path.join(HERE, "golden", "ladders.json")))
 EXH = json.load(open(os.path.join(HERE, "golden", "exhausted.json")))
-BEYOND = ["raft_n3v2e3_cfg2", "fsync_n3v2e3r1_cfg5"]
+BEYOND = ["raft_n3v2e3_cfg2", "fsync_n3v2e3r1_cfg5", "flex_cfg3"]
 
 pytestmark = pytest.mark.gpu
 
@@ -61,6 +64,14 @@ def test_ladder_prefix_logical_shards(name):
 def test_ladder_prefix_host_frontier(name):
     g = LAD[name]
     prefix_match(model(g).check(max_depth=g["depth"], host_frontier=1), g)
+
+
+@pytest.mark.parametrize("name", BEYOND)
+def test_ladder_prefix_sharded_host_frontiers(name):
+    """The configs beyond one GPU the way they are run at scale: fingerprint-
+    sharded (4 logical shards), every shard's levels in host pages."""
+    g = LAD[name]
+    prefix_match(model(g).check_logical(4, max_depth=g["depth"], host_frontier=1), g)
 
 
 _full = {}
