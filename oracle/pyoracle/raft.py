@@ -455,7 +455,7 @@ class RaftSpec:
         return self.default_actions()
 
     def ordered_actions(self, order):
-        """Next with the given disjuncts (by operator name) in the given order:
+        r"""Next with the given disjuncts (by operator name) in the given order:
         each disjunct's TLC actions as in the module's own Next, plus the network
         actions \E m \in DOMAIN messages : DuplicateMessage(m) / DropMessage(m)."""
         groups = {}

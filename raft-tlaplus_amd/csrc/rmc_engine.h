@@ -101,6 +101,9 @@ hipError_t upload_model(const Model& m);
 // sharded search (rmc_sharded.cpp)
 unsigned long long bucket_blocks(unsigned long long n);
 // blk_counts / blk_off: owner-major [W][bucket_blocks(n)]
+// sharded search: generator-side dedup of a tile's remote-owner candidates (OB_TDUP)
+void launch_tile_dedup(const LevelArgs& a, unsigned long long* cand_fp, unsigned long long* cand_val,
+                       uint32_t* cand_ob, hipStream_t s);
 void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_ob, unsigned long long n, int W,
                         unsigned int* blk_counts, hipStream_t s);
 void launch_bucket(const unsigned long long* cand_fp, const unsigned long long* cand_val, const uint32_t* cand_ob,

@@ -33,6 +33,7 @@ constexpr int EXPAND_SEGS = 8;  // candidate-buffer segments of the single-shard
 // cand_ob = ordinal << 16 | flags | binding (10 bits)
 constexpr uint32_t OB_ERR = 0x8000u;    // evaluation error: no successor
 constexpr uint32_t OB_LOCAL = 0x4000u;  // sharded search: this shard owns the fp and k_expand inserted it
+constexpr uint32_t OB_TDUP = 0x2000u;   // sharded search: repeats an earlier-ranked candidate of its tile (k_tile_dedup)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -98,8 +99,15 @@ constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
 #ifdef RMC_TILE_DEDUP
 constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-successor round
 #endif
+// Persistent k_expand (default): a grid of resident blocks walks the tiles,
+// and each block stages tile t+G's parent rows into a second LDS buffer by
+// LDS-DMA while tile t runs phases B-C (RMC_EXPAND_PERSIST=0: one tile per
+// block, staged synchronously).
+#ifndef RMC_EXPAND_PERSIST
+#define RMC_EXPAND_PERSIST 1
+#endif
 struct ExpandLds {
-  int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, bytes;
+  int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, off_S2, bytes;
 };
 __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes, int nfixed, int nord) {
   ExpandLds L;
@@ -130,11 +138,65 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
   o += PB * LIVE_WORDS * 4;
 #ifdef RMC_TILE_DEDUP
   const int hash_end = L.off_Hash + DEDUP * 12;
-  L.bytes = o > hash_end ? o : hash_end;
-#else
-  L.bytes = o;
+  o = o > hash_end ? o : hash_end;
 #endif
+  o = (o + 15) & ~15;
+  L.off_S2 = o;  // persistent kernel: the second parent-row buffer (the next tile, in flight)
+#if RMC_EXPAND_PERSIST
+  o += PB * L.Wp * 4;
+#endif
+  L.bytes = o;
   return L;
+}
+
+// LDS-DMA: lane l of the wave loads the dword at gsrc into LDS byte address
+// lds_dst + 4 l (lds_dst wave-uniform).  Written as asm so that hipcc neither
+// counts it (it would drain it with vmcnt(0) at every barrier and before every
+// LDS read it cannot prove disjoint) nor reorders LDS accesses across it; its
+// completion is waited for explicitly (vmcnt(0) + a barrier) before the
+// buffer is read.  M0 is saved and restored in the same statement.
+__device__ __forceinline__ void lds_dma_dword(const uint32_t* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// Rows [p0, p0 + np) of the frontier -> LDS rows of stride Wp words at dst,
+// by LDS-DMA: wave w takes rows w, w+4, ..., one instruction per 64 words of
+// a row (lanes past the row's end masked off), so the padded stride is kept.
+__device__ __forceinline__ void stage_rows_async(const uint32_t* __restrict__ frontier, unsigned long long p0, int np,
+                                                 int words, int Wp, uint32_t* dst) {
+  const int wv = threadIdx.x / WAVE, l = lane_id();
+  for (int p = wv; p < np; p += 256 / WAVE) {
+    const uint32_t* row = frontier + (p0 + p) * (unsigned long long)words;
+    const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(dst + p * Wp));
+    for (int c = 0; c < words; c += WAVE)
+      if (c + l < words) lds_dma_dword(row + c + l, base + 4u * (uint32_t)c);
+  }
+}
+__device__ __forceinline__ void wait_lds_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The same rows through registers (rows are a multiple of 4 words, 16 B
+// aligned: 16 B loads, 4 LDS writes each).  (Staging only each row's used
+// words -- headers first, then the 16 B units up to the last message -- was
+// measured and rejected: k_expand 852 vs 829 ms, k_materialize 447 vs 432 per
+// check; the dependent header load costs more than the bytes it saves.
+// profiles/r04/ab_stage_trim_r04u.txt)
+__device__ __forceinline__ void stage_rows_sync(const uint32_t* __restrict__ frontier, unsigned long long p0, int np,
+                                                int words, int Wp, uint32_t* dst) {
+  const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
+  for (int q = threadIdx.x; q < np * (words >> 2); q += 256) {
+    const int w = q << 2, p = w / words;
+    const uint4 v = src[q];
+    uint32_t* d = dst + p * Wp + (w - p * words);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
 }
 
 __device__ __forceinline__ int select_bit(const uint32_t* w, int j) {  // j-th set bit (0-based)
@@ -178,8 +240,15 @@ __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set 
 // Occupancy target (waves per SIMD) for k_expand: 8 caps it at 64 VGPRs with
 // no extra scratch for N <= 4, 4% faster than the compiler's 78-VGPR choice
 // on the bench workload (1.289 s vs 1.340 s).
+// The persistent form holds two parent-row buffers (about 31 KB of LDS per
+// block on the bench workload): 5 blocks per CU fit, so it is compiled for 5
+// waves per SIMD (96 VGPRs; at 7 the tile loop spilled 49 VGPRs to scratch).
 #ifndef RMC_EXPAND_WAVES
+#if RMC_EXPAND_PERSIST
+#define RMC_EXPAND_WAVES 5
+#else
 #define RMC_EXPAND_WAVES 7
+#endif
 #endif
 // FPW: fingerprint width in 64-bit words (1, or 2 for fp_bits = 128).
 template <int N, int FPW>
@@ -219,54 +288,104 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ unsigned long long sG, sSeg;
   __shared__ int sAFirst[MAXACT], sAEnd[MAXACT], sAChunk[MAXACT + 1];
-  const int tid = threadIdx.x;
   using MS = typename SumsOf<N, FPW>::T;
-  const int words = cM.words, ordw = cM.ord_words;
-  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS), cM.nfixed, cM.ordinal_limit);
-  uint32_t* sS = (uint32_t*)lds;
-  MS* sMS = (MS*)(lds + L.off_Ms);
-  uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);
-  uint32_t* sBase = (uint32_t*)(lds + L.off_Base);
-  uint32_t* sLive = (uint32_t*)(lds + L.off_Live);
-  unsigned long long* sMask = (unsigned long long*)(lds + L.off_Mask);
-  uint32_t* sBOff = (uint32_t*)(lds + L.off_BOff);
-  uint32_t* sDesc = (uint32_t*)(lds + L.off_Desc);
-  uint16_t* sO2b = (uint16_t*)(lds + L.off_O2b);
-  uint16_t* sMOff = (uint16_t*)(lds + L.off_MOff);
-  const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
-  const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
+  // the tile's LDS arrays (the same layout in both kernel forms)
+#define RMC_EXPAND_LDS_ARRAYS                                                                         \
+  const int words = cM.words, ordw = cM.ord_words;                                                     \
+  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS), cM.nfixed, cM.ordinal_limit);      \
+  MS* sMS = (MS*)(lds + L.off_Ms);                                                                     \
+  uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);                                                       \
+  uint32_t* sBase = (uint32_t*)(lds + L.off_Base);                                                     \
+  uint32_t* sLive = (uint32_t*)(lds + L.off_Live);                                                     \
+  unsigned long long* sMask = (unsigned long long*)(lds + L.off_Mask);                                 \
+  uint32_t* sBOff = (uint32_t*)(lds + L.off_BOff);                                                     \
+  uint32_t* sDesc = (uint32_t*)(lds + L.off_Desc);                                                     \
+  uint16_t* sO2b = (uint16_t*)(lds + L.off_O2b);                                                       \
+  uint16_t* sMOff = (uint16_t*)(lds + L.off_MOff);                                                     \
+  (void)sMS, (void)sOrd, (void)sBase, (void)sLive, (void)sMask, (void)sBOff, (void)sDesc, (void)sO2b, (void)sMOff;
 #ifdef RMC_STAMPS
   unsigned long long t_prev = clock64();
 #endif
-  // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
-  // rows are a multiple of 4 words (16 B aligned): 16 B loads, 4 LDS writes each
-  const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
-  // (Staging only each row's used words -- headers first, then the 16 B units
-  // up to the last message -- was measured and rejected: k_expand 852 vs 829
-  // ms, k_materialize 447 vs 432 per check; the dependent header load costs
-  // more than the bytes it saves.  profiles/r04/ab_stage_trim_r04u.txt)
-  for (int q = tid; q < np * (words >> 2); q += 256) {
-    const int w = q << 2, p = w / words;
-    const uint4 v = src[q];
-    uint32_t* d = sS + p * L.Wp + (w - p * words);
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-    d[3] = v.w;
+#if RMC_EXPAND_PERSIST
+  // ---- A: the block's tiles are blockIdx.x, blockIdx.x + G, ...  Tile t's
+  //      rows were put in flight (LDS-DMA) before tile t-G's phase B; the
+  //      wait below retires them, and tile t+G's go in flight into the other
+  //      buffer, whose last reader (tile t-G's phase C) is past the barrier.
+  //      A capacity flag (the chunk will be redone or the check stopped) ends
+  //      the walk early.
+  __shared__ int sQuit;
+  const unsigned long long ntiles = (nparents + PB - 1) / PB;
+  {
+    const int tid = threadIdx.x;
+    RMC_EXPAND_LDS_ARRAYS
+    // the model's binding tables: once per block
+    for (int q = tid; q < cM.nfixed; q += 256) sDesc[q] = cM.fb_desc[q];
+    for (int q = tid; q < cM.ordinal_limit; q += 256) sO2b[q] = cM.ord2b[q];
+    for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
+    if (blockIdx.x < ntiles && lds_addr(lds) + (uint32_t)L.bytes <= 65536u)
+      stage_rows_async(frontier, blockIdx.x * (unsigned long long)PB,
+                       (int)min((unsigned long long)PB, nparents - blockIdx.x * (unsigned long long)PB), words, L.Wp,
+                       (uint32_t*)lds);
   }
-  for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
-  for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
-  for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
-  for (int q = tid; q < cM.nfixed; q += 256) sDesc[q] = cM.fb_desc[q];
-  for (int q = tid; q < cM.ordinal_limit; q += 256) sO2b[q] = cM.ord2b[q];
-  for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
-  __syncthreads();
+  unsigned long long tile = blockIdx.x;
+  for (int buf = 0; tile < ntiles; tile += gridDim.x, buf ^= 1) {
+    // Everything per lane or per model is re-derived here from values the
+    // compiler cannot see are the same every tile (the thread id, the model's
+    // address): otherwise it hoists the lane addresses, masks and model loads
+    // of the whole body out of the walk and holds them live across it -- 76
+    // VGPRs of scratch spills at the 7-wave register budget.
+    int tid_ = threadIdx.x;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_;
+    const __attribute__((address_space(4))) Model* mp4 = (const __attribute__((address_space(4))) Model*)&cM;
+    asm volatile("" : "+s"(mp4));
+    const Model& tM = *(const Model*)mp4;
+#define cM tM
+    RMC_EXPAND_LDS_ARRAYS
+    uint32_t* sS = (uint32_t*)(lds + (buf ? L.off_S2 : 0));
+    const unsigned long long p0 = tile * PB;
+    const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
+    if (tid == 0) sQuit = *(volatile unsigned*)&st->cap_flags != 0;
+    wait_lds_dma();
+    __syncthreads();  // the tile's rows have landed; the previous tile's phase C is done with every LDS array
+    if (sQuit) break;
+    // (LDS-DMA takes its destination from M0, of which only the low 16 bits
+    // are trusted here: a layout past 64 KB -- rows widened near their cap on
+    // N = 5 -- stages each tile synchronously instead)
+    if (lds_addr(lds) + (uint32_t)L.bytes > 65536u) {
+      stage_rows_sync(frontier, p0, np, words, L.Wp, sS);
+    } else if (tile + gridDim.x < ntiles) {
+      const unsigned long long q0 = (tile + gridDim.x) * PB;
+      stage_rows_async(frontier, q0, (int)min((unsigned long long)PB, nparents - q0), words, L.Wp,
+                       (uint32_t*)(lds + (buf ? 0 : L.off_S2)));
+    }
+    for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
+    for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
+    for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
+    __syncthreads();
+#else
+  for (int once = 0; once < 1; once++) {  // one tile per block (`continue` ends it)
+    const int tid = threadIdx.x;
+    RMC_EXPAND_LDS_ARRAYS
+    uint32_t* sS = (uint32_t*)lds;
+    const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
+    const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
+    // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
+    stage_rows_sync(frontier, p0, np, words, L.Wp, sS);
+    for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
+    for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
+    for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
+    for (int q = tid; q < cM.nfixed; q += 256) sDesc[q] = cM.fb_desc[q];
+    for (int q = tid; q < cM.ordinal_limit; q += 256) sO2b[q] = cM.ord2b[q];
+    for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
+    __syncthreads();
+#endif
   STAMP(0);
   if (diag == 4) {  // staging only (a checksum keeps it live)
     uint32_t x = 0;
     for (int q = tid; q < np * words; q += 256) x ^= sS[(q / words) * L.Wp + q % words];
     if (tid < np) par_n[p0 + tid] = x;
-    return;
+    continue;
   }
   // ---- B: enabled bindings, lane per parent
   {
@@ -462,7 +581,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     // atomics per launch on one address.  The sharded search needs its
     // candidates dense, so it keeps one counter.
     if (tid == 0) {
-      const int seg = sharded ? 0 : (int)(blockIdx.x & (EXPAND_SEGS - 1));
+      const int seg = sharded ? 0 : (int)((p0 / PB) & (EXPAND_SEGS - 1));
       const unsigned long long seg_cap = sharded ? cand_cap : cand_cap / EXPAND_SEGS;
       sSeg = seg_cap;
       sG = seg * seg_cap + (total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL);
@@ -477,9 +596,9 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   }
   if (gbase % sSeg + (unsigned long long)total > sSeg) {
     if (tid == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
-    return;
+    continue;
   }
-  if (diag == 3) return;  // bindings only
+  if (diag == 3) continue;  // bindings only
 #ifdef RMC_STAMPS
   // diagnostic: phase C without the fingerprint-set inserts (stamp 7), so the
   // inserts' share is the difference from the real phase C (stamp 3)
@@ -595,7 +714,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
         __syncthreads();  // the next round resets the table
       }
       STAMP(3);
-      return;
+      continue;
     }
   }
 #endif
@@ -653,6 +772,14 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     cand_ob[t] = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : local);
   }
   STAMP(3);
+  }  // tile loop
+#if RMC_EXPAND_PERSIST
+#undef cM
+#endif
+#undef RMC_EXPAND_LDS_ARRAYS
+#if RMC_EXPAND_PERSIST
+  wait_lds_dma();  // (a walk ended early may leave its prefetch in flight)
+#endif
 }
 
 // One thread per parent: which of its candidates won their fingerprint, and
@@ -970,9 +1097,79 @@ __global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* _
   if (threadIdx.x < W) h[threadIdx.x] = 0;
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n && !(cand_ob[t] & (OB_ERR | OB_LOCAL))) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
+  if (t < n && !(cand_ob[t] & (OB_ERR | OB_LOCAL | OB_TDUP))) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
   __syncthreads();
   if (threadIdx.x < W) blk_counts[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+// Generator-side dedup of the remote-owner candidates, one block per
+// k_expand tile (its candidates are one contiguous range).  37 % of a tile's
+// successors repeat a fingerprint another successor of the same tile produced
+// (commuting actions of sibling parents).  Only the lowest-ranked of them (the
+// first in TLC order) can win at the owner, so the others need not travel:
+// one whose hidden variables equal that representative's is marked OB_TDUP
+// and its cand_val becomes the representative's candidate index.  Its outcome
+// is then known from the representative's flag: it loses, and it is a
+// hidden-variable collision exactly when the representative lost with one
+// (k_mark_recv's flag 2).  A repeat with other hidden variables is sent as
+// before (the owner counts its collision against the real winner).  Windows
+// of DEDUP_WIN candidates; repeats across windows are sent, as before.
+constexpr int DEDUP_WIN = 512, DEDUP_SLOTS = 1024;
+__global__ __launch_bounds__(256) void k_tile_dedup(unsigned long long nparents, const uint32_t* __restrict__ par_off,
+                                                    const uint32_t* __restrict__ par_n,
+                                                    const unsigned long long* __restrict__ cand_fp,
+                                                    unsigned long long* __restrict__ cand_val,
+                                                    uint32_t* __restrict__ cand_ob) {
+  __shared__ unsigned long long sK[DEDUP_SLOTS], sV[DEDUP_SLOTS];
+  __shared__ uint32_t sI[DEDUP_SLOTS];
+  constexpr int PB = 64;  // = Tile<N>::PB, every N
+  const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
+  const unsigned long long pl = min(nparents, p0 + PB) - 1;
+  const uint32_t t0 = par_off[p0], t1 = par_off[pl] + par_n[pl];
+  for (uint32_t w0 = t0; w0 < t1; w0 += DEDUP_WIN) {
+    const uint32_t w1 = min(t1, w0 + (uint32_t)DEDUP_WIN);
+    for (int q = threadIdx.x; q < DEDUP_SLOTS; q += 256) {
+      sK[q] = EMPTY;
+      sV[q] = ~0ULL;
+    }
+    __syncthreads();
+    constexpr int PER = DEDUP_WIN / 256;
+    int h[PER];
+    unsigned long long v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const uint32_t t = w0 + threadIdx.x + 256u * u;
+      h[u] = -1;
+      if (t < w1 && !(cand_ob[t] & (OB_ERR | OB_LOCAL))) {
+        const unsigned long long fp = cand_fp[t];
+        v[u] = cand_val[t];
+        int k = (int)((fp * 0x9E3779B97F4A7C15ULL) >> 54);  // top 10 bits
+        for (;;) {  // <= DEDUP_WIN keys in DEDUP_SLOTS slots: a slot is always found
+          const unsigned long long prev = atomicCAS(&sK[k], EMPTY, fp);
+          if (prev == EMPTY || prev == fp) break;
+          k = (k + 1) & (DEDUP_SLOTS - 1);
+        }
+        atomicMin(&sV[k], v[u]);
+        h[u] = k;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; u++)
+      if (h[u] >= 0 && sV[h[u]] == v[u]) sI[h[u]] = w0 + threadIdx.x + 256u * u;  // the representative
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      if (h[u] < 0) continue;
+      const unsigned long long rv = sV[h[u]];
+      if (rv != v[u] && ((rv ^ v[u]) & 0xFFFFULL) == 0) {
+        const uint32_t t = w0 + threadIdx.x + 256u * u;
+        cand_ob[t] |= OB_TDUP;
+        cand_val[t] = sI[h[u]];
+      }
+    }
+    __syncthreads();  // the next window resets the table
+  }
 }
 
 // Scatter (fp, val) records into per-owner segments of the send buffer;
@@ -995,7 +1192,7 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  if (cand_ob[t] & (OB_ERR | OB_LOCAL)) {
+  if (cand_ob[t] & (OB_ERR | OB_LOCAL | OB_TDUP)) {
     perm[t] = 0xFFFFFFFFu;
     return;
   }
@@ -1080,22 +1277,24 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
   for (int u = 0; u < U; u++) {
     const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
     if (j >= n) continue;
-    bool w = false;
+    bool w = false, c = false;
     if (!(rs[u] & CAND_DUP)) {
       const unsigned long long mine = recv[2 * j + 1];
-      bool c = false;
       w = fpset_won(tv[u], mine >> VAL_RANK_SHIFT, floor, mine, c);
       colls += c;
     }
+    // 1 won; 2 lost with a hidden-variable collision (the generator's OB_TDUP
+    // repeats of this record collide too); 0 lost
+    const uint8_t fl = w ? 1 : c ? 2 : 0;
     if (fbase) {
       int lo = 0, hi = W - 1;  // source q: srs[q] <= j < srs[q+1]
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (srs[mid] <= j) lo = mid; else hi = mid - 1;
       }
-      *reinterpret_cast<uint8_t*>(sfb[lo] + j) = w ? 1 : 0;
+      *reinterpret_cast<uint8_t*>(sfb[lo] + j) = fl;
     } else {
-      flag[j] = w ? 1 : 0;
+      flag[j] = fl;
     }
     wins += w;
   }
@@ -1151,9 +1350,11 @@ __global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, u
           if (mine[u] & CAND_DUP) { ob[u] |= OB_ERR; continue; }
           v[u] = moved ? fpset_value(table, mask, cand_val[t]) : table[2 * (mine[u] & CAND_SLOT_MASK) + 1];
           mine[u] >>= 47;
+        } else if (ob[u] & OB_TDUP) {  // loses to its tile's representative; collides when that did
+          coll += flag_back[perm[(uint32_t)cand_val[t]]] == 2 ? 1u : 0u;
         } else {
           const uint32_t q = perm[t];
-          w[u] = flag_back[q] != 0;
+          w[u] = flag_back[q] == 1;
         }
       }
 #pragma unroll
@@ -1182,6 +1383,12 @@ __global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, u
 }
 
 unsigned long long bucket_blocks(unsigned long long n) { return n ? (n + 255) / 256 : 1; }
+void launch_tile_dedup(const LevelArgs& a, unsigned long long* cand_fp, unsigned long long* cand_val,
+                       uint32_t* cand_ob, hipStream_t s) {
+  if (!a.nparents) return;
+  hipLaunchKernelGGL(k_tile_dedup, dim3((unsigned)((a.nparents + 63) / 64)), dim3(256), 0, s, a.nparents, a.par_off,
+                     a.par_n, cand_fp, cand_val, cand_ob);
+}
 void launch_owner_count(const unsigned long long* cand_fp, const uint32_t* cand_ob, unsigned long long n, int W,
                         unsigned int* blk_counts, hipStream_t s) {
   hipLaunchKernelGGL(k_owner_count, dim3((unsigned)bucket_blocks(n)), dim3(256), 0, s, cand_fp, cand_ob, n, W,
@@ -1238,6 +1445,22 @@ struct Launch {
     const Model& M = *a.model;
     ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T), M.nfixed,
                              M.ordinal_limit);
+#if RMC_EXPAND_PERSIST
+    {  // resident blocks only: as many as the CUs hold at this LDS size
+      static int cached_bytes = -1, cached_grid = 0;
+      if (cached_bytes != L.bytes) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_expand<SPEC, N, FPW, G>, 256,
+                                                         L.bytes) != hipSuccess)
+          throw std::runtime_error("k_expand: occupancy query failed");
+        cached_grid = std::max(1, cus * std::max(1, per_cu));
+        cached_bytes = L.bytes;
+      }
+      blocks = std::min<unsigned long long>(blocks, (unsigned long long)cached_grid);
+    }
+#endif
     hipLaunchKernelGGL((k_expand<SPEC, N, FPW, G>), dim3((unsigned)blocks), dim3(256), L.bytes, s, a.frontier, a.nparents, a.pbase,
                        a.floor, a.sharded, a.shard_self, a.table, a.mask, a.cand_slot, a.cand_ob, a.par_off, a.par_n, a.counters, a.cand_cap,
                        a.st, a.cand_val
@@ -1275,6 +1498,9 @@ static void dispatch_n(int N, bool expand, const LevelArgs& a, hipStream_t s) {
   }
 }
 static void dispatch(int spec, int N, bool expand, const LevelArgs& a, hipStream_t s) {
+#ifdef RMC_DEV_ONE  // development builds only: one instantiation (Raft, N = 3, 64-bit) compiles in seconds
+  if (spec == RAFT && N == 3) expand ? Launch::expand_w<RAFT, 3, 1>(a, s) : Launch::materialize<RAFT, 3>(a, s);
+#else
   switch (spec) {
     case RAFT: dispatch_n<RAFT>(N, expand, a, s); break;
     case FLEX: dispatch_n<FLEX>(N, expand, a, s); break;
@@ -1286,6 +1512,7 @@ static void dispatch(int spec, int N, bool expand, const LevelArgs& a, hipStream
       if (N == 3) expand ? Launch::expand<KRAFT, 3>(a, s) : Launch::materialize<KRAFT, 3>(a, s);
       break;
   }
+#endif
 }
 
 void launch_expand(int spec, int N, const LevelArgs& a, hipStream_t s) { dispatch(spec, N, true, a, s); }
@@ -1605,12 +1832,15 @@ void launch_simulate(int spec, int N, const uint32_t* init, unsigned long long w
                      DevStatus* st, int words, hipStream_t s) {
 #define RMC_SIM(SP, NN) \
   if (spec == SP && N == NN) return launch_sim_t<SP, NN>(init, walkers, depth, seed, binds, counters, ss, st, words, s);
-  RMC_SIM(RAFT, 2) RMC_SIM(RAFT, 3) RMC_SIM(RAFT, 4) RMC_SIM(RAFT, 5)
+  RMC_SIM(RAFT, 3)
+#ifndef RMC_DEV_ONE
+  RMC_SIM(RAFT, 2) RMC_SIM(RAFT, 4) RMC_SIM(RAFT, 5)
   RMC_SIM(FLEX, 2) RMC_SIM(FLEX, 3) RMC_SIM(FLEX, 4) RMC_SIM(FLEX, 5)
   RMC_SIM(FSYNC, 2) RMC_SIM(FSYNC, 3) RMC_SIM(FSYNC, 4) RMC_SIM(FSYNC, 5)
   RMC_SIM(PULL, 2) RMC_SIM(PULL, 3) RMC_SIM(PULL, 4) RMC_SIM(PULL, 5)
   RMC_SIM(PULL2, 2) RMC_SIM(PULL2, 3) RMC_SIM(PULL2, 4) RMC_SIM(PULL2, 5)
   RMC_SIM(KRAFT, 2) RMC_SIM(KRAFT, 3)
+#endif
 #undef RMC_SIM
 }
 

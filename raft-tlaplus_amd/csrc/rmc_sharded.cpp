@@ -582,6 +582,8 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
     HIPCHK(hipMemcpyAsync(&s.hst, s.B->stbuf.p, sizeof s.hst, hipMemcpyDeviceToHost, stream));
   };
   bool stop = false;
+  // generator-side dedup of each tile's remote candidates (RMC_SHARD_DEDUP=0 turns it off for an A/B)
+  const bool tile_dedup = !getenv("RMC_SHARD_DEDUP") || atoi(getenv("RMC_SHARD_DEDUP")) != 0;
   unsigned gmax_msgs = 0;  // largest |DOMAIN messages| materialized on any shard
   double rate = 4.0;       // new states per parent of the previous level (pre-sizes the tables per round)
   unsigned long long lbase = 0, floor = 0;
@@ -780,6 +782,13 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
             continue;
           }
           unsigned int* bc = s.B->bcnt.as<unsigned int>();
+          if (s.n && tile_dedup) {  // a tile's repeats of one fp stay home (OB_TDUP): fewer records to bucket and send
+            LevelArgs a;
+            round_args(a, s, c);
+            launch_tile_dedup(a, s.B->cfp.as<unsigned long long>(), s.B->cval.as<unsigned long long>(),
+                              s.B->cob.as<uint32_t>(), stream);
+            HIPCHK(hipGetLastError());
+          }
           HIPCHK(hipMemsetAsync(bc + nbw, 0, 4, stream));
           launch_owner_count(s.B->cfp.as<unsigned long long>(), s.B->cob.as<uint32_t>(), s.ncand, W, bc, stream);
           HIPCHK(hipGetLastError());
