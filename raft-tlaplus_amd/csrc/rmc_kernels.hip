@@ -286,7 +286,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
 #endif
   constexpr int PB = Tile<N>::PB;
   extern __shared__ __align__(16) unsigned char lds[];
-  __shared__ unsigned long long sG, sSeg;
+  __shared__ unsigned long long sG;
+  __shared__ int sOver;
   __shared__ int sAFirst[MAXACT], sAEnd[MAXACT], sAChunk[MAXACT + 1];
   using MS = typename SumsOf<N, FPW>::T;
   // the tile's LDS arrays (the same layout in both kernel forms)
@@ -311,9 +312,10 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   //      rows were put in flight (LDS-DMA) before tile t-G's phase B; the
   //      wait below retires them, and tile t+G's go in flight into the other
   //      buffer, whose last reader (tile t-G's phase C) is past the barrier.
-  //      A capacity flag (the chunk will be redone or the check stopped) ends
-  //      the walk early.
-  __shared__ int sQuit;
+  //      Every tile is walked even after a capacity flag: k_mark and the scan
+  //      run before the host reads the flags, and they read every parent's
+  //      par_off / par_n.  (An early exit on the flag left them stale -- a
+  //      fault in k_mark on a fresh model's message-slot widening.)
   const unsigned long long ntiles = (nparents + PB - 1) / PB;
   {
     const int tid = threadIdx.x;
@@ -345,10 +347,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     uint32_t* sS = (uint32_t*)(lds + (buf ? L.off_S2 : 0));
     const unsigned long long p0 = tile * PB;
     const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
-    if (tid == 0) sQuit = *(volatile unsigned*)&st->cap_flags != 0;
     wait_lds_dma();
     __syncthreads();  // the tile's rows have landed; the previous tile's phase C is done with every LDS array
-    if (sQuit) break;
     // (LDS-DMA takes its destination from M0, of which only the low 16 bits
     // are trusted here: a layout past 64 KB -- rows widened near their cap on
     // N = 5 -- stages each tile synchronously instead)
@@ -583,8 +583,9 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     if (tid == 0) {
       const int seg = sharded ? 0 : (int)((p0 / PB) & (EXPAND_SEGS - 1));
       const unsigned long long seg_cap = sharded ? cand_cap : cand_cap / EXPAND_SEGS;
-      sSeg = seg_cap;
-      sG = seg * seg_cap + (total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL);
+      const unsigned long long c = total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL;
+      sG = seg * seg_cap + c;
+      sOver = c + (unsigned long long)total > seg_cap;  // (c itself may be past the segment: no modulo test)
     }
   }
   __syncthreads();
@@ -594,7 +595,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     par_off[p0 + tid] = (uint32_t)(gbase + sBase[tid]);
     par_n[p0 + tid] = sBase[tid + 1] - sBase[tid];
   }
-  if (gbase % sSeg + (unsigned long long)total > sSeg) {
+  if (sOver) {
     if (tid == 0) atomicOr(&st->cap_flags, 1u << E_CAP_SUCC);
     continue;
   }
@@ -778,7 +779,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
 #endif
 #undef RMC_EXPAND_LDS_ARRAYS
 #if RMC_EXPAND_PERSIST
-  wait_lds_dma();  // (a walk ended early may leave its prefetch in flight)
+  wait_lds_dma();  // (the last tile issues no prefetch: a guard that nothing is in flight at exit)
 #endif
 }
 

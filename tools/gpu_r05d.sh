@@ -44,8 +44,9 @@ cp $(find $O/kt -name '*kernel_stats.csv' | head -n 1) $O/kernel_stats.csv
 find $O/kt -name '*kernel_trace.csv' -o -name '*agent_info.csv' | xargs rm -f
 head -n 6 $O/kernel_stats.csv
 cd $R
-for cfg in $RUNGS; do
-  timeout -k 10 ${RUNG_LIMIT:-150} ./raft-tlaplus_amd/build/raftmc -deadlock -json -v -hostfrontier 1 -module RaftFsync -config configs/$cfg.cfg > $O/ladder_$cfg.txt 2>&1; rc=$?
+for mc in $RUNGS; do  # Module:cfg
+  mod=${mc%%:*}; cfg=${mc#*:}
+  timeout -k 10 ${RUNG_LIMIT:-150} ./raft-tlaplus_amd/build/raftmc -deadlock -json -v -hostfrontier 1 -module $mod -config configs/$cfg.cfg > $O/ladder_$cfg.txt 2>&1; rc=$?
   echo "$cfg rc=$rc"; tail -n 2 $O/ladder_$cfg.txt
   [ $rc -eq 0 ] || [ $rc -eq 12 ] || [ $rc -eq 13 ] || exit $rc
 done
