@@ -99,12 +99,16 @@ constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
 #ifdef RMC_TILE_DEDUP
 constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-successor round
 #endif
-// Persistent k_expand (default): a grid of resident blocks walks the tiles,
-// and each block stages tile t+G's parent rows into a second LDS buffer by
-// LDS-DMA while tile t runs phases B-C (RMC_EXPAND_PERSIST=0: one tile per
-// block, staged synchronously).
+// Persistent k_expand (-DRMC_EXPAND_PERSIST=1, measured and rejected in r05):
+// a grid of resident blocks walks the tiles, and each block stages tile t+G's
+// parent rows into a second LDS buffer by LDS-DMA while tile t runs phases
+// B-C.  The second buffer costs 12.5 KB of LDS per block on the bench
+// workload: 4 blocks per CU instead of 7, and the hidden staging does not buy
+// back the lost occupancy -- k_expand 1,122 vs 729 ms per check, two
+// interleaved runs each (profiles/r05/ab_persistent_expand.txt).  The default
+// stages one tile per block synchronously.
 #ifndef RMC_EXPAND_PERSIST
-#define RMC_EXPAND_PERSIST 1
+#define RMC_EXPAND_PERSIST 0
 #endif
 struct ExpandLds {
   int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, off_S2, bytes;
@@ -241,8 +245,9 @@ __device__ __forceinline__ int rank_below(const uint32_t* w, int bit) {  // set 
 // no extra scratch for N <= 4, 4% faster than the compiler's 78-VGPR choice
 // on the bench workload (1.289 s vs 1.340 s).
 // The persistent form holds two parent-row buffers (about 31 KB of LDS per
-// block on the bench workload): 5 blocks per CU fit, so it is compiled for 5
-// waves per SIMD (96 VGPRs; at 7 the tile loop spilled 49 VGPRs to scratch).
+// block on the bench workload): at most 5 blocks per CU fit, so it is
+// compiled for 5 waves per SIMD (96 VGPRs; at 7 its tile loop spilled 49
+// VGPRs to scratch).
 #ifndef RMC_EXPAND_WAVES
 #if RMC_EXPAND_PERSIST
 #define RMC_EXPAND_WAVES 5
