@@ -187,6 +187,16 @@ int rmc_model_set_next(rmc_model* m, const char* disjuncts);
  * "RequestVote", "i", "electionCtr <= MaxElections /\ state[i] = Follower").
  * Returns 0, or a negative value (rmc_last_error()). */
 int rmc_model_set_guard(rmc_model* m, const char* action, const char* params, const char* expr);
+/* Define an action by its TLA+ text, for rmc_model_set_next to put in Next by
+ * `name`: `name(params) == body`, read beside the spec family's VARIABLES,
+ * their groupings (serverVars, logVars, ...), Quorum, LastTerm and send
+ * helpers, and compiled whole -- its guard and its effect (rmc_guard.cpp
+ * compile_effect; Raft, FlexibleRaft, RaftFsync; 64-bit fingerprints).
+ * `form` is the binding: 0 \E i \in Server, 1 \E i \in Server, v \in Value,
+ * 2 \E i, j \in Server.  The same as a module whose Next has a disjunct with
+ * that body (rmc_model_load).  Returns 0, or -2 naming what it cannot
+ * compile (rmc_last_error). */
+int rmc_model_define_action(rmc_model* m, const char* name, int form, const char* params, const char* body);
 int rmc_model_next(const rmc_model* m, char* out, size_t len);
 /* The TLA+ front end's structural hashes of a module's definitions (the
  * closure hashes the lowering matches against its action library; used by

@@ -13,7 +13,7 @@ from .cfg import load_cfg, parse_cfg
 from .tlc import bfs, EvalError
 
 
-def make_spec(module, cfg, next_order=None, guards=None):
+def make_spec(module, cfg, next_order=None, guards=None, defined=None):
     from .raft import RaftSpec
     from .variants import FlexibleRaftSpec, RaftFsyncSpec, PullRaftSpec, PullRaftVariant2Spec
     from .kraft import KRaftSpec
@@ -29,4 +29,8 @@ def make_spec(module, cfg, next_order=None, guards=None):
         if module == "KRaft":
             raise ValueError("oracle: guard overrides are not offered for KRaft")
         kw["guards"] = guards
+    if defined:
+        if module not in ("Raft", "FlexibleRaft", "RaftFsync"):
+            raise ValueError("oracle: defined actions are offered for Raft, FlexibleRaft and RaftFsync")
+        kw["defined"] = defined
     return table[module](cfg["constants"], invariants=tuple(cfg["invariants"]), **kw)

@@ -31,7 +31,13 @@ class RaftSpec:
     hidden_vars = ("acked", "electionCtr", "restartCtr")
 
     def __init__(self, consts, invariants=("LeaderHasAllAckedValues", "NoLogDivergence"), next_order=None,
-                 guards=None):
+                 guards=None, defined=None):
+        # defined: {name: (form, f(spec, s, *args) -> successors)}: actions
+        # written in Python for next_order to name, bound as a Next disjunct
+        # \E i \in Server (form "i"), \E i \in Server, v \in Value ("iv") or
+        # \E i, j \in Server ("ij"): the oracle side of actions the front end
+        # compiles whole (rmc_guard.cpp compile_effect)
+        self.defined = dict(defined or {})
         # guards: {action name: g(spec, s, *args) -> bool} replacing the
         # reference's guard of that action (its effect unchanged): the oracle
         # side of the front end's compiled guards (rmc_guard.cpp)
@@ -463,6 +469,19 @@ class RaftSpec:
             groups.setdefault(label.split("(")[0], []).append((label, fn))
         groups["DuplicateMessage"] = [("DuplicateMessage", self.DuplicateMessage)]
         groups["DropMessage"] = [("DropMessage", self.DropMessage)]
+        n, vn = self.server_names, self.value_names
+        for name, (form, f) in self.defined.items():
+            # TLC order: the first bound variable varies fastest
+            if form == "i":
+                groups[name] = [("%s(%s)" % (name, n[i]), lambda s, f=f, i=i: f(self, s, i)) for i in self.Server]
+            elif form == "iv":
+                groups[name] = [("%s(%s,%s)" % (name, n[i], vn[v]), lambda s, f=f, i=i, v=v: f(self, s, i, v))
+                                for v in self.Value for i in self.Server]
+            elif form == "ij":
+                groups[name] = [("%s(%s,%s)" % (name, n[i], n[j]), lambda s, f=f, i=i, j=j: f(self, s, i, j))
+                                for i, j in self.pairs()]
+            else:
+                raise ValueError("form %r" % form)
         out = []
         for name in order:
             if name not in groups:

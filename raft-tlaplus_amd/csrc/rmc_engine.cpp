@@ -200,7 +200,8 @@ const char* act_label(int a) {
                             "RejectFetchRequest", "DivergingFetchRequest", "AcceptFetchRequest",
                             "HandleBeginQuorumRequest", "SendFetchRequest", "HandleSuccessFetchResponse",
                             "HandleDivergingFetchResponse", "HandleErrorFetchResponse", "DuplicateMessage",
-                            "DropMessage"};
+                            "DropMessage", "Compiled0", "Compiled1", "Compiled2", "Compiled3"};
+  static_assert(sizeof n / sizeof n[0] == A_NUM, "a label per action id");
   return (a >= 0 && a < A_NUM) ? n[a] : "?";
 }
 
@@ -360,9 +361,10 @@ void install_guards(rmc_model* m, const std::vector<rmc::tla::GuardSrc>& gs) {
   env.values = m->value_names;
   for (auto& kv : m->int_consts) env.ints.insert(kv);
   std::vector<uint32_t> code;
-  std::vector<std::pair<int, int>> starts;
+  std::vector<std::pair<int, int>> starts, estarts;
   for (const auto& g : gs) {
-    const int kind = g.act == A_CLIENT ? K_IV : g.act == A_RVIJ ? K_IJ : K_I;
+    const bool whole = g.act >= A_C0;  // compiled whole: guard and effect (rmc_guard.cpp compile_effect)
+    const int kind = whole ? g.kind : g.act == A_CLIENT ? K_IV : g.act == A_RVIJ ? K_IJ : K_I;
     const std::vector<int> types = kind == K_IV ? std::vector<int>{0, 1} : kind == K_IJ ? std::vector<int>{0, 0}
                                                                                          : std::vector<int>{0};
     if (g.params.size() != types.size())
@@ -371,6 +373,13 @@ void install_guards(rmc_model* m, const std::vector<rmc::tla::GuardSrc>& gs) {
     std::vector<uint32_t> c = rmc::tla::compile_guard(*g.mod, g.params, types, g.conjuncts, env, g.op);
     starts.push_back({g.act, (int)code.size()});
     code.insert(code.end(), c.begin(), c.end());
+    if (whole) {
+      rmc::tla::GuardEnv eenv = env;
+      eenv.send_helpers = g.send_helpers;
+      std::vector<uint32_t> e = rmc::tla::compile_effect(*g.mod, g.params, types, g.effects, eenv, g.op);
+      estarts.push_back({g.act - A_C0, (int)code.size()});
+      code.insert(code.end(), e.begin(), e.end());
+    }
   }
   if (code.size() > (size_t)MAXGCODE)
     throw std::runtime_error("compiled guards take " + std::to_string(code.size()) + " words (at most " +
@@ -379,6 +388,8 @@ void install_guards(rmc_model* m, const std::vector<rmc::tla::GuardSrc>& gs) {
   memset(M.gcode, 0, sizeof M.gcode);
   for (size_t q = 0; q < code.size(); q++) M.gcode[q] = code[q];
   for (auto& s2 : starts) M.gstart[s2.first] = (int16_t)s2.second;
+  for (int q = 0; q < MAXCOMPILED; q++) M.estart[q] = -1;
+  for (auto& s2 : estarts) M.estart[s2.first] = (int16_t)s2.second;
   M.gany = starts.empty() ? 0 : 1;
   m->guard_srcs = gs;
 }
@@ -427,6 +438,7 @@ rmc_model* load_model(const std::string& module, const std::string& cfg_text, co
     Model& M = m->M;
     memset(&M, 0, sizeof M);
     for (int a = 0; a < A_NUM; a++) M.gstart[a] = -1;  // the library's guards
+    for (int q = 0; q < MAXCOMPILED; q++) M.estart[q] = -1;
     M.spec = spec;
     CfgVal& S = need("Server");
     CfgVal& Vv = need("Value");
@@ -986,6 +998,8 @@ unsigned long long model_signature(const rmc_model* m) {
   for (auto& n : m->value_names) s += "|v:" + n;
   for (int a = 0; a < A_NUM; a++)  // compiled guards (rmc_guard.cpp) are part of the model
     if (M.gstart[a] >= 0) s += "|g" + std::to_string(a) + ":" + std::to_string(M.gstart[a]);
+  for (int q = 0; q < MAXCOMPILED; q++)
+    if (M.estart[q] >= 0) s += "|e" + std::to_string(q) + ":" + std::to_string(M.estart[q]);
   for (int q = 0; q < MAXGCODE && M.gcode[q]; q++) s += "," + std::to_string(M.gcode[q]);
   return fnv1a64(s);
 }
@@ -2523,10 +2537,85 @@ int rmc_model_set_next(rmc_model* m, const char* disjuncts) {
       }
     }
     if (names.empty()) throw std::runtime_error("empty Next");
-    m->lowered_actions = rmc::tla::actions_by_name(m->M.spec, names);
+    // actions defined as TLA+ text (rmc_model_define_action) are compiled
+    // whole, A_C0.. in Next order; the rest are the library's
+    std::vector<std::pair<int, int>> acts;
+    std::vector<rmc::tla::GuardSrc> srcs;
+    for (auto& g : m->guard_srcs)
+      if (g.act < A_C0) srcs.push_back(g);
+    int k = 0;
+    for (const std::string& n : names) {
+      auto it = m->defined_actions.find(n);
+      if (it == m->defined_actions.end()) {
+        acts.push_back(rmc::tla::actions_by_name(m->M.spec, {n})[0]);
+        continue;
+      }
+      if (k >= MAXCOMPILED) throw std::runtime_error("more than " + std::to_string(MAXCOMPILED) + " defined actions in Next");
+      rmc::tla::GuardSrc g = it->second;
+      g.act = A_C0 + k++;
+      acts.push_back({g.act, g.kind});
+      srcs.push_back(g);
+    }
+    const Model saved = m->M;
+    const std::vector<rmc::tla::GuardSrc> saved_srcs = m->guard_srcs;
+    try {
+      install_guards(m, srcs);
+    } catch (...) {
+      m->M = saved;
+      m->guard_srcs = saved_srcs;
+      throw;
+    }
+    m->lowered_actions = acts;
     m->lowered_labels = names;
     m->hint_slots = m->hint_fcap = m->hint_trcap = 0;
     m->hint_kmax = 0;
+    return 0;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -2;
+  }
+}
+
+int rmc_model_define_action(rmc_model* m, const char* name, int form, const char* params, const char* body) {
+  if (!m || !name || !params || !body) { g_last_error = "null argument"; return -1; }
+  try {
+    const int spec = m->M.spec;
+    if (spec != RAFT && spec != FLEX && spec != FSYNC)
+      throw std::runtime_error("actions compiled whole are offered for Raft, FlexibleRaft and RaftFsync");
+    if (form != K_I && form != K_IV && form != K_IJ)
+      throw std::runtime_error("form must be 0 (\\E i \\in Server), 1 (i \\in Server, v \\in Value) or 2 (i, j \\in Server)");
+    std::vector<std::string> ps;
+    std::string cur;
+    for (const char* p = params;; p++) {
+      if (*p == ',' || *p == 0) {
+        while (!cur.empty() && cur.back() == ' ') cur.pop_back();
+        if (!cur.empty()) ps.push_back(cur);
+        cur.clear();
+        if (!*p) break;
+      } else if (!(cur.empty() && *p == ' ')) {
+        cur += *p;
+      }
+    }
+    if ((int)ps.size() != (form == K_I ? 1 : 2))
+      throw std::runtime_error(std::string("action ") + name + ": the form binds " + (form == K_I ? "one" : "two") +
+                               " parameters");
+    rmc::tla::GuardSrc g = rmc::tla::parse_action(spec, name, form, ps, body);
+    // compile it once now, against this model's constants, so errors show here
+    {
+      rmc::tla::GuardEnv env;
+      env.spec = spec;
+      env.N = m->M.N;
+      env.V = m->M.V;
+      env.servers = m->server_names;
+      env.values = m->value_names;
+      for (auto& kv : m->int_consts) env.ints.insert(kv);
+      env.send_helpers = g.send_helpers;
+      const std::vector<int> types = form == K_IV ? std::vector<int>{0, 1} : form == K_IJ ? std::vector<int>{0, 0}
+                                                                                         : std::vector<int>{0};
+      (void)rmc::tla::compile_guard(*g.mod, g.params, types, g.conjuncts, env, name);
+      (void)rmc::tla::compile_effect(*g.mod, g.params, types, g.effects, env, name);
+    }
+    m->defined_actions[name] = g;
     return 0;
   } catch (std::exception& e) {
     g_last_error = e.what();
@@ -2582,7 +2671,11 @@ int rmc_model_next(const rmc_model* m, char* out, size_t len) {
   if (!m || !out || !len) return -1;
   std::string o;
   if (!m->lowered_actions.empty()) {
-    for (auto& a : m->lowered_actions) o += (o.empty() ? "" : ",") + rmc::tla::action_name(m->M.spec, a.first);
+    for (size_t q = 0; q < m->lowered_actions.size(); q++) {
+      const int a = m->lowered_actions[q].first;
+      o += (o.empty() ? "" : ",") + (a >= A_C0 && q < m->lowered_labels.size() ? m->lowered_labels[q]
+                                                                                : rmc::tla::action_name(m->M.spec, a));
+    }
   } else {
     Model M = m->M;
     build_actions(M, nullptr);

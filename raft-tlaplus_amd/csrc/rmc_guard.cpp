@@ -81,6 +81,8 @@ struct Compiler {
   // parameters of inlined operators: name -> argument (innermost last)
   std::vector<std::pair<std::string, Arg>> params;
   int depth = 0;
+  // effects: `@` inside [x EXCEPT ![i] = ...] -- the old x[i], emitted by this
+  std::function<Ty()> at;
 
   Compiler(const Module& mod, const GuardEnv& e) : m(mod), env(e) {}
 
@@ -530,6 +532,9 @@ struct Compiler {
         return expr(n->k[0], s2);
       }
       case N_QUANT: return quant(n, sc);
+      case N_AT:
+        if (!at) fail(n, "@ outside an EXCEPT the effect compiler knows");
+        return at();
       case N_SETFILTER: {  // {y \in S : P} over a constant set: the bitmask of the elements P holds for
         if (n->bounds.size() != 1 || n->bounds[0].vars.size() != 1) fail(n, "set filter over several variables");
         Ty et;
@@ -629,6 +634,297 @@ std::vector<uint32_t> compile_guard(const Module& m, const std::vector<std::stri
     if (op == G_JZ || op == G_JNZ) flow(pc + 1 + imm, d);
     flow(pc + 1, d);
   }
+  return c.code;
+}
+
+namespace {
+// The stack-depth check of compile_guard, for any program (effects included).
+void check_depth(const std::vector<uint32_t>& code, const std::string& where) {
+  std::vector<int> at(code.size() + 1, -1);
+  std::vector<size_t> work{0};
+  at[0] = 0;
+  auto flow = [&](size_t to, int d) {
+    if (to > code.size()) throw std::runtime_error(where + ": a jump leaves the code (compiler bug)");
+    if (at[to] < 0) { at[to] = d; work.push_back(to); }
+    else if (at[to] != d) throw std::runtime_error(where + ": stack depths disagree at a join (compiler bug)");
+  };
+  while (!work.empty()) {
+    const size_t pc = work.back();
+    work.pop_back();
+    if (pc == code.size()) continue;
+    const uint32_t op = code[pc] & 0xFFu;
+    const int imm = (int)code[pc] >> 8;
+    int d = at[pc], need = 0, delta = 0;
+    switch (op) {
+      case G_END: case E_END: continue;
+      case G_CONST: case G_ARG: case G_ECTR: case G_RCTR: delta = 1; break;
+      case G_ST: case G_TERM: case G_VOTED: case G_VOTED2: case G_LEN: case G_COMMIT: case G_FSYNC: case G_VOTES:
+      case G_ACKED: case G_NEG: case G_NOT: case G_POPC: need = 1; break;
+      case G_JZ: case G_JNZ: need = 1; delta = -1; break;
+      case G_JMP: break;
+      case G_POP: case E_ST: case E_TERM: case E_VOTED: case E_VOTES: case E_COMMIT: case E_ECTR: case E_RCTR:
+        need = 1; delta = -1; break;
+      case E_ACKED: case E_APPEND: case E_NEXT: case E_MATCH: case E_PEND: need = 2; delta = -2; break;
+      case E_RVREQ: need = 5; delta = -5; break;
+      default: need = 2; delta = -1; break;  // binary operators
+    }
+    if (d < need) throw std::runtime_error(where + ": stack underflow (compiler bug)");
+    d += delta;
+    if (d > 8) throw std::runtime_error(where + " nests deeper than the machine's 8-value stack");
+    if (op == G_JMP) { flow(pc + 1 + imm, d); continue; }
+    if (op == G_JZ || op == G_JNZ) flow(pc + 1 + imm, d);
+    flow(pc + 1, d);
+  }
+}
+}  // namespace
+
+// An action's EFFECT compiled for effect_vm (rmc_spec.h): the conjuncts that
+// prime a variable, say UNCHANGED, or send messages, over the same typed
+// expression language as the guards (they read the unprimed state).  Server
+// variables may change at the action's own server only ([v EXCEPT ![i] = e],
+// with @), as every action of these specs does; the forms are those of the
+// specs' fixed-binding actions (Raft.tla:226-313): state, currentTerm,
+// votedFor, votesGranted, commitIndex, electionCtr, restartCtr, acked[v],
+// log[i] = Append(@, [term |-> t, value |-> v]), and SendMultipleOnce of a set
+// of RequestVoteRequest records {[...] : j \in S}.  Every VARIABLE must be
+// assigned, left UNCHANGED or (messages) sent to; anything else is refused
+// naming it.
+std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::string>& action_params,
+                                     const std::vector<int>& param_types, const std::vector<NodeP>& effects,
+                                     const GuardEnv& env, const std::string& where) {
+  Compiler c(m, env);
+  c.where = where;
+  auto fail = [&](const NodeP& n, const std::string& what) -> void {
+    throw std::runtime_error("effect of " + where + " (line " + std::to_string(n ? n->line : 0) + "): " + what);
+  };
+  if (env.spec != RAFT && env.spec != FLEX && env.spec != FSYNC)
+    throw std::runtime_error("effect of " + where + ": the effect compiler knows the Raft, FlexibleRaft and RaftFsync "
+                             "layouts only");
+  auto sc = std::make_shared<Scope>();
+  for (size_t q = 0; q < action_params.size(); q++) {
+    Binding b;
+    b.k = Binding::ARG;
+    b.v = (int)q;
+    b.ty = param_types[q] == 1 ? T_VAL : T_SRV;
+    sc->names[action_params[q]] = b;
+  }
+  std::set<std::string> vars(m.variables.begin(), m.variables.end()), done, kept;
+  auto mark = [&](const std::string& v, const NodeP& n) {
+    if (!vars.count(v)) fail(n, v + " is not a variable of the module");
+    if (done.count(v)) fail(n, v + " is changed twice");
+    if (kept.count(v)) fail(n, v + " is both changed and UNCHANGED");
+    done.insert(v);
+  };
+  // UNCHANGED e: variables, tuples of them, and definitions naming them (a
+  // variable may be named twice: RaftFsync.tla:116 lists fsyncIndex twice)
+  std::function<void(const NodeP&, int)> unchanged = [&](const NodeP& n, int depth) {
+    if (depth > 16) fail(n, "UNCHANGED nests too deeply");
+    if (n->kind == N_TUPLE) { for (auto& k : n->k) unchanged(k, depth + 1); return; }
+    if (n->kind == N_ID) {
+      if (vars.count(n->s)) {
+        if (done.count(n->s)) fail(n, n->s + " is both changed and UNCHANGED");
+        kept.insert(n->s);
+        return;
+      }
+      const Def* d = m.find(n->s);
+      if (d && d->params.empty() && d->body) { unchanged(d->body, depth + 1); return; }
+    }
+    fail(n, "UNCHANGED of something other than variables");
+  };
+  auto is_param0 = [&](const NodeP& n) { return n->kind == N_ID && !action_params.empty() && n->s == action_params[0]; };
+  auto value = [&](const NodeP& e, Ty want) {
+    if (e->kind == N_SETENUM && e->k.empty() && (want == T_SET_SRV || want == T_SET_VAL || want == T_SET_STATE)) {
+      c.emit(G_CONST, 0);  // {} takes the variable's set type
+      return;
+    }
+    Ty t = c.expr(e, sc);
+    if (t == T_NIL || t == T_TRUE || t == T_FALSE) {
+      c.emit(G_CONST, c.sym_code(t, want, e));
+      t = want;
+    }
+    if (t != want) fail(e, std::string("the new value is ") + ty_name(t) + ", the variable holds " + ty_name(want));
+  };
+  // [v EXCEPT ![p] = e]: the single path element and its value
+  auto except1 = [&](const NodeP& rhs, const std::string& v, NodeP& path, NodeP& val) {
+    if (rhs->kind != N_EXCEPT || rhs->k.size() != 2 || rhs->k[0]->kind != N_ID || rhs->k[0]->s != v ||
+        rhs->paths.size() != 1 || rhs->paths[0].size() != 1 || rhs->paths[0][0].field ||
+        rhs->paths[0][0].args.size() != 1)
+      fail(rhs, v + "' must be [" + v + " EXCEPT ![x] = e]");
+    path = rhs->paths[0][0].args[0];
+    val = rhs->k[1];
+  };
+  bool sent = false;
+  std::vector<NodeP> items;
+  for (auto& e : effects) c.flatten(e, "/\\", items);
+  for (auto& n : items) {
+    if (n->kind == N_UNARY && n->s == "UNCHANGED") { unchanged(n->k[0], 0); continue; }
+    if (n->kind == N_BIN && n->s == "=" && n->k[0]->kind == N_PRIME && n->k[0]->k[0]->kind == N_ID) {
+      const std::string v = n->k[0]->k[0]->s;
+      const NodeP& rhs = n->k[1];
+      mark(v, n);
+      uint32_t load = 0, store = 0;
+      Ty ty = T_INT;
+      if (v == "state") { load = G_ST; store = E_ST; ty = T_STATE; }
+      else if (v == "currentTerm") { load = G_TERM; store = E_TERM; ty = T_INT; }
+      else if (v == "votedFor") { load = G_VOTED; store = E_VOTED; ty = T_SRV; }
+      else if (v == "votesGranted") { load = G_VOTES; store = E_VOTES; ty = T_SET_SRV; }
+      else if (v == "commitIndex") { load = G_COMMIT; store = E_COMMIT; ty = T_INT; }
+      if (store) {
+        NodeP path, val;
+        except1(rhs, v, path, val);
+        if (!is_param0(path)) fail(path, v + " may change at the action's own server (" + action_params[0] + ") only");
+        c.at = [&c, load, ty]() { c.emit(G_ARG, 0); c.emit(load); return ty; };
+        value(val, ty);
+        c.at = nullptr;
+        c.emit(store);
+        continue;
+      }
+      // the leader's rows: [v EXCEPT ![i] = [j \in Server |-> e]] (unrolled over
+      // Server) or [v EXCEPT ![i][q] = e]
+      uint32_t rstore = 0;
+      Ty rty = T_INT;
+      if (v == "nextIndex") { rstore = E_NEXT; }
+      else if (v == "matchIndex") { rstore = E_MATCH; }
+      else if (v == "pendingResponse" && env.spec == RAFT) { rstore = E_PEND; rty = T_BOOL; }
+      if (rstore) {
+        if (rhs->kind != N_EXCEPT || rhs->k.size() != 2 || rhs->k[0]->kind != N_ID || rhs->k[0]->s != v ||
+            rhs->paths.size() != 1 || rhs->paths[0].empty() || rhs->paths[0].size() > 2 || rhs->paths[0][0].field ||
+            rhs->paths[0][0].args.size() != 1 || (rhs->paths[0].size() == 2 && (rhs->paths[0][1].field ||
+                                                                                 rhs->paths[0][1].args.size() != 1)))
+          fail(rhs, v + "' must be [" + v + " EXCEPT ![i] = [j \\in Server |-> e]] or [" + v + " EXCEPT ![i][j] = e]");
+        if (!is_param0(rhs->paths[0][0].args[0]))
+          fail(rhs->paths[0][0].args[0], v + " may change at the action's own server (" + action_params[0] + ") only");
+        const NodeP& val = rhs->k[1];
+        if (rhs->paths[0].size() == 2) {  // one entry: ![i][q] = e
+          const NodeP& q = rhs->paths[0][1].args[0];
+          if (c.concrete(c.expr(q, sc), q) != T_SRV) fail(q, v + " indexed by a non-server");
+          value(val, rty);
+          c.emit(rstore);
+          continue;
+        }
+        if (val->kind != N_FUNC || val->bounds.size() != 1 || val->bounds[0].vars.size() != 1 || !val->bounds[0].set ||
+            val->bounds[0].set->kind != N_ID || val->bounds[0].set->s != "Server")
+          fail(val, v + "[i]' must be a function [j \\in Server |-> e]");
+        for (int x = 0; x < env.N; x++) {
+          auto s2 = std::make_shared<Scope>();
+          s2->up = sc;
+          Binding b;
+          b.k = Binding::CONSTV;
+          b.v = x;
+          b.ty = T_SRV;
+          s2->names[val->bounds[0].vars[0]] = b;
+          c.emit(G_CONST, x);
+          Ty t = c.expr(val->k[0], s2);
+          if (t == T_NIL || t == T_TRUE || t == T_FALSE) {
+            c.emit(G_CONST, c.sym_code(t, rty, val->k[0]));
+            t = rty;
+          }
+          if (t != rty) fail(val->k[0], std::string("the new value is ") + ty_name(t) + ", " + v + " holds " + ty_name(rty));
+          c.emit(rstore);
+        }
+        continue;
+      }
+      if (v == "electionCtr" || v == "restartCtr") {
+        value(rhs, T_INT);
+        c.emit(v == "electionCtr" ? E_ECTR : E_RCTR);
+        continue;
+      }
+      if (v == "acked") {
+        NodeP path, val;
+        except1(rhs, v, path, val);
+        if (c.concrete(c.expr(path, sc), path) != T_VAL) fail(path, "acked indexed by a non-value");
+        value(val, T_ACK);  // (no @ here: the compiler refuses it)
+        c.emit(E_ACKED);
+        continue;
+      }
+      if (v == "log") {
+        NodeP path, val;
+        except1(rhs, v, path, val);
+        if (!is_param0(path)) fail(path, "log may change at the action's own server only");
+        const bool app = val->kind == N_APP && val->s == "Append" && val->k.size() == 2 && !m.find("Append");
+        const NodeP base = app ? val->k[0] : nullptr;
+        const bool on_own = base && (base->kind == N_AT || (base->kind == N_FAPP && base->k.size() == 2 &&
+                                                            base->k[0]->kind == N_ID && base->k[0]->s == "log" &&
+                                                            is_param0(base->k[1])));
+        if (!app || !on_own) fail(val, "log[i]' must be Append(@, entry) or Append(log[i], entry)");
+        const NodeP& rec = val->k[1];
+        if (rec->kind != N_RECORD || rec->names.size() != 2) fail(rec, "a log entry is [term |-> t, value |-> v]");
+        NodeP tv, vv;
+        for (size_t q = 0; q < 2; q++) (rec->names[q] == "term" ? tv : vv) = rec->k[q];
+        if (!tv || !vv) fail(rec, "a log entry is [term |-> t, value |-> v]");
+        value(tv, T_INT);
+        value(vv, T_VAL);
+        c.emit(E_APPEND);
+        continue;
+      }
+      fail(n, "the effect compiler does not assign " + v + " (it may stay UNCHANGED)");
+    }
+    // the bag helpers (the lowering checked each is the family's own, by closure
+    // hash): a set of RequestVoteRequest records {[...] : j \in S} sent all new
+    // (class 0), or one record sent new (1) or with its count + 1 (2)
+    if (n->kind == N_APP && n->k.size() == 1 && env.send_helpers.count(n->s)) {
+      const int cls = env.send_helpers.at(n->s);
+      if (sent) fail(n, "messages are sent twice");
+      sent = true;
+      mark("messages", n);
+      NodeP rec = n->k[0];
+      const NodeP S = cls == 0 ? n->k[0] : nullptr;
+      if (cls == 0) {
+        if (S->kind != N_SETMAP || S->bounds.size() != 1 || S->bounds[0].vars.size() != 1)
+          fail(S, n->s + " of something other than {record : j \\in S}");
+        rec = S->k[0];
+      }
+      if (rec->kind != N_RECORD) fail(rec, n->s + " of something other than a record literal");
+      std::map<std::string, NodeP> f;
+      for (size_t q = 0; q < rec->names.size(); q++) f[rec->names[q]] = rec->k[q];
+      const char* want[] = {"mtype", "mterm", "mlastLogTerm", "mlastLogIndex", "msource", "mdest"};
+      bool rv = f.size() == 6 && f.count("mtype") && f["mtype"]->kind == N_ID && f["mtype"]->s == "RequestVoteRequest";
+      for (const char* w : want) rv = rv && f.count(w);
+      if (!rv) fail(rec, "the effect compiler sends RequestVoteRequest records only");
+      auto send = [&](ScopeP s2) {
+        auto field = [&](const char* name, Ty t) {
+          Ty got = c.concrete(c.expr(f[name], s2), f[name]);
+          if (got != t) fail(f[name], std::string(name) + " is " + ty_name(got));
+        };
+        field("mterm", T_INT);
+        field("mlastLogTerm", T_INT);
+        field("mlastLogIndex", T_INT);
+        field("msource", T_SRV);
+        field("mdest", T_SRV);
+        c.emit(E_RVREQ, cls == 2 ? 1 : 0);
+      };
+      if (cls != 0) {
+        send(sc);
+        continue;
+      }
+      const std::string jv = S->bounds[0].vars[0];
+      // over every server x: if x \in S, send the record with j = x
+      for (int x = 0; x < env.N; x++) {
+        auto s2 = std::make_shared<Scope>();
+        s2->up = sc;
+        Binding b;
+        b.k = Binding::CONSTV;
+        b.v = x;
+        b.ty = T_SRV;
+        s2->names[jv] = b;
+        auto xnode = std::make_shared<Node>();
+        xnode->kind = N_ID;
+        xnode->s = jv;
+        xnode->line = S->line;
+        if (c.member(S, xnode, S->bounds[0].set, sc, s2) != T_BOOL) fail(S, "the message set's domain");
+        const size_t skip = c.jump(G_JZ);
+        send(s2);
+        c.patch(skip);
+      }
+      continue;
+    }
+    fail(n, "this effect conjunct (the effect compiler knows v' = ..., UNCHANGED and the module's send helpers)");
+  }
+  for (const std::string& v : vars)
+    if (!done.count(v) && !kept.count(v))
+      throw std::runtime_error("effect of " + where + ": " + v + " is neither assigned nor UNCHANGED");
+  c.emit(E_END);
+  check_depth(c.code, "effect of " + where);
   return c.code;
 }
 

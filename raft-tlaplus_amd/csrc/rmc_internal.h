@@ -59,6 +59,9 @@ struct rmc_model {
   // guards compiled onto library effects (rmc_guard.cpp)
   std::map<std::string, long long> int_consts;
   std::vector<rmc::tla::GuardSrc> guard_srcs;
+  // actions defined as TLA+ text (rmc_model_define_action), by name: compiled
+  // whole when rmc_model_set_next puts them in Next
+  std::map<std::string, rmc::tla::GuardSrc> defined_actions;
   // the last check's row widenings (depth, first parent of the redone chunk, new message slots)
   std::vector<std::array<unsigned long long, 3>> widenings;
 };

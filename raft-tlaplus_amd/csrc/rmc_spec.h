@@ -70,8 +70,12 @@ enum ActId {
   // the network actions every module defines but leaves out of Next (Raft.tla:509-522, :540-541):
   // DuplicateMessage(m) / DropMessage(m), bound by \E m \in DOMAIN messages (the TLA+ front end
   // lowers them when a module's Next re-enables them; rmc_tla.cpp)
-  A_DUP, A_DROP, A_NUM
+  A_DUP, A_DROP,
+  // actions the TLA+ front end compiles whole (guard and effect, rmc_guard.cpp
+  // compile_effect): Model::gstart / estart hold their programs
+  A_C0, A_C1, A_C2, A_C3, A_NUM
 };
+constexpr int MAXCOMPILED = 4;
 // binding forms: \E i \in Server (K_I), i \in Server, v \in Value (K_IV), i, j \in Server (K_IJ), a message
 // handler ranging over DOMAIN messages with one enabled action per element (K_MSG), and an action bound
 // by \E m \in DOMAIN messages that is NOT exclusive with the handlers (K_M: its bindings are fixed
@@ -120,7 +124,10 @@ struct Model {
   // guard runs the library effect unguarded, behind this program.  gstart[a]
   // = first word of action id a's program in gcode, -1 = the library guard.
   int16_t gstart[A_NUM];
-  int gany;  // some action has a compiled guard
+  // Compiled effects (rmc_guard.cpp compile_effect): estart[k] = first word of
+  // action A_C0 + k's effect program in gcode (its guard is at gstart[A_C0 + k])
+  int16_t estart[MAXCOMPILED];
+  int gany;  // some action has a compiled guard (or is compiled whole)
   uint32_t gcode[MAXGCODE];
 };
 
@@ -1004,6 +1011,25 @@ enum GOp : uint32_t {
   G_JMP,       // jump imm
   G_POP,
   G_ERR,       // evaluation error
+  // effect programs only (effect_vm): store the top of the stack into the
+  // successor -- server i's (the action's first bound variable) fields, the
+  // header's counters and acked, a log entry appended to log[i], a
+  // RequestVoteRequest sent as SendMultipleOnce sends each of its messages
+  E_ST,        // x ->   state[i]' = x
+  E_TERM,      // x ->   currentTerm[i]' = x            (> 15: capacity)
+  E_VOTED,     // x ->   votedFor[i]' = x               (Nil = 7)
+  E_VOTES,     // S ->   votesGranted[i]' = S
+  E_COMMIT,    // x ->   commitIndex[i]' = x            (> 7: capacity)
+  E_ECTR,      // x ->   electionCtr' = x
+  E_RCTR,      // x ->   restartCtr' = x
+  E_ACKED,     // v c -> acked[v]' = c                  (0 Nil, 1 FALSE, 2 TRUE)
+  E_APPEND,    // t v -> log[i]' = Append(log[i], [term |-> t, value |-> v])
+  E_NEXT,      // j x -> nextIndex[i][j]' = x           (> 7: capacity)
+  E_MATCH,     // j x -> matchIndex[i][j]' = x          (> 7: capacity)
+  E_PEND,      // j b -> pendingResponse[i][j]' = b
+  E_RVREQ,     // term llt lli src dst -> the RequestVoteRequest record, sent new (imm 0: disabled if in
+               // DOMAIN) or counted (imm 1: _SendNoRestriction)
+  E_END,       // the successor is complete
   G_NUM
 };
 RMC_HD uint32_t g_ins(uint32_t op, int imm = 0) { return op | ((uint32_t)imm << 8); }
@@ -1012,10 +1038,22 @@ RMC_HD uint32_t g_ins(uint32_t op, int imm = 0) { return op | ((uint32_t)imm << 
 // every kernel that can reach it save its live registers around it: the
 // kernels' register budgets are set for the library actions).  The compiler
 // refuses a guard deeper than that (rmc_guard.cpp).
-template <int SPEC, int N>
-RMC_HD int guard_vm(const uint32_t* S, const Model& M, int pc, int i, int jv) {
+// EFF: an effect program (effect_vm): the same expression machine, reading the
+// parent state, plus the E_* stores into the successor d (server i's words,
+// the header, the message ops).  Returns 1 (enabled; d complete at E_END),
+// 0 (disabled: a SendMultipleOnce message already in DOMAIN) or -1 (a TLC
+// evaluation error); a value past the packed layout's field sets d.err.
+template <int SPEC, int N, bool EFF>
+RMC_HD int vm_run(const uint32_t* S, const Model& M, int pc, int i, int jv, Delta& d) {
   int t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0, t6 = 0, t7 = 0;
   const PState<SPEC, N> s{S};
+  uint32_t ea = 0, eb = 0, eh = 0;  // effects: server i's words A and B, the header
+  if constexpr (EFF) {
+    begin_srv(s, d, i);
+    ea = d.w[0];
+    eb = d.w[1];
+    eh = s.hdr();
+  }
 #define GPUSH(x) do { const int x_ = (x); t7 = t6; t6 = t5; t5 = t4; t4 = t3; t3 = t2; t2 = t1; t1 = t0; t0 = x_; } while (0)
 #define GPOP() do { t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = t5; t5 = t6; t6 = t7; } while (0)
 #define GBIN(e) do { const int a_ = t1, b_ = t0; GPOP(); t0 = (e); } while (0)
@@ -1069,13 +1107,87 @@ RMC_HD int guard_vm(const uint32_t* S, const Model& M, int pc, int i, int jv) {
       case G_JNZ: { const int c_ = t0; GPOP(); if (c_) pc += imm; break; }
       case G_JMP: pc += imm; break;
       case G_POP: GPOP(); break;
-      default: return -1;  // G_ERR
+      default:
+        if constexpr (EFF) {
+          switch (op) {
+            case E_ST: ea = setb(ea, 4, 2, (uint32_t)t0); GPOP(); break;
+            case E_TERM:
+              if (t0 < 0 || t0 > 15) { d.err = E_CAP_TERM; return 1; }
+              ea = setb(ea, 0, 4, (uint32_t)t0);
+              GPOP();
+              break;
+            case E_VOTED: ea = setb(ea, 6, 3, (uint32_t)t0 & 7u); GPOP(); break;
+            case E_VOTES: ea = setb(ea, 18, 7, (uint32_t)t0); GPOP(); break;
+            case E_COMMIT:
+              if (t0 < 0 || t0 > 7) { d.err = E_CAP_FIELD; return 1; }
+              ea = setb(ea, 12, 3, (uint32_t)t0);
+              GPOP();
+              break;
+            case E_ECTR:
+            case E_RCTR:
+              if (t0 < 0 || t0 > 15) { d.err = E_CAP_FIELD; return 1; }
+              eh = setb(eh, op == E_ECTR ? 8 : 12, 4, (uint32_t)t0);
+              GPOP();
+              break;
+            case E_ACKED: eh = setb(eh, 16 + 2 * (t1 & 3), 2, (uint32_t)t0 & 3u); GPOP(); GPOP(); break;
+            case E_NEXT:
+            case E_MATCH:
+              if (t0 < 0 || t0 > 7) { d.err = E_CAP_FIELD; return 1; }
+              if (op == E_NEXT) d.w[2] = row_set(d.w[2], t1 & 7, t0);
+              else d.w[3] = row_set(d.w[3], t1 & 7, t0);
+              GPOP();
+              GPOP();
+              break;
+            case E_PEND: ea = setb(ea, 25 + (t1 & 7), 1, (uint32_t)t0 & 1u); GPOP(); GPOP(); break;
+            case E_APPEND: {
+              if (t1 < 0 || t1 > 15) { d.err = E_CAP_TERM; return 1; }
+              int err = 0;
+              log_append(ea, eb, t1, t0 & 3, err);
+              if (err) { d.err = err; return 1; }
+              GPOP();
+              GPOP();
+              break;
+            }
+            case E_RVREQ: {  // stack: term llt lli src dst (dst on top)
+              MsgF m = msg_zero();
+              m.type = RVREQ; m.term = t4; m.llt = t3; m.lli = t2; m.src = t1 & 7; m.dst = t0 & 7; m.count = 1;
+              if (t4 < 0 || t4 > 15) { d.err = E_CAP_TERM; return 1; }
+              if (t3 < 0 || t3 > 15 || t2 < 0 || t2 > 7) { d.err = E_CAP_FIELD; return 1; }
+              GPOP(); GPOP(); GPOP(); GPOP(); GPOP();
+              if (imm) {
+                op_send_any(s, d, msg_encode<SPEC>(m));
+                if (d.err) return 1;
+              } else if (!op_send_once(s, d, msg_encode<SPEC>(m))) {
+                return 0;  // already in DOMAIN: the action is disabled
+              }
+              break;
+            }
+            case E_END:
+              d.w[0] = ea;
+              d.w[1] = eb;
+              d.hdr = eh;
+              return 1;
+            default: return -1;
+          }
+          break;
+        } else {
+          return -1;  // G_ERR
+        }
     }
   }
 #undef GPUSH
 #undef GPOP
 #undef GBIN
   return -1;
+}
+template <int SPEC, int N>
+RMC_HD int guard_vm(const uint32_t* S, const Model& M, int pc, int i, int jv) {
+  Delta unused;
+  return vm_run<SPEC, N, false>(S, M, pc, i, jv, unused);
+}
+template <int SPEC, int N>
+RMC_HD int effect_vm(const PState<SPEC, N>& s, const Model& M, int pc, int i, int jv, Delta& d) {
+  return vm_run<SPEC, N, true>(s.S, M, pc, i, jv, d);
 }
 
 template <int SPEC, int N>
@@ -1533,6 +1645,17 @@ RMC_HD bool eval_fixed_id(const PState<SPEC, N>& s, const Model& M, int act, int
     push_op(d, k, w + 1u);
     return true;
   }
+  if constexpr (G) {
+    if (act >= A_C0) {  // compiled whole by the front end (rmc_guard.cpp): its guard, then its effect
+      const int g = guard_vm<SPEC, N>(s.S, M, M.gstart[act], i, jv);
+      if (g < 0) { d.err = E_DOMAIN; return true; }
+      if (!g) return false;
+      const int e = effect_vm<SPEC, N>(s, M, M.estart[act - A_C0], i, jv, d);
+      if (e < 0) { d.err = E_DOMAIN; return true; }
+      return e != 0;
+    }
+  }
+  if (act >= A_C0) return false;  // (never: a model with compiled actions runs the G instantiation)
   if (SPEC == KRAFT) return kr_fixed(s, M, act, i, jv, d);
   bool ug = false;
   if constexpr (G) {

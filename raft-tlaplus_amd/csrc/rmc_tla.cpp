@@ -740,10 +740,14 @@ struct Hasher {
   // the module whose body does (Send, Reply, ...)?  Bound names shadow
   // definitions.
   std::map<std::string, bool> eff_memo;
+  // operators that change the state although the text does not define them
+  // (parse_action: the family's send helpers, restated by the effect compiler)
+  std::set<std::string> effect_ops;
   bool has_effect(const NodeP& n, std::set<std::string>& bound) {
     if (!n) return false;
     if (n->kind == N_PRIME) return true;
     if (n->kind == N_UNARY && n->s == "UNCHANGED") return true;
+    if ((n->kind == N_ID || n->kind == N_APP) && effect_ops.count(n->s) && !bound.count(n->s)) return true;
     if ((n->kind == N_ID || n->kind == N_APP) && !bound.count(n->s)) {
       const Def* d = m.find(n->s);
       if (d && !is_declared(n->s)) {
@@ -797,9 +801,11 @@ struct Hasher {
   // Hash of an action's EFFECT: its effect conjuncts in order, parameters
   // bound by position as in def_hash.  Two actions with equal effect hashes
   // differ at most in their guards.
-  bool effect_hash(const std::string& name, uint64_t& out, std::vector<NodeP>* guards_out = nullptr) {
+  bool effect_hash(const std::string& name, uint64_t& out, std::vector<NodeP>* guards_out = nullptr,
+                   std::vector<NodeP>* effects_out = nullptr) {
     std::vector<NodeP> g, e;
     if (!split(name, g, e)) return false;
+    if (effects_out) *effects_out = e;
     const Def* d = m.find(name);
     std::vector<Ent> save;
     save.swap(env);
@@ -957,7 +963,7 @@ std::vector<Disjunct> next_disjuncts(const Module& m, const std::string& next) {
 
 // ------------------------------------------------------------------ lowering
 namespace {
-enum Role { R_INIT = 0, R_ACTION = 1, R_INV = 2, R_VIEW = 3, R_SYMM = 4, R_VARS = 5, R_EFFECT = 6 };
+enum Role { R_INIT = 0, R_ACTION = 1, R_INV = 2, R_VIEW = 3, R_SYMM = 4, R_VARS = 5, R_EFFECT = 6, R_HELPER = 7 };
 struct Known {
   int spec, role, id, kind;
   unsigned long long hash;
@@ -1113,12 +1119,52 @@ Lowering lower(const std::string& text, const std::string& next, const std::stri
         L.guards.push_back(gs);
       }
     }
+    if (!k && (L.spec == RAFT || L.spec == FLEX || L.spec == FSYNC) &&
+        (dj.form == B_I || dj.form == B_IJ || dj.form == B_IV)) {
+      // compiled whole: its guard and its effect (rmc_guard.cpp compile_effect)
+      uint64_t eh = 0;
+      std::vector<NodeP> g, e;
+      if (H.effect_hash(dj.op, eh, &g, &e)) {
+        int ncomp = 0;
+        for (const GuardSrc& q : L.guards) ncomp += q.act >= A_C0;
+        if (ncomp >= MAXCOMPILED)
+          throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + "): more than " +
+                                   std::to_string(MAXCOMPILED) + " actions to compile");
+        // the bag helpers an effect calls must be the family's own (by closure hash)
+        std::map<std::string, int> helpers;
+        for (const NodeP& c : e)
+          if (c->kind == N_APP && m.find(c->s)) {
+            const Known* hk = nullptr;
+            const uint64_t hh = hash_of(c->s);
+            for (const Known& q : kKnown)
+              if (q.spec == L.spec && q.role == R_HELPER && q.hash == hh && c->s == q.name) hk = &q;
+            if (!hk)
+              throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") calls " + c->s +
+                                       ", which is not one of the " + spec_name(L.spec) + " module's own bag helpers");
+            helpers[c->s] = hk->id;
+          }
+        GuardSrc gs;
+        gs.send_helpers = helpers;
+        gs.act = A_C0 + ncomp;
+        gs.op = dj.op;
+        gs.params = m.find(dj.op)->params;
+        gs.conjuncts = g;
+        gs.effects = e;
+        gs.kind = dj.form == B_I ? K_I : dj.form == B_IJ ? K_IJ : K_IV;
+        gs.mod = mp;
+        L.guards.push_back(gs);
+        L.actions.push_back({gs.act, gs.kind});
+        L.labels.push_back(dj.op);
+        continue;
+      }
+    }
     if (!k)
       throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") computes an action "
                                "the " + spec_name(L.spec) + " lowering does not have (its definition differs from "
                                "every lowered action of the spec family, and its effect -- the conjuncts that change "
-                               "the state -- from every effect whose guard the front end compiles); adding it needs a "
-                               "lowering in rmc_spec.h");
+                               "the state -- from every effect whose guard the front end compiles, and it is not a "
+                               "fixed-binding action of the Raft / FlexibleRaft / RaftFsync families the effect "
+                               "compiler takes); adding it needs a lowering in rmc_spec.h");
     static const int form_of_kind[] = {B_I, B_IV, B_IJ, B_MSG, B_M};
     if (form_of_kind[k->kind] != dj.form)
       throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) +
@@ -1144,6 +1190,56 @@ Lowering lower(const std::string& text, const std::string& next, const std::stri
     L.symmetry_ok = true;
   }
   return L;
+}
+
+GuardSrc parse_action(int spec, const std::string& op, int kind, const std::vector<std::string>& params,
+                      const std::string& body) {
+  // the family's state (Raft.tla:58-107, FlexibleRaft.tla:63-109, RaftFsync.tla:62-110), restated
+  std::string vars = "messages, acked, electionCtr, restartCtr, currentTerm, state, votedFor, log, commitIndex, "
+                     "votesGranted, nextIndex, matchIndex";
+  std::string leader = "<<nextIndex, matchIndex>>", logv = "<<log, commitIndex>>";
+  std::map<std::string, int> helpers;
+  if (spec == RAFT) {
+    vars += ", pendingResponse";
+    leader = "<<nextIndex, matchIndex, pendingResponse>>";
+    helpers = {{"SendMultipleOnce", 0}, {"_SendOnce", 1}, {"Send", 2}, {"_SendNoRestriction", 2}};
+  } else if (spec == FLEX) {
+    helpers = {{"SendMultiple", 0}, {"Send", 1}};
+  } else if (spec == FSYNC) {
+    vars += ", fsyncIndex";
+    logv = "<<log, commitIndex, fsyncIndex>>";
+    helpers = {{"Send", 1}};
+  } else {
+    throw std::runtime_error("actions compiled whole are offered for Raft, FlexibleRaft and RaftFsync");
+  }
+  std::string ps;
+  for (size_t q = 0; q < params.size(); q++) ps += (q ? ", " : "") + params[q];
+  const std::string text = "---- MODULE ActionText ----\n"
+                           "VARIABLES " + vars + "\n"
+                           "auxVars == <<acked, electionCtr, restartCtr>>\n"
+                           "serverVars == <<currentTerm, state, votedFor>>\n"
+                           "candidateVars == <<votesGranted>>\n"
+                           "leaderVars == " + leader + "\n"
+                           "logVars == " + logv + "\n"
+                           "Quorum == {i \\in SUBSET(Server) : Cardinality(i) * 2 > Cardinality(Server)}\n"
+                           "LastTerm(xlog) == IF Len(xlog) = 0 THEN 0 ELSE xlog[Len(xlog)].term\n" +
+                           op + (params.empty() ? "" : "(" + ps + ")") + " ==\n    " + body + "\n====\n";
+  auto mod = std::make_shared<Module>(parse_module(text));
+  const Def* d = mod->find(op);
+  if (!d) throw ParseError("action text did not parse");
+  if (!d->error.empty()) throw ParseError("action text: " + d->error);
+  Hasher H(*mod);
+  GuardSrc g;
+  g.act = -1;
+  g.op = op;
+  g.params = params;
+  g.kind = kind;
+  g.mod = mod;
+  g.send_helpers = helpers;
+  // the send helpers are not defined in the text: mark them as effects for the split
+  for (auto& h : helpers) H.effect_ops.insert(h.first);
+  if (!H.split(op, g.conjuncts, g.effects)) throw std::runtime_error("action " + op + " changes nothing");
+  return g;
 }
 
 GuardSrc parse_guard(int spec, int act, const std::string& op, const std::vector<std::string>& params,

@@ -57,7 +57,7 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
            "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm",
            "rmc_abi_layout", "rmc_abi_version", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes",
-           "rmc_model_set_guard", "rmc_source_id"]
+           "rmc_model_set_guard", "rmc_source_id", "rmc_model_define_action"]
 
 # the rmc_options / rmc_result layout these ctypes mirrors follow (include/rmc.h RMC_ABI_VERSION)
 ABI_VERSION = 2
@@ -116,6 +116,7 @@ def lib():
                       % (LIB_PATH, stale))
     L.rmc_model_set_next.argtypes = [P, ctypes.c_char_p]
     L.rmc_model_set_guard.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    L.rmc_model_define_action.argtypes = [P, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p]
     L.rmc_model_next.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_tla_hashes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_size_t]
     L.rmc_comm_unique_id.argtypes = [ctypes.c_char_p]
@@ -231,6 +232,17 @@ class Model:
         if isinstance(params, (list, tuple)):
             params = ", ".join(params)
         if lib().rmc_model_set_guard(self._h, action.encode(), params.encode(), expr.encode()) != 0:
+            raise RaftmcError(lib().rmc_last_error().decode())
+
+    def define_action(self, name, form, params, body):
+        """Define an action by its TLA+ text for set_next to use by name
+        (rmc_model_define_action: compiled whole, guard and effect,
+        rmc_guard.cpp compile_effect).  form: "i", "iv" or "ij" (the binding
+        \\E i \\in Server / i \\in Server, v \\in Value / i, j \\in Server)."""
+        f = {"i": 0, "iv": 1, "ij": 2}[form] if isinstance(form, str) else int(form)
+        if isinstance(params, (list, tuple)):
+            params = ", ".join(params)
+        if lib().rmc_model_define_action(self._h, name.encode(), f, params.encode(), body.encode()) != 0:
             raise RaftmcError(lib().rmc_last_error().decode())
 
     def next(self):

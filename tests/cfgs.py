@@ -281,3 +281,100 @@ GUARDS = [
     ("pull2_restart_emptylog_n2v1e2r1", "PullRaftVariant2", dict(n=2, v=1, E=2, R=1),
      [("Restart", "i", "restartCtr < MaxRestarts /\\ Len(log[i]) = 0")], 0),
 ]
+
+
+# (name, module, kwargs, Next (names), [(action, form, params, TLA+ body)],
+# max_depth): actions the TLA+ front end compiles whole -- guard AND effect
+# (rmc_guard.cpp compile_effect) -- given as TLA+ text (rmc_model_define_action
+# is the table a module with such a Next disjunct lowers to).  The Python side
+# of each action is make_golden._effect_py()[name].
+_RV_BODY = """/\\ electionCtr < MaxElections
+    /\\ state[i] \\in {Follower, Candidate}
+    /\\ state' = [state EXCEPT ![i] = Candidate]
+    /\\ currentTerm' = [currentTerm EXCEPT ![i] = currentTerm[i] + 1]
+    /\\ votedFor' = [votedFor EXCEPT ![i] = Nil]
+    /\\ votesGranted' = [votesGranted EXCEPT ![i] = {}]
+    /\\ electionCtr' = electionCtr + 1
+    /\\ %s({[mtype |-> RequestVoteRequest, mterm |-> currentTerm[i] + 1, mlastLogTerm |-> LastTerm(log[i]),
+          mlastLogIndex |-> Len(log[i]), msource |-> i, mdest |-> j] : j \\in Server \\ {i}})
+    /\\ UNCHANGED <<acked, leaderVars, logVars, restartCtr>>"""
+EFFECTS = [
+    # Raft.tla:242-257 RequestVote whose candidate does not vote for itself
+    ("raft_rv_noself_n3v1e2", "Raft", dict(n=3, v=1, E=2),
+     ("Restart", "RequestVoteNoSelf") + NEXT_RAFT[2:],
+     [("RequestVoteNoSelf", "i", "i", _RV_BODY % "SendMultipleOnce")], 0),
+    # RequestVote that moves two terms on but asks for votes at the next term, with @ in the EXCEPTs
+    ("raft_rv_term2_n2v1e2", "Raft", dict(n=2, v=1, E=2),
+     ("Restart", "RequestVoteTwo") + NEXT_RAFT[2:],
+     [("RequestVoteTwo", "i", "i", """/\\ electionCtr < MaxElections
+    /\\ state[i] \\in {Follower, Candidate}
+    /\\ state' = [state EXCEPT ![i] = Candidate]
+    /\\ currentTerm' = [currentTerm EXCEPT ![i] = @ + 2]
+    /\\ votedFor' = [votedFor EXCEPT ![i] = i]
+    /\\ votesGranted' = [votesGranted EXCEPT ![i] = {i}]
+    /\\ electionCtr' = electionCtr + 1
+    /\\ SendMultipleOnce({[mtype |-> RequestVoteRequest, mterm |-> currentTerm[i] + 1, mlastLogTerm |-> LastTerm(log[i]),
+          mlastLogIndex |-> Len(log[i]), msource |-> i, mdest |-> j] : j \\in Server \\ {i}})
+    /\\ UNCHANGED <<acked, leaderVars, logVars, restartCtr>>""")], 0),
+    # Raft.tla:304-313 ClientRequest that acks the value at once: LeaderHasAllAckedValues breaks
+    ("raft_client_eager_n3v1e2", "Raft", dict(n=3, v=1, E=2),
+     NEXT_RAFT[:3] + ("ClientRequestEager",) + NEXT_RAFT[4:],
+     [("ClientRequestEager", "iv", "i, v", """/\\ state[i] = Leader
+    /\\ acked[v] = Nil
+    /\\ log' = [log EXCEPT ![i] = Append(@, [term |-> currentTerm[i], value |-> v])]
+    /\\ acked' = [acked EXCEPT ![v] = TRUE]
+    /\\ UNCHANGED <<messages, serverVars, candidateVars, leaderVars, commitIndex, electionCtr, restartCtr>>""")], 0),
+    # Raft.tla:226-235 Restart that keeps the leader's rows and its commitIndex at 0
+    ("raft_restart_keep_n2v1e2r1", "Raft", dict(n=2, v=1, E=2, R=1),
+     ("RestartKeep",) + NEXT_RAFT[1:],
+     [("RestartKeep", "i", "i", """/\\ restartCtr < MaxRestarts
+    /\\ state' = [state EXCEPT ![i] = Follower]
+    /\\ votesGranted' = [votesGranted EXCEPT ![i] = {}]
+    /\\ commitIndex' = [commitIndex EXCEPT ![i] = 0]
+    /\\ restartCtr' = restartCtr + 1
+    /\\ UNCHANGED <<messages, currentTerm, votedFor, leaderVars, log, acked, electionCtr>>""")], 0),
+    # Raft: a candidate re-sends its vote request (Send: _SendNoRestriction, count + 1); depth-bounded
+    # below the 3-bit message count's cap (7)
+    ("raft_resend_rv_n2v1e1", "Raft", dict(n=2, v=1, E=1),
+     NEXT_RAFT + ("ResendVote",),
+     [("ResendVote", "ij", "i, j", """/\\ state[i] = Candidate
+    /\\ i /= j
+    /\\ Send([mtype |-> RequestVoteRequest, mterm |-> currentTerm[i], mlastLogTerm |-> LastTerm(log[i]),
+             mlastLogIndex |-> Len(log[i]), msource |-> i, mdest |-> j])
+    /\\ UNCHANGED <<serverVars, candidateVars, leaderVars, logVars, auxVars>>""")], 8),
+    # RaftFsync.tla:234-243 RequestVote(i, j) that claims an empty log
+    ("fsync_rvij_empty_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1),
+     NEXT_FSYNC[:2] + ("RequestVoteEmpty",) + NEXT_FSYNC[3:],
+     [("RequestVoteEmpty", "ij", "i, j", """/\\ state[i] = Candidate
+    /\\ i # j
+    /\\ Send([mtype |-> RequestVoteRequest, mterm |-> currentTerm[i], mlastLogTerm |-> 0,
+             mlastLogIndex |-> 0, msource |-> i, mdest |-> j])
+    /\\ UNCHANGED <<serverVars, candidateVars, leaderVars, logVars, auxVars>>""")], 0),
+    # Raft.tla:226-235 Restart counting two restarts (its leader rows reset as the reference's)
+    ("raft_restart_two_n2v1e2r3", "Raft", dict(n=2, v=1, E=2, R=3),
+     ("RestartTwo",) + NEXT_RAFT[1:],
+     [("RestartTwo", "i", "i", """/\\ restartCtr < MaxRestarts
+    /\\ state'           = [state EXCEPT ![i] = Follower]
+    /\\ votesGranted'    = [votesGranted EXCEPT ![i] = {}]
+    /\\ nextIndex'       = [nextIndex EXCEPT ![i] = [j \\in Server |-> 1]]
+    /\\ matchIndex'      = [matchIndex EXCEPT ![i] = [j \\in Server |-> 0]]
+    /\\ pendingResponse' = [pendingResponse EXCEPT ![i] = [j \\in Server |-> FALSE]]
+    /\\ commitIndex'     = [commitIndex EXCEPT ![i] = 0]
+    /\\ restartCtr'      = restartCtr + 2
+    /\\ UNCHANGED <<messages, currentTerm, votedFor, log, acked, electionCtr>>""")], 0),
+    # Raft.tla:289-300 BecomeLeader that starts every follower's nextIndex at 1 and marks its own
+    # pendingResponse[i][i]
+    ("raft_bl_next1_n2v1e2", "Raft", dict(n=2, v=1, E=2),
+     NEXT_RAFT[:2] + ("BecomeLeaderNext1",) + NEXT_RAFT[3:],
+     [("BecomeLeaderNext1", "i", "i", """/\\ state[i] = Candidate
+    /\\ votesGranted[i] \\in Quorum
+    /\\ state'      = [state EXCEPT ![i] = Leader]
+    /\\ nextIndex'  = [nextIndex EXCEPT ![i] = [j \\in Server |-> 1]]
+    /\\ matchIndex' = [matchIndex EXCEPT ![i] = [j \\in Server |-> IF j = i THEN Len(log[i]) ELSE 0]]
+    /\\ pendingResponse' = [pendingResponse EXCEPT ![i][i] = TRUE]
+    /\\ UNCHANGED <<messages, currentTerm, votedFor, candidateVars, auxVars, logVars>>""")], 0),
+    # FlexibleRaft.tla:215-230 RequestVote without the self vote (SendMultiple)
+    ("flex_rv_noself_n3v1e1", "FlexibleRaft", dict(n=3, v=1, E=1, ElectionQuorumSize=2, ReplicationQuorumSize=2),
+     ("Restart", "RequestVoteNoSelf") + NEXT_RAFT[2:],
+     [("RequestVoteNoSelf", "i", "i", _RV_BODY % "SendMultiple")], 0),
+]

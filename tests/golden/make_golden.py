@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import (EXTRAS, FLEX_RESTART, FRONTEND, GUARDS, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
+from cfgs import (EFFECTS, EXTRAS, FLEX_RESTART, FRONTEND, GUARDS, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
                   VARIANT2_N5, VARIANT2_SMALL, cfg_text)
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
@@ -321,7 +321,132 @@ def guards():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def _effect_py():
+    """The Python side of every cfgs.EFFECTS action (written here by hand from
+    each TLA+ body): {case: {name: (form, f(spec, s, *args))}}."""
+    from oracle.pyoracle.raft import CANDIDATE, FOLLOWER, LEADER, RVREQ
+    from oracle.pyoracle.tlc import NIL, Rec, fset
+
+    def rv(spec, s, i, self_vote, step, mstep=None):
+        # RequestVote (Raft.tla:242-257) with the self vote optional, a term step
+        # and the requests' term step
+        if not (s["electionCtr"] < spec.MaxElections and s["state"][i] in (FOLLOWER, CANDIDATE)):
+            return
+        term = s["currentTerm"][i] + step
+        ms = [Rec(mtype=RVREQ, mterm=s["currentTerm"][i] + (step if mstep is None else mstep), mlastLogTerm=spec.LastTerm(s["log"][i]), mlastLogIndex=len(s["log"][i]),
+                  msource=i, mdest=j) for j in spec.Server if j != i]
+        msgs = spec.SendMultipleOnce(s["messages"], ms)
+        if msgs is None:
+            return
+        t = dict(s)
+        t["state"] = fset(s["state"], i, CANDIDATE)
+        t["currentTerm"] = fset(s["currentTerm"], i, term)
+        t["votedFor"] = fset(s["votedFor"], i, i if self_vote else NIL)
+        t["votesGranted"] = fset(s["votesGranted"], i, frozenset([i]) if self_vote else frozenset())
+        t["electionCtr"] = s["electionCtr"] + 1
+        t["messages"] = msgs
+        yield t
+
+    def client_eager(spec, s, i, v):
+        if not (s["state"][i] == LEADER and s["acked"][v] == NIL):
+            return
+        t = dict(s)
+        t["log"] = fset(s["log"], i, s["log"][i] + (Rec(term=s["currentTerm"][i], value=v),))
+        t["acked"] = fset(s["acked"], v, True)
+        yield t
+
+    def restart_keep(spec, s, i):
+        if not s["restartCtr"] < spec.MaxRestarts:
+            return
+        t = dict(s)
+        t["state"] = fset(s["state"], i, FOLLOWER)
+        t["votesGranted"] = fset(s["votesGranted"], i, frozenset())
+        t["commitIndex"] = fset(s["commitIndex"], i, 0)
+        t["restartCtr"] = s["restartCtr"] + 1
+        yield t
+
+    def resend(spec, s, i, j, empty):
+        # one RequestVoteRequest by the family's Send (Raft: count + 1; RaftFsync: once)
+        if not (s["state"][i] == CANDIDATE and i != j):
+            return
+        m = Rec(mtype=RVREQ, mterm=s["currentTerm"][i], mlastLogTerm=0 if empty else spec.LastTerm(s["log"][i]),
+                mlastLogIndex=0 if empty else len(s["log"][i]), msource=i, mdest=j)
+        msgs = spec.Send(s["messages"], m)
+        if msgs is None:
+            return
+        t = dict(s)
+        t["messages"] = msgs
+        yield t
+
+    def restart_two(spec, s, i):
+        if not s["restartCtr"] < spec.MaxRestarts:
+            return
+        N = spec.N
+        t = dict(s)
+        t["state"] = fset(s["state"], i, FOLLOWER)
+        t["votesGranted"] = fset(s["votesGranted"], i, frozenset())
+        t["nextIndex"] = fset(s["nextIndex"], i, tuple(1 for _ in range(N)))
+        t["matchIndex"] = fset(s["matchIndex"], i, tuple(0 for _ in range(N)))
+        t["pendingResponse"] = fset(s["pendingResponse"], i, tuple(False for _ in range(N)))
+        t["commitIndex"] = fset(s["commitIndex"], i, 0)
+        t["restartCtr"] = s["restartCtr"] + 2
+        yield t
+
+    def bl_next1(spec, s, i):
+        if not (s["state"][i] == CANDIDATE and spec.IsQuorum(s["votesGranted"][i])):
+            return
+        N = spec.N
+        t = dict(s)
+        t["state"] = fset(s["state"], i, LEADER)
+        t["nextIndex"] = fset(s["nextIndex"], i, tuple(1 for _ in range(N)))
+        t["matchIndex"] = fset(s["matchIndex"], i, tuple(len(s["log"][i]) if j == i else 0 for j in range(N)))
+        row = list(s["pendingResponse"][i])
+        row[i] = True
+        t["pendingResponse"] = fset(s["pendingResponse"], i, tuple(row))
+        yield t
+
+    return {
+        "raft_restart_two_n2v1e2r3": {"RestartTwo": ("i", restart_two)},
+        "raft_bl_next1_n2v1e2": {"BecomeLeaderNext1": ("i", bl_next1)},
+        "raft_rv_noself_n3v1e2": {"RequestVoteNoSelf": ("i", lambda sp, s, i: rv(sp, s, i, False, 1))},
+        "raft_rv_term2_n2v1e2": {"RequestVoteTwo": ("i", lambda sp, s, i: rv(sp, s, i, True, 2, 1))},
+        "raft_client_eager_n3v1e2": {"ClientRequestEager": ("iv", client_eager)},
+        "raft_restart_keep_n2v1e2r1": {"RestartKeep": ("i", restart_keep)},
+        "raft_resend_rv_n2v1e1": {"ResendVote": ("ij", lambda sp, s, i, j: resend(sp, s, i, j, False))},
+        "fsync_rvij_empty_n2v1e2r1": {"RequestVoteEmpty": ("ij", lambda sp, s, i, j: resend(sp, s, i, j, True))},
+        "flex_rv_noself_n3v1e1": {"RequestVoteNoSelf": ("i", lambda sp, s, i: rv(sp, s, i, False, 1))},
+    }
+
+
+def effects():
+    """--effects: Next with actions the front end compiles whole (cfgs.EFFECTS),
+    by the Python oracle with the same actions written in Python (_effect_py).
+    The C oracle has no configurable actions, so these are pinned by the Python
+    oracle alone."""
+    py = _effect_py()
+    path = os.path.join(HERE, "effects.json")
+    only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--only=")]
+    out = json.load(open(path)) if only and os.path.exists(path) else {}
+    for name, module, kw, nxt, acts, md in EFFECTS:
+        if only and name not in only[0]:
+            continue
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        p = bfs(make_spec(module, cfg, next_order=nxt, defined=py[name]), max_depth=md or None)
+        out[name] = dict(module=module, cfg=txt, next=list(nxt), actions=[list(a) for a in acts], max_depth=md,
+                         generated=p.generated, distinct=p.distinct, depth=p.depth, status=p.status,
+                         violated=getattr(p, "violated", None), levels=[list(x) for x in p.levels],
+                         hidden_same_level=p.hidden_same_level, max_msgs=p.max_msgs, pinned_by="pyoracle")
+        print(name, p.generated, p.distinct, p.depth, p.status, getattr(p, "violated", None), p.hidden_same_level,
+              "%.1fs" % p.seconds, flush=True)
+    out = {k: v for k, v in out.items() if k in {e[0] for e in EFFECTS}}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--effects" in sys.argv:
+        return effects()
     if "--guards" in sys.argv:
         return guards()
     if "--frontend" in sys.argv:

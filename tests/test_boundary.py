@@ -41,19 +41,31 @@ def test_reference_cfg_same_first_levels(name):
     assert r["levels"] == g["levels"][:14]
 
 
-def test_edited_spec_is_refused(tmp_path):
+def test_edited_spec_is_not_checked_as_the_built_in_one(tmp_path):
     """Raft with an action whose EFFECT computes something else (Restart
-    counting two restarts, Raft.tla:234) is a different spec: refused with a
-    message naming the action, not checked as the built-in one.  (An edited
-    GUARD -- Restart on restartCtr <= MaxRestarts, Raft.tla:227 -- is compiled
-    instead: tests/test_guards.py; re-enabling the commented-out
-    DuplicateMessage disjunct, Raft.tla:540, is lowered: tests/test_frontend.py.)"""
+    counting two restarts, Raft.tla:234) is a different spec: never checked
+    as the built-in one.  The front end compiles that action whole
+    (rmc_guard.cpp compile_effect; its counts against the Python oracle:
+    tests/test_effects.py), and an effect it cannot compile -- here an
+    AppendEntries request sent by Restart -- is refused naming the action.
+    (An edited GUARD is compiled behind the library's effect:
+    tests/test_guards.py; re-enabling the commented-out DuplicateMessage
+    disjunct, Raft.tla:540, is lowered: tests/test_frontend.py.)"""
     txt = open(ref("Raft", ".tla")).read()
     edited = txt.replace("    /\\ restartCtr'      = restartCtr + 1\n", "    /\\ restartCtr'      = restartCtr + 2\n")
     assert edited != txt
     p = tmp_path / "Raft.tla"
     p.write_text(edited)
-    with pytest.raises(raftmc.RaftmcError, match="Next disjunct Restart"):
+    m = raftmc.Model(str(p), ref("Raft", ".cfg"))
+    builtin = raftmc.Model(module="Raft", cfg_path=ref("Raft", ".cfg"))
+    assert m.next() == builtin.next()  # the module's own names; Restart now compiled whole
+    bad = txt.replace("    /\\ restartCtr'      = restartCtr + 1\n",
+                      "    /\\ restartCtr'      = restartCtr + 1\n    /\\ Send([mtype |-> AppendEntriesRequest])\n")
+    bad = bad.replace("UNCHANGED <<messages, currentTerm, votedFor, log, acked, electionCtr>>",
+                      "UNCHANGED <<currentTerm, votedFor, log, acked, electionCtr>>", 1)
+    assert bad != txt
+    p.write_text(bad)
+    with pytest.raises(raftmc.RaftmcError, match="Restart"):
         raftmc.Model(str(p), ref("Raft", ".cfg"))
 
 

@@ -220,11 +220,14 @@ def test_renamed_helpers_and_module_are_accepted(tmp_path):
 @needs_ref
 def test_changed_action_is_refused_by_name(tmp_path):
     text = ref_text("Raft")
-    # the effect edited (an edited guard is compiled instead: tests/test_guards.py)
-    edited = text.replace("    /\\ votedFor' = [votedFor EXCEPT ![i] = i]", "    /\\ votedFor' = [votedFor EXCEPT ![i] = Nil]")
+    # a message handler's effect edited (an edited guard is compiled behind the
+    # library's effect, tests/test_guards.py; a fixed-binding action's new
+    # effect is compiled whole, tests/test_effects.py; a handler over DOMAIN
+    # messages has no compiled form)
+    edited = text.replace("votesGranted[i] \\cup {j}]", "votesGranted[i] \\cup {i}]")
     assert edited != text
     cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
-    with pytest.raises(raftmc.RaftmcError, match="RequestVote"):
+    with pytest.raises(raftmc.RaftmcError, match="HandleRequestVoteResponse"):
         load(tmp_path, edited, cfg)
 
 

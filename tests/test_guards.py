@@ -132,9 +132,22 @@ def test_edited_becomeleader_guard_is_compiled(tmp_path):
 
 
 @needs_ref
-def test_edited_effect_is_still_refused(tmp_path):
+def test_edited_effect_is_compiled_whole_or_refused(tmp_path):
+    """An edited EFFECT is no longer the library's: the action is compiled
+    whole (rmc_guard.cpp compile_effect; tests/test_effects.py), so counting
+    two elections per RequestVote checks a smaller space; an effect the
+    compiler cannot take (electionCtr set from the message bag) is refused
+    naming the action."""
     text = ref_text()
+    cfg = GUARDS["raft_rv_le_n2v1e1"]["cfg"]
+    assert "MaxElections = 1" in cfg
+    cfg = cfg.replace("MaxElections = 1", "MaxElections = 2")  # two elections, or one counted twice
     edited = text.replace("    /\\ electionCtr' = electionCtr + 1\n", "    /\\ electionCtr' = electionCtr + 2\n")
     assert edited != text
+    m = load(tmp_path, edited, cfg)
+    base = raftmc.Model(module="Raft", cfg_text=cfg).check_cpu(workers=4)
+    assert m.check_cpu(workers=4)["distinct"] < base["distinct"]
+    bad = text.replace("    /\\ electionCtr' = electionCtr + 1\n", "    /\\ electionCtr' = Cardinality(DOMAIN messages)\n")
+    assert bad != text
     with pytest.raises(raftmc.RaftmcError, match="RequestVote"):
-        load(tmp_path, edited, GUARDS["raft_rv_le_n2v1e1"]["cfg"])
+        load(tmp_path, bad, cfg)

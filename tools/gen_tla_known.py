@@ -66,6 +66,18 @@ INVARIANTS = {"LeaderHasAllAckedValues": 0, "NoLogDivergence": 1, "CommittedEntr
 GUARDED = {"Restart", "RequestVote", "Timeout", "BecomeLeader", "ClientRequest"}
 
 
+# The bag helpers the effect compiler implements (by their reference semantics):
+# 0 = a set of records, all new, each sent once (Raft.tla:153-155 SendMultipleOnce,
+# FlexibleRaft.tla:131-133 SendMultiple); 1 = one record, new, sent once
+# (Raft.tla:136-138 _SendOnce, FlexibleRaft.tla:127-129 / RaftFsync.tla:131-134
+# Send); 2 = one non-empty-AppendEntries record, count + 1 (Raft.tla:129-132
+# _SendNoRestriction, and Raft.tla:145-149 Send for every record but an empty
+# AppendEntriesRequest)
+HELPERS = {"RAFT": {"SendMultipleOnce": 0, "_SendOnce": 1, "Send": 2, "_SendNoRestriction": 2},
+           "FLEX": {"SendMultiple": 0, "Send": 1},
+           "FSYNC": {"Send": 1}}
+
+
 def hashes(lib, text):
     buf = ctypes.create_string_buffer(1 << 20)
     n = lib.rmc_tla_hashes(text.encode(), buf, len(buf))
@@ -104,6 +116,9 @@ def main():
             rows.append("{%s, R_ACTION, %s, %s, 0x%sULL, \"%s\"}," % (kind, act, form, h[name], name))
             if name in GUARDED and name in eff and kind != "KRAFT":
                 rows.append("{%s, R_EFFECT, %s, %s, 0x%sULL, \"%s\"}," % (kind, act, form, eff[name], name))
+        # bag helpers an action compiled whole may call (rmc_guard.cpp compile_effect)
+        for name, cls in HELPERS.get(kind, {}).items():
+            rows.append("{%s, R_HELPER, %d, 0, 0x%sULL, \"%s\"}," % (kind, cls, h[name], name))
         for name, iid in INVARIANTS.items():
             if name in h:
                 rows.append("{%s, R_INV, %d, 0, 0x%sULL, \"%s\"}," % (kind, iid, h[name], name))
