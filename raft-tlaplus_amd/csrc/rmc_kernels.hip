@@ -271,8 +271,9 @@ __device__ __forceinline__ MsgSums<N>& sums1(MsgSums2<N>& m) { return m.m; }
 template <int SPEC, int N, int FPW, bool G = false>
 // waves per SIMD: as many as fit without scratch spills (N >= 4 and 128-bit
 // fingerprints need more registers; a spill costs a scratch store per binding)
-// G: the instantiation for models with compiled guards (rmc_guard.cpp)
-__global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW == 2 ? 3 : 4) : FPW == 2 ? 4 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+// G: the instantiation for models with compiled guards or actions (rmc_guard.cpp):
+// 5 waves at N <= 3, so the guard/effect machine's registers do not spill
+__global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW == 2 ? 3 : 4) : FPW == 2 ? 4 : G ? 5 : RMC_EXPAND_WAVES)) void k_expand(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                 unsigned long long pbase, unsigned long long floor, int sharded,
                                                 int shard_self,
                                                 unsigned long long* __restrict__ table, unsigned long long mask,
