@@ -117,6 +117,19 @@ def cpu_baseline(module, cfg_path, seconds=15.0):
                                      what="C oracle (exact canonical forms) over the whole check, in the build "
                                           "container, not on this host")
             break
+    # ... and the CPU engine's own whole check on the GPU box's host (same
+    # threads as the sample above), for a same-host time-to-exhaust
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "cpu_full_*.json")), reverse=True):
+        try:
+            o = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if o.get("cfg_path") == cfg_path and o.get("status") == "ok":
+            out["full_check_same_host"] = dict(seconds=o["seconds"], threads=o["threads"], distinct=o["distinct"],
+                                               source=os.path.relpath(path, ROOT),
+                                               what="the CPU engine over the whole check on the GPU box's host "
+                                                    "(%s; not timed here)" % o.get("host", "?"))
+            break
     return out
 
 
