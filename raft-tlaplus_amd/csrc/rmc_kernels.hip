@@ -30,6 +30,26 @@ __constant__ Model cM;
 
 constexpr int WAVE = 64;
 constexpr int EXPAND_SEGS = 8;  // candidate-buffer segments of the single-shard k_expand (one per XCD)
+
+// XCD-aware block -> tile map (MI355X_MICROARCH.md, workgroup dispatch: blocks
+// b and b + 8 share an XCD and its L2).  RMC_XCD_REMAP = 1 gives each of the 8
+// XCD labels one contiguous run of tiles, so neighbouring tiles -- whose
+// successors are often the same states -- probe and re-read the same
+// fingerprint-set lines through one L2.  A bijection on [0, n) for any n;
+// placement is a speed choice only, the tile a block computes is all that
+// changes.
+#ifndef RMC_XCD_REMAP
+#define RMC_XCD_REMAP 0
+#endif
+__device__ __forceinline__ unsigned long long xcd_tile(unsigned long long b, unsigned long long n) {
+#if RMC_XCD_REMAP
+  const unsigned long long q = n >> 3, r = n & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+#else
+  (void)n;
+  return b;
+#endif
+}
 // cand_ob = ordinal << 16 | flags | binding (10 bits)
 constexpr uint32_t OB_ERR = 0x8000u;    // evaluation error: no successor
 constexpr uint32_t OB_LOCAL = 0x4000u;  // sharded search: this shard owns the fp and k_expand inserted it
@@ -374,7 +394,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     const int tid = threadIdx.x;
     RMC_EXPAND_LDS_ARRAYS
     uint32_t* sS = (uint32_t*)lds;
-    const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
+    const unsigned long long p0 = xcd_tile(blockIdx.x, gridDim.x) * PB;
     const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
     // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
     stage_rows_sync(frontier, p0, np, words, L.Wp, sS);
@@ -587,7 +607,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     // atomics per launch on one address.  The sharded search needs its
     // candidates dense, so it keeps one counter.
     if (tid == 0) {
+#if RMC_EXPAND_PERSIST
       const int seg = sharded ? 0 : (int)((p0 / PB) & (EXPAND_SEGS - 1));
+#else
+      const int seg = sharded ? 0 : (int)(blockIdx.x & (EXPAND_SEGS - 1));  // the block's XCD label
+#endif
       const unsigned long long seg_cap = sharded ? cand_cap : cand_cap / EXPAND_SEGS;
       const unsigned long long c = total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL;
       sG = seg * seg_cap + c;
@@ -859,7 +883,8 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
                                                     uint32_t* __restrict__ par_win, DevStatus* st) {
   __shared__ uint32_t sOff[MARK_WPB][WAVE + 1], sCarry[MARK_WPB][WAVE];
   const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-  const unsigned long long p0 = ((unsigned long long)blockIdx.x * MARK_WPB + w) * WAVE;
+  const unsigned long long bx = xcd_tile(blockIdx.x, gridDim.x);
+  const unsigned long long p0 = (bx * MARK_WPB + w) * WAVE;
   const bool active = p0 < nparents;
   const int np = active ? (int)((nparents - p0) < WAVE ? (nparents - p0) : WAVE) : 0;
   const uint32_t off0 = active ? par_off[p0] : 0u;
@@ -872,9 +897,9 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
   const int total = active ? (int)sOff[w][np] : 0;
   int steps = 0;  // block-uniform trip count (the loop holds a barrier)
   for (int q = 0; q < MARK_WPB; ++q) {
-    const bool qa = ((unsigned long long)blockIdx.x * MARK_WPB + q) * WAVE < nparents;
+    const bool qa = (bx * MARK_WPB + q) * WAVE < nparents;
     if (qa) {
-      const unsigned long long qp = ((unsigned long long)blockIdx.x * MARK_WPB + q) * WAVE;
+      const unsigned long long qp = (bx * MARK_WPB + q) * WAVE;
       const int qn = (int)((nparents - qp) < WAVE ? (nparents - qp) : WAVE);
       const int qt = (int)sOff[q][qn];
       steps = steps > qt ? steps : qt;
@@ -981,7 +1006,7 @@ __global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restric
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int words = cM.words, Wp = words | 1;
   uint32_t* sS = (uint32_t*)lds;
-  const unsigned long long p0 = (unsigned long long)blockIdx.x * PB;
+  const unsigned long long p0 = xcd_tile(blockIdx.x, gridDim.x) * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
   const uint32_t start = par_off[p0];
   const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
