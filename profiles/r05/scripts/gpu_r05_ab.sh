@@ -2,7 +2,7 @@
 # r05: persistent k_expand (LDS-DMA prefetch of the next tile) -- the GPU suite
 # on it, then the bench line interleaved with the one-tile-per-block build
 # (build_np, -DRMC_EXPAND_PERSIST=0) for the A/B.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out/r05ab
 O=gpurun_out/r05ab
 if [ "${SUITE:-1}" = 1 ]; then

@@ -4,7 +4,7 @@
 # block build (build_np, -DRMC_EXPAND_PERSIST=0), the kernel-trace summary of
 # the bench, a fresh-process CLI check of the bench workload, and host-frontier
 # ladders of the candidate config-5 rungs (last: they may run into their limit).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 R=$PWD
 O=$R/gpurun_out/r05d
 mkdir -p $O

@@ -5,7 +5,7 @@
 # HBM the previous process freed), the config-5 rung RaftFsync_n3v1e2r2
 # exhausted single-GPU and on 4 logical shards with host frontiers, then the
 # profile set (bench line, kernel-trace stats, PMC passes: tools/gpu_profile.sh).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 R=$PWD
 O=$R/gpurun_out/r05e
 mkdir -p $O

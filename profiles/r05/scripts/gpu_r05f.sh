@@ -1,7 +1,7 @@
 #!/bin/bash
 # r05 closing check on the committed build, the way the driver runs it: the
 # whole -m gpu suite, smoke(), then the default bench line.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 O=gpurun_out/r05f
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?

@@ -2,7 +2,7 @@
 # r05g: config 3 (FlexibleRaft.cfg verbatim, N = 5) on 4 logical shards, each
 # shard's levels in host pages, as deep as the host allows -- to compare every
 # level with the single-GPU host-frontier ladder (profiles/r03/ladder_FlexibleRaft_hf1.txt).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 R=$PWD
 O=$R/gpurun_out/r05g
 mkdir -p $O

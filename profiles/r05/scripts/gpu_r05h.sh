@@ -1,7 +1,7 @@
 #!/bin/bash
 # r05h: bench.py right after a ~150 GB process (the driver's order: pytest / smoke, then the
 # bench), with the bench's wait for freed HBM before its warm-up check
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 R=$PWD
 O=$R/gpurun_out/r05h
 mkdir -p $O

@@ -2,7 +2,7 @@
 # r05i: the CPU engine (raftmc -cpu, 16 worker threads: the box's CPU share)
 # over the WHOLE bench workload on the GPU box's host -- the same-host
 # time-to-exhaust beside the GPU's (bench.py's cpu_baseline samples a prefix)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 R=$PWD
 O=$R/gpurun_out/r05i
 mkdir -p $O

@@ -2,7 +2,7 @@
 # r05j: A/B of the XCD-aware block -> tile map (build_xcd: -DRMC_XCD_REMAP=1)
 # against the default build on the bench workload, interleaved, bench.py's
 # own timing (3 checks after a warm-up), counts checked
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 R=$PWD
 O=$R/gpurun_out/r05j
 mkdir -p $O
