@@ -16,7 +16,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RUNS = {"fsync_n3v1e2r1_rung": "profiles/r04/oracle_RaftFsync_n3v1e2r1.json",
-        "raft_n3v2e2_bench": "profiles/r04/oracle_Raft_n3v2e2.json"}
+        "raft_n3v2e2_bench": "profiles/r04/oracle_Raft_n3v2e2.json",
+        "fsync_n3v1e2r2_rung": "profiles/r05/oracle_RaftFsync_n3v1e2r2.json"}
 
 
 def main():
