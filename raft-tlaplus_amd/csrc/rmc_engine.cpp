@@ -1598,6 +1598,9 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
   // point (hf_flush), when the compact sizes are known
   struct PendingOut { bool on; int k; unsigned long long n; } hf_pend{false, 0, 0};
   auto hf_pack_async = [&](int k, unsigned long long n) {
+    // the pack buffer k is still the source of chunk ck-2's copy-out (hs.co):
+    // a regrowth waits for it (DevBuf::alloc also drains the device)
+    if (A.hf_pack[k].bytes < std::max<size_t>(n * W * 4, 16)) HIPCHK(hipEventSynchronize(hs.out[k]));
     hf_ensure_out(k, n);
     HIPCHK(hipStreamWaitEvent(hs.cp, hs.mat[k], 0));  // the rows are written
     HIPCHK(hipStreamWaitEvent(hs.cp, hs.out[k], 0));  // the pack buffer's last copy-out is done
@@ -2912,6 +2915,7 @@ int rmc_format_report(const rmc_model* m, const rmc_result* r, char* buf, size_t
 void rmc_model_free(rmc_model* m) { delete m; }
 
 void rmc_release_device_memory(void) {
+  drain_device();
   release_shard_buffers();
   std::lock_guard<std::mutex> lk(g_arena_mu);
   int cur = 0;

@@ -75,11 +75,21 @@ struct OutOfDeviceMemory : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// Freeing or unmapping device memory waits for the whole device first: async
+// copies and kernels of the check's several streams (the host frontier's
+// copy streams among them) may still read a buffer that is being regrown or
+// released -- an unmapped range they touch is a GPU page fault ("illegal
+// memory access" at the next sync, the r04/r05 host-frontier failure).
+inline void drain_device() { (void)hipDeviceSynchronize(); }
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   void alloc(size_t b) {
-    if (p) HIPCHK(hipFree(p));
+    if (p) {
+      drain_device();
+      HIPCHK(hipFree(p));
+    }
     p = nullptr;
     bytes = 0;
     if (b) {
@@ -97,7 +107,10 @@ struct DevBuf {
     void* q = nullptr;
     HIPCHK(hipMalloc(&q, b));
     if (p && keep) HIPCHK(hipMemcpy(q, p, keep, hipMemcpyDeviceToDevice));
-    if (p) HIPCHK(hipFree(p));
+    if (p) {
+      drain_device();
+      HIPCHK(hipFree(p));
+    }
     p = q;
     bytes = b;
   }
@@ -106,7 +119,10 @@ struct DevBuf {
     alloc(b);
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      drain_device();
+      (void)hipFree(p);
+    }
     p = nullptr;
     bytes = 0;
   }
@@ -161,7 +177,10 @@ struct GrowBuf {
         throw OutOfDeviceMemory("device memory exhausted growing a frontier/trace buffer");
       }
       if (p && bytes) HIPCHK(hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice));
-      if (p) HIPCHK(hipFree(p));
+      if (p) {
+        drain_device();
+        HIPCHK(hipFree(p));
+      }
       p = q;
       bytes = nb;
       return;
@@ -198,6 +217,7 @@ struct GrowBuf {
   // hipMemAddressFree), so the range goes as well; the next ensure()
   // reserves a new one.
   void release() {
+    if (p) drain_device();
     if (vmm) {
       size_t off = 0;
       for (auto& c : chunks) {
@@ -259,6 +279,7 @@ struct PinnedPageCache {
     return *c;
   }
   static void retire(void* p, size_t bytes) {
+    drain_device();  // no copy may still target the page
     (void)hipHostUnregister(p);
     void* q = mmap(p, bytes, PROT_NONE, MAP_FIXED | MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
     if (q == MAP_FAILED) munmap(p, bytes);
