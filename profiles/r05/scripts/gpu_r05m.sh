@@ -1,8 +1,8 @@
 #!/bin/bash
-# r05 closing check (second) on the committed build, the way the driver runs it: the
+# r05 closing check (third) on the committed build, the way the driver runs it: the
 # whole -m gpu suite, smoke(), then the default bench line.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
-O=gpurun_out/r05l
+O=gpurun_out/r05m
 mkdir -p $O
 timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -n 3 $O/pytest.log
