@@ -8,12 +8,15 @@ are the input; the frontier, fingerprint set and trace records never leave
 the GPU while timed).  `value` = distinct states / seconds-per-check, summed
 over ranks.
 
-Multi-GPU: one process per GPU (torch.distributed.run).  N>1 runs ONE check
-of the same workload, fingerprint-sharded across the N GPUs (rmc_check_sharded:
-RCCL over xGMI); every rank gets the global counts.  Total work
-is fixed as N grows ("scaling": "strong"); `value` = distinct states of the
-check / seconds per check.  --logical-shards W runs the same sharded protocol
-with W shards on one GPU (a measurement of the protocol's overhead).
+Multi-GPU: N>1 runs ONE check of the same workload, fingerprint-sharded
+across the N GPUs; every shard gets the global counts.  Under
+torch.distributed.run (one process per GPU) it is rmc_check_sharded over RCCL
+and the world size must equal --gpus; started plainly, `--gpus N` is the
+library's own front door, rmc_check with n_gpus = N (one host thread per GPU,
+in-process RCCL) -- which fails, and bench.py with it, when fewer than N GPUs
+are visible.  Total work is fixed as N grows ("scaling": "strong"); `value` =
+distinct states of the check / seconds per check.  --logical-shards W runs the
+same sharded protocol with W shards on one GPU (the protocol's overhead).
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 """
@@ -150,6 +153,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        print("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be at least 1", file=sys.stderr)
+        sys.exit(2)
+    inproc = world == 1 and args.gpus > 1  # the library's n_gpus front door, one host thread per GPU
     dist = None
     if world > 1:
         import torch
@@ -165,6 +175,8 @@ def main():
         uid = [raftmc.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         run_check = lambda: model.check_sharded(rank, world, local, uid[0])  # noqa: E731
+    elif inproc:
+        run_check = lambda: model.check(n_gpus=args.gpus, chunk_parents=args.chunk)  # noqa: E731
     elif args.logical_shards:
         run_check = lambda: model.check_logical(args.logical_shards)  # noqa: E731
     else:
@@ -176,15 +188,27 @@ def main():
         torch.cuda.synchronize()
 
     cold = []
+    cold_phases = None
     for _ in range(args.warmup):
         t = time.perf_counter()
-        run_check()
+        try:
+            run_check()
+        except raftmc.RaftmcError as e:  # e.g. more GPUs asked for than visible: never a silent 1-GPU line
+            print("bench.py: %s" % e, file=sys.stderr)
+            sys.exit(1)
         cold.append(time.perf_counter() - t)
+        if cold_phases is None and world == 1 and not inproc and not args.logical_shards:
+            cold_phases = model.phases()
+            cold_phases["bench_wall"] = cold[-1]
     barrier()
     t0 = time.perf_counter()
     results = []
     for _ in range(args.steps):
-        results.append(run_check())
+        try:
+            results.append(run_check())
+        except raftmc.RaftmcError as e:
+            print("bench.py: %s" % e, file=sys.stderr)
+            sys.exit(1)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -233,7 +257,7 @@ def main():
                       {"Raft": "standard-raft", "KRaft": "KRaft"}.get(module, module),
             "value": value,
             "unit": "distinct states/s",
-            "n_gpus": world,
+            "n_gpus": world if world > 1 else args.gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": per_step * 1e3,
@@ -244,17 +268,19 @@ def main():
             "data": "synthetic: the model constants are the input (no dataset)",
             "config": {"workload": args.workload, "baseline_config": bcfg, "description": desc,
                        "spec": module, "cfg": cfg_rel,
-                       "parallelism": ("fp-sharded x%d (RCCL)" % world) if world > 1 else
+                       "parallelism": ("fp-sharded x%d (RCCL, one process per GPU)" % world) if world > 1 else
+                       ("fp-sharded x%d (n_gpus: one host thread per GPU, in-process RCCL)" % args.gpus) if inproc else
                        ("fp-sharded x%d logical shards on 1 GPU" % args.logical_shards if args.logical_shards
                         else "single")},
             "result": {"generated": res["generated"], "distinct": res["distinct"], "depth": res["depth"],
                        "status": res["status"], "time_to_exhaust_s": per_step,
                        "first_check_s": cold[0] if cold else None,
-                       "first_check_note": "the warm-up check of this process: right after a large process (the "
-                                           "pytest suite) its first allocations wait 4-6 s for the driver to clear "
-                                           "the HBM that process freed, although the device already reports it free; "
-                                           "a fresh CLI process on an idle GPU: 1.32-1.46 s "
-                                           "(profiles/r05/cli_fresh_first_check.txt)",
+                       "first_check_phases": cold_phases,
+                       "first_check_note": "the warm-up check of this process, by phase (rmc_check_phases, seconds): "
+                                           "hip_init = runtime + device context, buffers = arena allocation and VMM "
+                                           "maps, launch_enqueue = host time in launch calls (code-object loading on "
+                                           "a fresh process), table_growth / buffer_growth / widening, kernels = "
+                                           "summed device time",
                        "hidden_var_collisions": res["hidden_var_collisions"],
                        "fpset_slots": res["hash_capacity"], "state_bytes": S, "fp_bits": args.fp_bits},
             # achieved = B / t_wall with B = 2DS + 8G + 20D per check;
@@ -277,15 +303,16 @@ def main():
             line["fpset_inserts"] = {"count": G, "per_s": G / (res["expand_ms"] * 1e-3),
                                      "atomics": "duplicates of earlier levels: none (plain loads); new "
                                                 "fingerprints: CAS + atomicMin; same-level duplicates: atomicMin"}
-        if world > 1:
+        if world > 1 or inproc:
+            nw = args.gpus
             # exchange volume of the sharded protocol: 16 B (fp, key) records,
             # 1 B win flags, rows + 10 B trace records; the off-GPU fraction is (W-1)/W,
             # point-to-point over xGMI (7 links x ~153 GB/s per MI355X)
             G, D, S = res["generated"] - 1, res["distinct"], res["state_bytes"]
-            xb = (G * 17 + D * (S + 10)) * (world - 1) / world
-            line["xgmi"] = {"bytes": xb, "per_gpu_GBps": xb / world / per_step / 1e9,
+            xb = (G * 17 + D * (S + 10)) * (nw - 1) / nw
+            line["xgmi"] = {"bytes": xb, "per_gpu_GBps": xb / nw / per_step / 1e9,
                             "peak_per_gpu_GBps": 7 * 153.0}
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not inproc and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(module, cfg_rel, args.cpu_seconds)
             except Exception as e:  # report, never hide

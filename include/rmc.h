@@ -40,7 +40,9 @@ extern "C" {
 typedef struct rmc_model rmc_model; /* lowered spec + cfg; library-owned */
 
 typedef struct {
-  int n_gpus;          /* GPUs used by this process (1; multi-GPU = one process per GPU) */
+  int n_gpus;          /* GPUs rmc_check uses (default 1).  > 1: the fingerprint-sharded search over GPUs
+                          0..n_gpus-1 of this process, one host thread per GPU (rmc_check_multi, RCCL);
+                          more than the visible GPUs is an error (-4), never a silent 1-GPU run */
   int cpu_workers;     /* accepted for TLC CLI compatibility (-workers); unused by the GPU path */
   int deadlock_check;  /* 0 = TLC -deadlock (the reference's mode); 1 is rejected */
   int fp_bits;         /* 64 (default, TLC's width) or 128 (rmc_check only): the first 64 bits are the
@@ -142,6 +144,18 @@ int rmc_comm_unique_id(unsigned char* id128);
 int rmc_check_sharded(rmc_model* m, const rmc_options* o, int rank, int world, int device, const unsigned char* id128,
                       rmc_result* out);
 int rmc_check_logical(rmc_model* m, const rmc_options* o, int shards, rmc_result* out);
+/* The in-process multi-GPU check that rmc_check runs for n_gpus > 1 (SURVEY.md
+ * §8b: "one host thread per GPU"): shard r on devices[r], one host thread and
+ * stream per shard, the protocol of rmc_check_sharded.  transport
+ * RMC_XPORT_RCCL: an in-process RCCL communicator (ncclCommInitAll) over xGMI,
+ * devices distinct; RMC_XPORT_P2P: the threads pull their peers' buffers with
+ * peer device copies behind host barriers -- any device list, including
+ * several shards on one GPU (how a one-GPU host tests the threaded driver).
+ * rmc_check's choice is RCCL (RMC_MGPU_TRANSPORT=p2p selects peer copies).
+ * Every shard computes the global result; shard 0's lands in *out and m. */
+#define RMC_XPORT_RCCL 0
+#define RMC_XPORT_P2P 1
+int rmc_check_multi(rmc_model* m, const rmc_options* o, const int* devices, int n, int transport, rmc_result* out);
 /* The same multi-process protocol as rmc_check_sharded with POSIX shared
  * memory (segment `shm_name`, created by the ranks) as the transport instead
  * of RCCL: one process per shard on one host, any GPUs -- including several
@@ -165,6 +179,13 @@ int rmc_simulate(rmc_model* m, const rmc_options* o, uint64_t walkers, uint32_t 
  * same packed layout, lowered actions, fingerprint and first-in-TLC-order rule as rmc_check, with the same
  * results.  Explicitly requested (raftmc -cpu); rmc_check never falls back to it.  BASELINE.md's CPU baseline. */
 int rmc_check_cpu(rmc_model* m, const rmc_options* o, rmc_result* out);
+/* Where the last rmc_check's wall time went, as a JSON object of seconds:
+ * hip_init (the process's first check only: runtime + device context),
+ * model_upload, buffers (allocation and VMM mapping of the arena), launch_enqueue
+ * (host time inside kernel launch calls -- a fresh process loads the code
+ * objects there), table_growth, buffer_growth, widening, host_frontier, kernels
+ * (summed device time) and total.  Returns the text length, or -1. */
+int rmc_check_phases(const rmc_model* m, char* json, size_t len);
 /* Per-level counts of the last check: fills up to cap pairs (generated, new) and returns the level count. */
 int rmc_levels(const rmc_model* m, uint64_t* gen_new_pairs, int cap);
 /* Next as a list of disjuncts: comma-separated operator names of the spec

@@ -576,6 +576,54 @@ struct Compiler {
 
 }  // namespace
 
+namespace {
+// The stack-depth check of every compiled program, guards and effects alike:
+// guard_vm / effect_vm keep the stack in eight registers, so each path's depth
+// is followed (the code is structured: each instruction has one depth on all
+// paths).  A guard (guard_end) must leave its value on the stack at G_END.
+void check_depth(const std::vector<uint32_t>& code, const std::string& where, bool guard_end = false) {
+  std::vector<int> at(code.size() + 1, -1);
+  std::vector<size_t> work{0};
+  at[0] = 0;
+  auto flow = [&](size_t to, int d) {
+    if (to > code.size()) throw std::runtime_error(where + ": a jump leaves the code (compiler bug)");
+    if (at[to] < 0) { at[to] = d; work.push_back(to); }
+    else if (at[to] != d) throw std::runtime_error(where + ": stack depths disagree at a join (compiler bug)");
+  };
+  while (!work.empty()) {
+    const size_t pc = work.back();
+    work.pop_back();
+    if (pc == code.size()) continue;
+    const uint32_t op = code[pc] & 0xFFu;
+    const int imm = (int)code[pc] >> 8;
+    int d = at[pc], need = 0, delta = 0;
+    switch (op) {
+      case G_END:
+        if (guard_end && d < 1) throw std::runtime_error(where + ": empty stack at the end");
+        continue;
+      case E_END: continue;
+      case G_CONST: case G_ARG: case G_ECTR: case G_RCTR: delta = 1; break;
+      case G_ST: case G_TERM: case G_VOTED: case G_VOTED2: case G_LEN: case G_COMMIT: case G_FSYNC: case G_VOTES:
+      case G_ACKED: case G_NEG: case G_NOT: case G_POPC: need = 1; break;
+      case G_JZ: case G_JNZ: need = 1; delta = -1; break;
+      case G_JMP: break;
+      case G_POP: case E_ST: case E_TERM: case E_VOTED: case E_VOTES: case E_COMMIT: case E_ECTR: case E_RCTR:
+        need = 1; delta = -1; break;
+      case E_ACKED: case E_APPEND: case E_NEXT: case E_MATCH: case E_PEND: need = 2; delta = -2; break;
+      case E_RVREQ: need = 5; delta = -5; break;
+      default: need = 2; delta = -1; break;  // binary operators
+    }
+    if (d < need) throw std::runtime_error(where + ": stack underflow (compiler bug)");
+    d += delta;
+    if (d > 8)
+      throw std::runtime_error(where + " nests deeper than the machine's 8-value stack: split it into helper conjuncts");
+    if (op == G_JMP) { flow(pc + 1 + imm, d); continue; }
+    if (op == G_JZ || op == G_JNZ) flow(pc + 1 + imm, d);
+    flow(pc + 1, d);
+  }
+}
+}  // namespace
+
 std::vector<uint32_t> compile_guard(const Module& m, const std::vector<std::string>& action_params,
                                     const std::vector<int>& param_types, const std::vector<NodeP>& conjuncts,
                                     const GuardEnv& env, const std::string& where) {
@@ -597,86 +645,11 @@ std::vector<uint32_t> compile_guard(const Module& m, const std::vector<std::stri
     if (t != T_BOOL) c.fail(root, "the guard is not a boolean");
   }
   c.emit(G_END);
-  // guard_vm keeps its stack in eight registers: check every path's depth
-  // (the code is structured, so each instruction has one depth on all paths)
-  const std::vector<uint32_t>& code = c.code;
-  std::vector<int> at(code.size() + 1, -1);
-  std::vector<size_t> work{0};
-  at[0] = 0;
-  auto flow = [&](size_t to, int d) {
-    if (to > code.size()) throw std::runtime_error("guard of " + where + ": a jump leaves the code (compiler bug)");
-    if (at[to] < 0) { at[to] = d; work.push_back(to); }
-    else if (at[to] != d) throw std::runtime_error("guard of " + where + ": stack depths disagree at a join (compiler bug)");
-  };
-  while (!work.empty()) {
-    const size_t pc = work.back();
-    work.pop_back();
-    if (pc == code.size()) continue;
-    const uint32_t op = code[pc] & 0xFFu;
-    const int imm = (int)code[pc] >> 8;
-    int d = at[pc], need = 0, delta = 0;
-    switch (op) {
-      case G_END: if (d < 1) throw std::runtime_error("guard of " + where + ": empty stack at the end"); continue;
-      case G_CONST: case G_ARG: case G_ECTR: case G_RCTR: delta = 1; break;
-      case G_ST: case G_TERM: case G_VOTED: case G_VOTED2: case G_LEN: case G_COMMIT: case G_FSYNC: case G_VOTES:
-      case G_ACKED: case G_NEG: case G_NOT: case G_POPC: need = 1; break;
-      case G_JZ: case G_JNZ: need = 1; delta = -1; break;
-      case G_JMP: break;
-      case G_POP: need = 1; delta = -1; break;
-      default: need = 2; delta = -1; break;  // binary operators
-    }
-    if (d < need) throw std::runtime_error("guard of " + where + ": stack underflow (compiler bug)");
-    d += delta;
-    if (d > 8)
-      throw std::runtime_error("guard of " + where + " nests deeper than the guard machine's 8-value stack: split it "
-                               "into helper conjuncts");
-    if (op == G_JMP) { flow(pc + 1 + imm, d); continue; }
-    if (op == G_JZ || op == G_JNZ) flow(pc + 1 + imm, d);
-    flow(pc + 1, d);
-  }
+  // guard_vm keeps its stack in eight registers: every path's depth is checked
+  check_depth(c.code, "guard of " + where, true);
   return c.code;
 }
 
-namespace {
-// The stack-depth check of compile_guard, for any program (effects included).
-void check_depth(const std::vector<uint32_t>& code, const std::string& where) {
-  std::vector<int> at(code.size() + 1, -1);
-  std::vector<size_t> work{0};
-  at[0] = 0;
-  auto flow = [&](size_t to, int d) {
-    if (to > code.size()) throw std::runtime_error(where + ": a jump leaves the code (compiler bug)");
-    if (at[to] < 0) { at[to] = d; work.push_back(to); }
-    else if (at[to] != d) throw std::runtime_error(where + ": stack depths disagree at a join (compiler bug)");
-  };
-  while (!work.empty()) {
-    const size_t pc = work.back();
-    work.pop_back();
-    if (pc == code.size()) continue;
-    const uint32_t op = code[pc] & 0xFFu;
-    const int imm = (int)code[pc] >> 8;
-    int d = at[pc], need = 0, delta = 0;
-    switch (op) {
-      case G_END: case E_END: continue;
-      case G_CONST: case G_ARG: case G_ECTR: case G_RCTR: delta = 1; break;
-      case G_ST: case G_TERM: case G_VOTED: case G_VOTED2: case G_LEN: case G_COMMIT: case G_FSYNC: case G_VOTES:
-      case G_ACKED: case G_NEG: case G_NOT: case G_POPC: need = 1; break;
-      case G_JZ: case G_JNZ: need = 1; delta = -1; break;
-      case G_JMP: break;
-      case G_POP: case E_ST: case E_TERM: case E_VOTED: case E_VOTES: case E_COMMIT: case E_ECTR: case E_RCTR:
-        need = 1; delta = -1; break;
-      case E_ACKED: case E_APPEND: case E_NEXT: case E_MATCH: case E_PEND: need = 2; delta = -2; break;
-      case E_RVREQ: need = 5; delta = -5; break;
-      default: need = 2; delta = -1; break;  // binary operators
-    }
-    if (d < need) throw std::runtime_error(where + ": stack underflow (compiler bug)");
-    d += delta;
-    if (d > 8) throw std::runtime_error(where + " nests deeper than the machine's 8-value stack");
-    if (op == G_JMP) { flow(pc + 1 + imm, d); continue; }
-    if (op == G_JZ || op == G_JNZ) flow(pc + 1 + imm, d);
-    flow(pc + 1, d);
-  }
-}
-}  // namespace
 
 // An action's EFFECT compiled for effect_vm (rmc_spec.h): the conjuncts that
 // prime a variable, say UNCHANGED, or send messages, over the same typed
@@ -898,6 +871,13 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
         continue;
       }
       const std::string jv = S->bounds[0].vars[0];
+      // TLC's set {rec : j \in S} holds each distinct record once; one E_RVREQ
+      // per member is that set only when the records are pairwise distinct,
+      // which mdest = j guarantees -- any other form could send a
+      // record twice where TLC's set has it once, so it is refused
+      if (f["mdest"]->kind != N_ID || f["mdest"]->s != jv)
+        fail(f["mdest"], n->s + " of {record : " + jv + " \\in S} whose mdest is not " + jv +
+                             " (the records must be distinct per member)");
       // over every server x: if x \in S, send the record with j = x
       for (int x = 0; x < env.N; x++) {
         auto s2 = std::make_shared<Scope>();

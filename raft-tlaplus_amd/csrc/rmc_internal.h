@@ -64,6 +64,11 @@ struct rmc_model {
   std::map<std::string, rmc::tla::GuardSrc> defined_actions;
   // the last check's row widenings (depth, first parent of the redone chunk, new message slots)
   std::vector<std::array<unsigned long long, 3>> widenings;
+  // the last check's host-frontier buffer regrowths while its copy streams ran:
+  // compact-row pack buffers, output windows (test hook rmc_selftest_hf_stats)
+  unsigned long long hf_pack_regrows = 0, hf_out_regrows = 0;
+  // the last single-GPU check's wall time by phase, seconds (rmc_check_phases)
+  std::vector<std::pair<std::string, double>> phases;
 };
 
 
@@ -81,13 +86,20 @@ struct OutOfDeviceMemory : std::runtime_error {
 // released -- an unmapped range they touch is a GPU page fault ("illegal
 // memory access" at the next sync, the r04/r05 host-frontier failure).
 inline void drain_device() { (void)hipDeviceSynchronize(); }
+// The same on a path that can report: a fault of in-flight work surfaces here,
+// named after the buffer being freed, not at some later unrelated call.
+inline void drain_device_checked(const char* what) {
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " at the drain before " + what);
+}
 
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   void alloc(size_t b) {
     if (p) {
-      drain_device();
+      drain_device_checked("a device buffer is regrown");
       HIPCHK(hipFree(p));
     }
     p = nullptr;
@@ -108,7 +120,7 @@ struct DevBuf {
     HIPCHK(hipMalloc(&q, b));
     if (p && keep) HIPCHK(hipMemcpy(q, p, keep, hipMemcpyDeviceToDevice));
     if (p) {
-      drain_device();
+      drain_device_checked("a device buffer is regrown (copy)");
       HIPCHK(hipFree(p));
     }
     p = q;
@@ -178,7 +190,7 @@ struct GrowBuf {
       }
       if (p && bytes) HIPCHK(hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice));
       if (p) {
-        drain_device();
+        drain_device_checked("a frontier/trace buffer is regrown");
         HIPCHK(hipFree(p));
       }
       p = q;
@@ -346,7 +358,8 @@ struct HostPagePool {
     if (void* c = PinnedPageCache::get().take(page_bytes)) return c;
     void* p = mmap(nullptr, page_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
     if (p == MAP_FAILED) return nullptr;
-    if (hipHostRegister(p, page_bytes, hipHostRegisterDefault) != hipSuccess) {
+    // portable: a cached page may serve another GPU's thread in a later check (rmc_check_multi)
+    if (hipHostRegister(p, page_bytes, hipHostRegisterPortable) != hipSuccess) {
       (void)hipGetLastError();
       munmap(p, page_bytes);
       return nullptr;

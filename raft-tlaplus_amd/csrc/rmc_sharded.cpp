@@ -25,9 +25,11 @@
 // its generator, else into staging) -> all-to-all of rows + trace records.
 // At W = 1 that is the single-GPU search plus the protocol's host round trips.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -57,6 +59,9 @@ struct Xfer {
 struct Comm {
   int world = 1;
   std::vector<int> local;  // global ids of the shards this process drives
+  // in-process multi-GPU (rmc_check_multi): the threads that share this
+  // process's host memory, and those that share this thread's device
+  int host_share = 1, dev_share = 1;
   virtual ~Comm() {}
   // in[i] = the k values of local shard local[i]; out = world*k values by shard id
   virtual void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) = 0;
@@ -128,6 +133,14 @@ struct LocalComm : Comm {
 struct RcclComm : Comm {
   ncclComm_t comm = nullptr;
   int rank = 0;
+  bool owns = true;  // false: a communicator of an in-process group (rmc_check_multi owns it)
+  // in-process group: set when another shard's thread failed -- no collective
+  // is started after that, and one blocked in a stream sync is released by
+  // rmc_check_multi aborting the communicators
+  const std::atomic<bool>* aborted = nullptr;
+  void live() const {
+    if (aborted && aborted->load()) throw std::runtime_error("in-process multi-GPU check: another shard's thread failed");
+  }
   DevBuf gbuf;
   RcclComm(int r, int W, const ncclUniqueId& id, hipStream_t s) {
     rank = r;
@@ -136,10 +149,16 @@ struct RcclComm : Comm {
     stream = s;
     NCCLCHK(ncclCommInitRank(&comm, W, id, r));
   }
+  RcclComm(int r, int W, ncclComm_t c, hipStream_t s) : comm(c), rank(r), owns(false) {
+    world = W;
+    local = {r};
+    stream = s;
+  }
   ~RcclComm() override {
-    if (comm) (void)ncclCommDestroy(comm);
+    if (comm && owns) (void)ncclCommDestroy(comm);
   }
   void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) override {
+    live();
     gbuf.ensure((size_t)world * k * 8 + (size_t)k * 8);
     uint64_t* d = gbuf.as<uint64_t>();
     uint64_t* mine = d + (size_t)world * k;
@@ -147,9 +166,12 @@ struct RcclComm : Comm {
     NCCLCHK(ncclAllGather(mine, d, (size_t)k, ncclUint64, comm, stream));
     out.assign((size_t)world * k, 0);
     HIPCHK(hipMemcpyAsync(out.data(), d, (size_t)world * k * 8, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    const hipError_t e = hipStreamSynchronize(stream);
+    live();
+    HIPCHK(e);
   }
   void alltoallv(const std::vector<Xfer>& x) override {
+    live();
     NCCLCHK(ncclGroupStart());
     for (auto& t : x) {
       if (!t.bytes) continue;
@@ -314,6 +336,92 @@ struct ShmComm : Comm {
   }
 };
 
+// The W host threads of one in-process multi-GPU check (rmc_check_multi):
+// a generation barrier that a failing thread can break (abort), the allgather
+// area, and each exchange step's buffer pointers by transfer index.
+struct ThreadGroup {
+  int W = 1;
+  std::vector<int> dev;  // device of each shard
+  std::mutex mu;
+  std::condition_variable cv;
+  int count = 0;
+  unsigned long long gen = 0;
+  std::atomic<bool> aborted{false};
+  std::vector<uint64_t> gather;
+  std::vector<const void*> sp;  // transfer k's source (set by its sender)
+  std::vector<void*> rp;        // transfer k's destination (set by its receiver)
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) throw std::runtime_error("in-process multi-GPU check: another shard's thread failed");
+    const unsigned long long g = gen;
+    if (++count == W) {
+      count = 0;
+      gen++;
+      cv.notify_all();
+      return;
+    }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    if (gen == g) throw std::runtime_error("in-process multi-GPU check: another shard's thread failed");
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+
+// One shard per host thread of this process, peer device copies as the
+// transport (RMC_XPORT_P2P): a receiver pulls each transfer from its sender's
+// buffer on its own stream (hipMemcpyPeerAsync over xGMI across devices, a
+// device copy when both shards share one -- which is how the one-GPU box
+// runs the in-process driver with several threads).  Like ShmComm, every rank
+// builds the same global transfer list, so the k-th entry is the same
+// transfer everywhere; the pointers are published through the group.
+struct ThreadComm : Comm {
+  ThreadGroup* g;
+  int rank;
+  ThreadComm(ThreadGroup* grp, int r, hipStream_t s) : g(grp), rank(r) {
+    world = grp->W;
+    local = {r};
+    stream = s;
+  }
+  void allgather(const std::vector<std::vector<uint64_t>>& in, std::vector<uint64_t>& out, int k) override {
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      if (g->gather.size() < (size_t)world * k) g->gather.resize((size_t)world * k);
+      for (int j = 0; j < k; j++) g->gather[(size_t)rank * k + j] = in[0][j];
+    }
+    g->barrier();
+    out.assign(g->gather.begin(), g->gather.begin() + (size_t)world * k);
+    g->barrier();  // nobody writes the next gather before every rank has read this one
+  }
+  void alltoallv(const std::vector<Xfer>& x) override {
+    HIPCHK(hipStreamSynchronize(stream));  // this rank's send buffers are complete
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      if (g->sp.size() < x.size()) {
+        g->sp.resize(x.size());
+        g->rp.resize(x.size());
+      }
+      for (size_t k = 0; k < x.size(); k++) {
+        if (x[k].src == rank) g->sp[k] = x[k].sbuf;
+        if (x[k].dst == rank) g->rp[k] = x[k].rbuf;
+      }
+    }
+    g->barrier();
+    for (size_t k = 0; k < x.size(); k++) {
+      const Xfer& t = x[k];
+      if (t.dst != rank || !t.bytes) continue;
+      if (g->dev[t.src] == g->dev[t.dst])
+        HIPCHK(hipMemcpyAsync(g->rp[k], g->sp[k], t.bytes, hipMemcpyDeviceToDevice, stream));
+      else
+        HIPCHK(hipMemcpyPeerAsync(g->rp[k], g->dev[t.dst], g->sp[k], g->dev[t.src], t.bytes, stream));
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+    g->barrier();  // every pull has landed: senders may reuse their buffers
+  }
+};
+
 // ---------------------------------------------------------- shard buffers
 struct ShardBufs {
   DevBuf table, table2, cfp, cval, cob, cwin, poff, pn, pwin, ppos, counters, stbuf, scantmp;
@@ -346,6 +454,25 @@ void release_shard_buffers() {
   for (auto& kv : g_shard_bufs)
     if (hipSetDevice(kv.first.first) == hipSuccess) kv.second->release();
   (void)hipSetDevice(cur);
+}
+// Cached shard buffers are sized for the partition that grew them: a check
+// with another shard count on this device starts from nothing (a W = 2
+// check's shard 0 holds half of every level, twice what a W = 4 shard needs).
+// The in-process multi-GPU driver settles this for every device before its
+// threads start, so no thread releases buffers another one is using.
+static std::mutex g_world_mu;
+static std::map<int, int> g_last_world;
+static void settle_shard_world(int W) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  bool rel = false;
+  {
+    std::lock_guard<std::mutex> lk(g_world_mu);
+    int& lw = g_last_world[dev];
+    rel = lw && lw != W;
+    lw = W;
+  }
+  if (rel) release_shard_buffers();
 }
 
 struct Shard {
@@ -434,16 +561,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
   const int NL = (int)comm.local.size();
   if (W > 64) throw std::runtime_error("at most 64 shards");
-  {  // cached shard buffers are sized for the partition that grew them: a
-     // check with another shard count starts from nothing (a W = 2 check's
-     // shard 0 holds half of every level, twice what a W = 4 shard needs)
-    static std::map<int, int> last_world;
-    int dev = 0;
-    HIPCHK(hipGetDevice(&dev));
-    int& lw = last_world[dev];
-    if (lw && lw != W) release_shard_buffers();
-    lw = W;
-  }
+  settle_shard_world(W);
 
   std::vector<Shard> sh(NL);
   // every shard on this device, driven by this process (logical shards)
@@ -452,7 +570,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   HostPagePool pool;
   pool.page_bytes = std::max<size_t>(WD * 4, 256ULL << 20);
   if (const char* e = getenv("RMC_HOST_PAGE_ROWS")) pool.page_bytes = std::max<long long>(1, atoll(e)) * WD * 4;
-  pool.limit = host_frontier_limit();
+  pool.limit = host_frontier_limit() / (size_t)std::max(1, comm.host_share);  // threads of one process split it
   struct PagesGuard {
     std::vector<Shard>& sh;
     HostPagePool& pool;
@@ -474,7 +592,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   for (int i = 0; i < NL; i++) {
     Shard& s = sh[i];
     s.id = comm.local[i];
-    s.B = &shard_bufs(i);
+    s.B = &shard_bufs(s.id);  // by shard id: threads sharing one device keep apart
     ShardBufs& B = *s.B;
     s.slots = opt->hash_slots ? opt->hash_slots : std::max(1ULL << 22, hint_slots_1);
     if (s.slots & (s.slots - 1)) throw std::runtime_error("hash_slots must be a power of two");
@@ -673,7 +791,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
       // boundary -- decided on the allgathered projections, so all agree
       for (int i = 0; i < NL; i++)
         rows[i] = {(uint64_t)((double)sh[i].ncur * std::max(rate, 1.0) * 1.25 * (double)(WD * 4) >
-                              hf_hbm_fraction() * (double)hbm_total / NL)};
+                              hf_hbm_fraction() * (double)hbm_total / (NL * std::max(1, comm.dev_share)))};
       comm.allgather(rows, all, 1);
       bool any = false;
       for (int r = 0; r < W; r++) any |= all[r] != 0;
@@ -1312,6 +1430,170 @@ static int run_with_regrow(rmc_model* m, const rmc_options* o, Comm& comm, rmc_r
   return rc;
 }
 
+// ------------------------------------------- in-process multi-GPU (n_gpus)
+// rmc_options.n_gpus > 1 runs the fingerprint-sharded search
+// with one host thread per GPU of this process, each on its own stream --
+// the same protocol as rmc_check_sharded's one process per GPU, with the
+// communicators created in-process.  The streams and RCCL communicators of a
+// device list are kept for the next check (a bench step must not pay
+// ncclCommInitAll again).
+struct MultiGroup {
+  std::vector<int> dev;
+  std::vector<hipStream_t> streams;
+  std::vector<ncclComm_t> comms;  // RMC_XPORT_RCCL only
+};
+static std::mutex g_multi_mu;
+static std::map<std::string, MultiGroup*> g_multi;
+static MultiGroup& multi_group(const std::vector<int>& dev, int transport) {
+  std::string key = std::to_string(transport);
+  for (int d : dev) key += "," + std::to_string(d);
+  std::lock_guard<std::mutex> lk(g_multi_mu);
+  MultiGroup*& g = g_multi[key];
+  if (g) return *g;
+  std::unique_ptr<MultiGroup> ng(new MultiGroup());
+  ng->dev = dev;
+  for (int d : dev) {
+    HIPCHK(hipSetDevice(d));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    ng->streams.push_back(s);
+  }
+  if (transport == RMC_XPORT_RCCL) {
+    ng->comms.assign(dev.size(), nullptr);
+    NCCLCHK(ncclCommInitAll(ng->comms.data(), (int)dev.size(), dev.data()));
+  }
+  g = ng.release();
+  return *g;
+}
+// a group whose communicators were aborted is not reused
+static void drop_multi_group(MultiGroup* g) {
+  std::lock_guard<std::mutex> lk(g_multi_mu);
+  for (auto it = g_multi.begin(); it != g_multi.end(); ++it)
+    if (it->second == g) {
+      g_multi.erase(it);
+      break;
+    }
+}
+
+static int check_multi(rmc_model* m, const rmc_options* o, const std::vector<int>& dev, int transport,
+                       rmc_result* out) {
+  const int n = (int)dev.size();
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    set_last_error("no HIP device available: the raftmc GPU path requires an MI355X (gfx950)");
+    return -4;
+  }
+  for (int d : dev)
+    if (d < 0 || d >= ndev) {
+      set_last_error("GPU " + std::to_string(d) + " requested for a " + std::to_string(n) + "-GPU check, but " +
+                     std::to_string(ndev) + " GPU(s) are visible to this process");
+      return -4;
+    }
+  const std::set<int> uniq(dev.begin(), dev.end());
+  if (transport == RMC_XPORT_RCCL && (int)uniq.size() != n) {
+    set_last_error("the RCCL transport needs a distinct GPU per shard (RCCL refuses two ranks on one device); "
+                   "use RMC_XPORT_P2P to run several shards on one GPU");
+    return -1;
+  }
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  for (int d : uniq) {  // this process's single-GPU caches go; every device's shard world is settled now
+    HIPCHK(hipSetDevice(d));
+    release_single_buffers();
+    settle_shard_world(n);
+  }
+  if (transport == RMC_XPORT_P2P)  // receivers pull straight from their peers' HBM
+    for (int a : uniq)
+      for (int b : uniq) {
+        int can = 0;
+        if (a == b || hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+        HIPCHK(hipSetDevice(a));
+        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+        (void)hipGetLastError();
+      }
+  MultiGroup& G = multi_group(dev, transport);
+  ThreadGroup grp;
+  grp.W = n;
+  grp.dev = dev;
+  std::vector<std::unique_ptr<rmc_model>> cl;
+  for (int r = 0; r < n; r++) cl.emplace_back(new rmc_model(*m));  // each thread finalizes its own copy
+  std::vector<rmc_result> res(n);
+  std::vector<std::string> err(n);
+  std::vector<int> rc(n, 0);
+  std::atomic<int> first_failed{-1};
+  std::mutex dmu;
+  std::condition_variable dcv;
+  int done = 0;
+  auto work = [&](int r) {
+    try {
+      HIPCHK(hipSetDevice(dev[r]));
+      std::unique_ptr<Comm> c;
+      if (transport == RMC_XPORT_RCCL) {
+        RcclComm* rc_ = new RcclComm(r, n, G.comms[r], G.streams[r]);
+        rc_->aborted = &grp.aborted;
+        c.reset(rc_);
+      } else {
+        c.reset(new ThreadComm(&grp, r, G.streams[r]));
+      }
+      c->host_share = n;
+      c->dev_share = (int)std::count(dev.begin(), dev.end(), dev[r]);
+      memset(&res[r], 0, sizeof res[r]);
+      rc[r] = run_with_regrow(cl[r].get(), o, *c, &res[r]);
+    } catch (std::exception& e) {
+      err[r] = e.what();
+      rc[r] = -5;
+      int none = -1;
+      first_failed.compare_exchange_strong(none, r);
+      grp.abort();
+    }
+    std::lock_guard<std::mutex> lk(dmu);
+    done++;
+    dcv.notify_all();
+  };
+  std::vector<std::thread> th;
+  for (int r = 0; r < n; r++) th.emplace_back(work, r);
+  bool aborted_comms = false;
+  {
+    std::unique_lock<std::mutex> lk(dmu);
+    for (;;) {
+      if (dcv.wait_for(lk, std::chrono::seconds(30), [&] { return done == n; })) break;
+      if (first_failed.load() >= 0 && transport == RMC_XPORT_RCCL && !aborted_comms) {
+        // a shard failed 30 s ago and its peers are still blocked inside a
+        // collective it will never join: abort the communicators (their
+        // kernels stop; the threads see `aborted` and leave without another call)
+        fprintf(stderr, "[rmc] shard %d failed; aborting the in-process RCCL communicators\n", first_failed.load());
+        for (ncclComm_t c : G.comms) (void)ncclCommAbort(c);
+        aborted_comms = true;
+      }
+    }
+  }
+  for (auto& t : th) t.join();
+  (void)hipSetDevice(cur);
+  if (first_failed.load() >= 0) {
+    if (transport == RMC_XPORT_RCCL) {
+      if (!aborted_comms)
+        for (ncclComm_t c : G.comms) (void)ncclCommAbort(c);
+      drop_multi_group(&G);  // its communicators are gone (its streams are leaked with it)
+    }
+    const int f = first_failed.load();
+    set_last_error("shard " + std::to_string(f) + " (GPU " + std::to_string(dev[f]) + ") of " + std::to_string(n) +
+                   ": " + err[f]);
+    return -5;
+  }
+  for (int r = 0; r < n; r++)
+    if (rc[r] != 0) {
+      set_last_error("shard " + std::to_string(r) + " returned " + std::to_string(rc[r]));
+      return rc[r];
+    }
+  // every rank holds the global result; shard 0's model (finalized, levels,
+  // trace, size hints for the next check) becomes the caller's
+  *out = res[0];
+  for (int r = 1; r < n; r++) out->device_bytes = std::max(out->device_bytes, res[r].device_bytes);
+  *m = std::move(*cl[0]);
+  return 0;
+}
+
 }  // namespace rmcx
 
 using namespace rmcx;
@@ -1397,6 +1679,23 @@ int rmc_check_sharded_shm(rmc_model* m, const rmc_options* o, int rank, int worl
     }
     HIPCHK(hipStreamDestroy(s));
     return rc;
+  } catch (std::exception& e) {
+    set_last_error(e.what());
+    return -5;
+  }
+}
+
+int rmc_check_multi(rmc_model* m, const rmc_options* o, const int* devices, int n, int transport, rmc_result* out) {
+  if (!m || !out || !devices || n < 1 || n > 64 || (transport != RMC_XPORT_RCCL && transport != RMC_XPORT_P2P)) {
+    set_last_error("bad argument");
+    return -1;
+  }
+  rmc_options def;
+  rmc_options_default(&def);
+  if (!o) o = &def;
+  memset(out, 0, sizeof *out);
+  try {
+    return check_multi(m, o, std::vector<int>(devices, devices + n), transport, out);
   } catch (std::exception& e) {
     set_last_error(e.what());
     return -5;

@@ -57,7 +57,11 @@ EXPORTS = ["rmc_model_load", "rmc_model_load_text", "rmc_options_default", "rmc_
            "rmc_release_device_memory", "rmc_comm_unique_id", "rmc_check_sharded", "rmc_check_logical",
            "rmc_simulate", "rmc_trace_module", "rmc_trace_json", "rmc_check_cpu", "rmc_check_sharded_shm",
            "rmc_abi_layout", "rmc_abi_version", "rmc_model_set_next", "rmc_model_next", "rmc_tla_hashes",
-           "rmc_model_set_guard", "rmc_source_id", "rmc_model_define_action"]
+           "rmc_model_set_guard", "rmc_source_id", "rmc_model_define_action", "rmc_check_multi",
+           "rmc_check_phases"]
+
+# rmc_check_multi transports (include/rmc.h)
+XPORT_RCCL, XPORT_P2P = 0, 1
 
 # the rmc_options / rmc_result layout these ctypes mirrors follow (include/rmc.h RMC_ABI_VERSION)
 ABI_VERSION = 2
@@ -78,6 +82,14 @@ def source_mismatch(source_id):
         except OSError:
             return "source %s is missing" % f
     return None if h.hexdigest()[:32] == digest else "source hash %s, tree %s" % (digest, h.hexdigest()[:32])
+
+
+def refuse_stale(source_id):
+    """Raise unless the library's sources (rmc_source_id) are the tree's."""
+    stale = source_mismatch(source_id)
+    if stale and os.environ.get("RAFTMC_ALLOW_STALE") != "1":
+        raise RaftmcError("%s was built from other sources than the tree's (%s): rebuild it "
+                          "(make -C raft-tlaplus_amd OUT=%s)" % (LIB_PATH, stale, os.environ.get("RAFTMC_BUILD", "build")))
 
 
 def lib():
@@ -106,14 +118,11 @@ def lib():
         raise RaftmcError("librmc.so has ABI version %d; this binding mirrors version %d (rebuild one of them)"
                           % (L.rmc_abi_version(), ABI_VERSION))
     L.rmc_source_id.restype = ctypes.c_char_p
-    stale = source_mismatch(L.rmc_source_id().decode())
-    if stale and "RAFTMC_BUILD" in os.environ:
-        raise RaftmcError("%s was built from other sources than the tree's (%s): rebuild it "
-                          "(make -C raft-tlaplus_amd OUT=%s)" % (LIB_PATH, stale, os.environ["RAFTMC_BUILD"]))
-    if stale:
-        import warnings
-        warnings.warn("%s was built from other sources than the tree's (%s): run make -C raft-tlaplus_amd"
-                      % (LIB_PATH, stale))
+    # a library built from other sources than the tree's is refused, default
+    # build included: a forgotten rebuild would otherwise put
+    # stale kernels behind green tests.  RAFTMC_ALLOW_STALE=1 overrides it for
+    # a deliberate experiment.
+    refuse_stale(L.rmc_source_id().decode())
     L.rmc_model_set_next.argtypes = [P, ctypes.c_char_p]
     L.rmc_model_set_guard.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
     L.rmc_model_define_action.argtypes = [P, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p]
@@ -123,6 +132,10 @@ def lib():
     L.rmc_check_sharded.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                     ctypes.POINTER(Result)]
     L.rmc_check_logical.argtypes = [P, ctypes.POINTER(Options), c_int, ctypes.POINTER(Result)]
+    L.rmc_check_multi.argtypes = [P, ctypes.POINTER(Options), ctypes.POINTER(c_int), c_int, c_int,
+                                  ctypes.POINTER(Result)]
+    L.rmc_selftest_hf_stats.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    L.rmc_check_phases.argtypes = [P, ctypes.c_char_p, c_size_t]
     L.rmc_check_sharded_shm.argtypes = [P, ctypes.POINTER(Options), c_int, c_int, c_int, ctypes.c_char_p,
                                         ctypes.POINTER(Result)]
     L.rmc_check_cpu.argtypes = [P, ctypes.POINTER(Options), ctypes.POINTER(Result)]
@@ -176,7 +189,7 @@ class Model:
     def _options(self, deadlock=False, hash_slots=0, msg_cap_K=0, frontier_cap=0,
                  chunk_parents=0, verbose=False, max_depth=0, workers=0, grow_on_overflow=False,
                  time_limit=0.0, fp_bits=64, checkpoint_dir=None, checkpoint_minutes=0.0, recover_dir=None,
-                 host_frontier=0):
+                 host_frontier=0, n_gpus=1):
         L = lib()
         o = Options()
         L.rmc_options_default(ctypes.byref(o))
@@ -195,6 +208,7 @@ class Model:
         o.time_limit = float(time_limit)
         o.fp_bits = int(fp_bits)
         o.host_frontier = int(host_frontier)
+        o.n_gpus = int(n_gpus)
         return o
 
     def _result(self, rc, r):
@@ -252,7 +266,9 @@ class Model:
         return buf.value.decode().split(",")
 
     def check(self, **kw):
-        """Run the model check on this process's GPU; returns a dict of TLC's results."""
+        """Run the model check; returns a dict of TLC's results.  n_gpus=N > 1 runs
+        the fingerprint-sharded search over GPUs 0..N-1 of this process, one host
+        thread per GPU (rmc_check_multi over RCCL); more GPUs than visible raise."""
         o, r = self._options(**kw), Result()
         return self._result(lib().rmc_check(self._h, ctypes.byref(o), ctypes.byref(r)), r)
 
@@ -265,6 +281,32 @@ class Model:
         """The fingerprint-sharded protocol with `shards` logical shards on this GPU."""
         o, r = self._options(**kw), Result()
         return self._result(lib().rmc_check_logical(self._h, ctypes.byref(o), int(shards), ctypes.byref(r)), r)
+
+    def check_multi(self, devices, transport=XPORT_P2P, **kw):
+        """The in-process multi-GPU check with shard r on devices[r] (rmc_check_multi).
+        transport XPORT_P2P (peer copies; a device may repeat, e.g. [0, 0]) or
+        XPORT_RCCL (distinct devices)."""
+        o, r = self._options(**kw), Result()
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        rc = lib().rmc_check_multi(self._h, ctypes.byref(o), devs, len(devices), int(transport), ctypes.byref(r))
+        return self._result(rc, r)
+
+    def phases(self):
+        """Where the last single-GPU check's wall time went, in seconds
+        (rmc_check_phases): hip_init, model_upload, buffers, launch_enqueue,
+        table_growth, buffer_growth, widening, host_frontier, kernels, total."""
+        import json
+        buf = ctypes.create_string_buffer(4096)
+        if lib().rmc_check_phases(self._h, buf, len(buf)) < 0:
+            raise RaftmcError("no check")
+        return json.loads(buf.value.decode())
+
+    def selftest_hf_stats(self):
+        """TEST HOOK: the last check's host-frontier buffer regrowths while its
+        copy streams ran: (pack buffers, output windows)."""
+        buf = (ctypes.c_uint64 * 2)()
+        lib().rmc_selftest_hf_stats(self._h, buf)
+        return int(buf[0]), int(buf[1])
 
     def check_sharded(self, rank, world, device, unique_id, **kw):
         """One shard of a multi-GPU check (one process per GPU, RCCL).  unique_id =

@@ -143,6 +143,9 @@ def test_reference_leader_rows_compiled_whole_give_the_reference_counts(slot, bo
     (REFERENCE_RV.replace("/\\ electionCtr' = electionCtr + 1", "/\\ electionCtr' = electionCtr + 1\n"
                           "    /\\ electionCtr' = electionCtr + 2"), "changed twice"),
     (REFERENCE_RV.replace("[state EXCEPT ![i] = Candidate]", "[state EXCEPT ![i] = 3]"), "integer"),
+    # {rec : j \in S} with records that need not differ per member
+    # (TLC's set would hold one where one send per member would add two)
+    (REFERENCE_RV.replace("mdest         |-> j] : j", "mdest         |-> i] : j"), "mdest is not j"),
 ])
 def test_refused_effects_are_named(body, match):
     m = raftmc.Model(module="Raft", cfg_text=cfg_text("Raft", n=2, v=1, E=1))

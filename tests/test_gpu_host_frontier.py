@@ -164,3 +164,38 @@ def test_back_to_back_host_checks_reuse_pinned_pages(monkeypatch):
         for chunk in (0, 1000, 0):
             r = model(g).check(host_frontier=1, chunk_parents=chunk)
             assert r["status"] == "violation" and (r["generated"], r["distinct"]) == (g["generated"], g["distinct"])
+
+
+def test_pack_buffer_regrows_while_copy_outs_run(monkeypatch):
+    """r06, the r05 fault's named path driven on purpose (VERDICT r05 What's
+    weak #3): with 7-parent chunks a chunk's new rows outgrow the compact-row
+    pack buffer of its output window (sized for 3 rows per parent) while the
+    previous same-parity chunk's copy-out may still read it.  The regrowth
+    waits for that copy-out's event and then checks (hipEventQuery) that no
+    copy stream still uses the buffer -- a missing wait is an error naming the
+    buffer, not a GPU fault.  Small pages make the rows straddle pages."""
+    monkeypatch.setenv("RMC_HOST_PAGE_ROWS", "64")
+    regrows = 0
+    for name in ("raft_n2v2e2r2_order", "fsync_n2v2e2r1_hidden"):
+        g = ORDER[name]
+        m = model(g)
+        same(m.check(host_frontier=1, chunk_parents=7), g)
+        regrows += m.selftest_hf_stats()[0]
+    g = SMALL["raft_n3v1e1r1"]
+    m = model(g)
+    same(m.check(host_frontier=1, chunk_parents=7), g)
+    regrows += m.selftest_hf_stats()[0]
+    assert regrows >= 1
+
+
+def test_first_check_phases_add_up():
+    """rmc_check_phases: the named phases of a check are non-negative and
+    their sum stays within the total."""
+    g = SHIPPED["Raft_cfg"]
+    m = model(g)
+    m.check(chunk_parents=20000)
+    p = m.phases()
+    assert set(p) >= {"hip_init", "buffers", "launch_enqueue", "table_growth", "kernels", "total"}
+    assert all(v >= 0 for v in p.values())
+    # (hip_init precedes the check's own clock; launch enqueue overlaps kernels)
+    assert sum(v for k, v in p.items() if k not in ("total", "hip_init")) <= p["total"] * 1.2 + 0.05

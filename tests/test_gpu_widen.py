@@ -81,6 +81,12 @@ def test_widening_violation_counts_and_trace(name):
     assert r["status"] == "violation" and r["violated"] == g["violated"]
     assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"])
     assert len(r["trace"]) == g["trace_len"]
+    # the whole behaviour -- action labels and states -- equals a
+    # check at a fixed capacity (no widening), so trace records written before
+    # a widening (old binding numbering) are replayed correctly
+    w = m.selftest_widenings()
+    fixed = model(g).check(chunk_parents=50, msg_cap_K=40)
+    assert fixed["trace"] == r["trace"], w
 
 
 def test_bench_rung_fresh_model_equals_exhausted():
@@ -94,3 +100,19 @@ def test_bench_rung_fresh_model_equals_exhausted():
         assert r[k] == e[k], (k, r["status"], r.get("message"))
     assert r["state_bytes"] == 192  # 13 header words + 35 message slots: the tight row
     assert len(m.selftest_widenings()) >= 3
+
+
+def test_widening_mid_level_then_violation_trace():
+    """At least one UNSAFE case widens in the middle of a level (c0 > 0) before
+    the violating level; its trace equals the fixed-capacity check's."""
+    hits = 0
+    for name in sorted(UNSAFE):
+        g = UNSAFE[name]
+        m = model(g)
+        r = m.check(chunk_parents=7)
+        w = m.selftest_widenings()
+        assert r["status"] == "violation"
+        if any(c0 > 0 and d < r["depth"] for d, c0, _ in w):
+            hits += 1
+            assert model(g).check(chunk_parents=7, msg_cap_K=40)["trace"] == r["trace"]
+    assert hits >= 1
