@@ -34,9 +34,10 @@ class RaftSpec:
                  guards=None, defined=None):
         # defined: {name: (form, f(spec, s, *args) -> successors)}: actions
         # written in Python for next_order to name, bound as a Next disjunct
-        # \E i \in Server (form "i"), \E i \in Server, v \in Value ("iv") or
-        # \E i, j \in Server ("ij"): the oracle side of actions the front end
-        # compiles whole (rmc_guard.cpp compile_effect)
+        # \E i \in Server (form "i"), \E i \in Server, v \in Value ("iv"),
+        # \E i, j \in Server ("ij") or over DOMAIN messages ("m": f(spec, s)):
+        # the oracle side of actions the front end compiles whole (rmc_guard.cpp
+        # compile_effect, compile_handler)
         self.defined = dict(defined or {})
         # guards: {action name: g(spec, s, *args) -> bool} replacing the
         # reference's guard of that action (its effect unchanged): the oracle
@@ -480,6 +481,10 @@ class RaftSpec:
             elif form == "ij":
                 groups[name] = [("%s(%s,%s)" % (name, n[i], n[j]), lambda s, f=f, i=i, j=j: f(self, s, i, j))
                                 for i, j in self.pairs()]
+            elif form == "m":
+                # a message handler (\E m \in DOMAIN messages : ...): f ranges over
+                # DOMAIN messages itself, in TLC's order, as the module's handlers do
+                groups[name] = [(name, lambda s, f=f: f(self, s))]
             else:
                 raise ValueError("form %r" % form)
         out = []

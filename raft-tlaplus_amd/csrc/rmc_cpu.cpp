@@ -196,8 +196,9 @@ int check_cpu_t(rmc_model* m, const rmc_options* opt, int T, rmc_result* res) {
             if (src != dst) ms.S[MsgSums<N>::pair(src, dst)] += u;
           }
           succ.clear();
-          const int B = M.nfixed + nm;
-          for (int b = 0; b < B; b++) {
+          const int B = nbindings(M, nm);
+          for (int x = 0; x < B; x++) {
+            const int b = binding_at(M, x, nm);
             Delta d;
             if (!eval_binding<SPEC, N>(s, M, b, d)) continue;
             Cand c;

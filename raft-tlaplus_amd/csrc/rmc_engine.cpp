@@ -244,6 +244,7 @@ void build_actions(Model& M, const std::vector<std::pair<int, int>>* lowered) {
   int off = 0, nf = 0;
   for (int a = 0; a < A_NUM; a++) M.msg_act_slot[a] = 0;
   M.msg_act_mask = 0;
+  M.nmsgc = 0;
   for (int s = 0; s < M.nact; s++) {
     M.act_fb_first[s] = (uint8_t)nf;
     M.act_id[s] = t[s].id;
@@ -253,6 +254,10 @@ void build_actions(Model& M, const std::vector<std::pair<int, int>>* lowered) {
     if (t[s].kind == K_MSG) {
       M.msg_act_slot[t[s].id] = s;
       M.msg_act_mask |= 1ULL << t[s].id;
+    } else if (t[s].kind == K_MSGC) {  // a compiled message handler: evaluated on its own (act_message skips it)
+      if (t[s].id < A_C0 || t[s].id >= A_C0 + MAXCOMPILED) throw std::runtime_error("compiled handler id");
+      M.msg_act_slot[t[s].id] = s;
+      M.msgc_q[M.nmsgc++] = (int8_t)(t[s].id - A_C0);
     } else
       for (int x = 0; x < size; x++) {
         // bindings the constants disable for good are not evaluated at all
@@ -282,9 +287,14 @@ void build_actions(Model& M, const std::vector<std::pair<int, int>>* lowered) {
   if (off > 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");
   for (int q = 0; q < 1024; q++) M.ord2b[q] = 0xFFFF;
   for (int b = 0; b < nf; b++) M.ord2b[M.act_off[M.fb_act[b]] + M.fb_x[b]] = (uint16_t)b;
-  for (int sl = 0; sl < M.nact; sl++)
+  for (int sl = 0; sl < M.nact; sl++) {
     if (M.act_kind[sl] == K_MSG)
       for (int k = 0; k < M.kmax; k++) M.ord2b[M.act_off[sl] + k] = (uint16_t)(nf + k);
+    if (M.act_kind[sl] == K_MSGC)
+      for (int k = 0; k < M.kmax; k++)
+        M.ord2b[M.act_off[sl] + k] = (uint16_t)(nf + MSGC_STRIDE * (1 + M.act_id[sl] - A_C0) + k);
+  }
+  if (M.kmax > MSGC_STRIDE) throw std::runtime_error("more message slots than a compiled handler's binding stride");
   M.bind_words = (M.nfixed + M.kmax + 31) / 32;
   M.ord_words = (off + 31) / 32;
   if (off >= 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");
@@ -368,6 +378,14 @@ void install_guards(rmc_model* m, const std::vector<rmc::tla::GuardSrc>& gs) {
   std::vector<std::pair<int, int>> starts, estarts;
   for (const auto& g : gs) {
     const bool whole = g.act >= A_C0;  // compiled whole: guard and effect (rmc_guard.cpp compile_effect)
+    if (whole && g.kind == K_MSGC) {  // a message handler: one program, guards and effects in the text's order
+      rmc::tla::GuardEnv eenv = env;
+      eenv.send_helpers = g.send_helpers;
+      std::vector<uint32_t> h = rmc::tla::compile_handler(*g.mod, g.params, g.conjuncts, eenv, g.op);
+      estarts.push_back({g.act - A_C0, (int)code.size()});
+      code.insert(code.end(), h.begin(), h.end());
+      continue;
+    }
     const int kind = whole ? g.kind : g.act == A_CLIENT ? K_IV : g.act == A_RVIJ ? K_IJ : K_I;
     const std::vector<int> types = kind == K_IV ? std::vector<int>{0, 1} : kind == K_IJ ? std::vector<int>{0, 0}
                                                                                          : std::vector<int>{0};
@@ -394,7 +412,7 @@ void install_guards(rmc_model* m, const std::vector<rmc::tla::GuardSrc>& gs) {
   for (auto& s2 : starts) M.gstart[s2.first] = (int16_t)s2.second;
   for (int q = 0; q < MAXCOMPILED; q++) M.estart[q] = -1;
   for (auto& s2 : estarts) M.estart[s2.first] = (int16_t)s2.second;
-  M.gany = starts.empty() ? 0 : 1;
+  M.gany = starts.empty() && estarts.empty() ? 0 : 1;
   m->guard_srcs = gs;
 }
 
@@ -1302,7 +1320,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
                                            hf_hbm_fraction() * (double)hbm_total) ||
                          getenv("RMC_RECOVER_TO_HOST"));  // test hook
   if (recovering && !rec_host) fcap = std::max(fcap, rc.cur_n);
-  int maxsucc = M.nfixed + M.kmax;
+  int maxsucc = max_successors(M);
   // 8M parents per launch (bench cfg: 1.325 s per check vs 1.349 s at 4M; 4M
   // was 4% below 2M, 2M 4% below 1M), held to 2^31 candidates per launch
   unsigned long long chunk = opt->chunk_parents
@@ -1837,7 +1855,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     nxt = gn.as<uint32_t>();
     restride(cur, cur_n);
     restride(nxt, lvl_next_n);
-    maxsucc = M.nfixed + M.kmax;
+    maxsucc = max_successors(M);
     cand_cap = (chunk + 1024) * (unsigned long long)std::min(maxsucc, 256);
     if (cand_cap > 0xFFFFFFFFULL) throw std::runtime_error("widened rows: more than 2^32 candidates per launch");
     HIPCHK(hipStreamSynchronize(stream));  // the candidate buffer served as the slice buffer
@@ -2637,8 +2655,10 @@ int rmc_model_define_action(rmc_model* m, const char* name, int form, const char
     const int spec = m->M.spec;
     if (spec != RAFT && spec != FLEX && spec != FSYNC)
       throw std::runtime_error("actions compiled whole are offered for Raft, FlexibleRaft and RaftFsync");
-    if (form != K_I && form != K_IV && form != K_IJ)
-      throw std::runtime_error("form must be 0 (\\E i \\in Server), 1 (i \\in Server, v \\in Value) or 2 (i, j \\in Server)");
+    if (form != K_I && form != K_IV && form != K_IJ && form != 3)
+      throw std::runtime_error("form must be 0 (\\E i \\in Server), 1 (i \\in Server, v \\in Value), 2 (i, j \\in "
+                               "Server) or 3 (a message handler, \\E m \\in DOMAIN messages)");
+    const int kind = form == 3 ? K_MSGC : form;
     std::vector<std::string> ps;
     std::string cur;
     for (const char* p = params;; p++) {
@@ -2651,10 +2671,10 @@ int rmc_model_define_action(rmc_model* m, const char* name, int form, const char
         cur += *p;
       }
     }
-    if ((int)ps.size() != (form == K_I ? 1 : 2))
-      throw std::runtime_error(std::string("action ") + name + ": the form binds " + (form == K_I ? "one" : "two") +
-                               " parameters");
-    rmc::tla::GuardSrc g = rmc::tla::parse_action(spec, name, form, ps, body);
+    if ((int)ps.size() != (kind == K_I || kind == K_MSGC ? 1 : 2))
+      throw std::runtime_error(std::string("action ") + name + ": the form binds " +
+                               (kind == K_I || kind == K_MSGC ? "one" : "two") + " parameters");
+    rmc::tla::GuardSrc g = rmc::tla::parse_action(spec, name, kind, ps, body);
     // compile it once now, against this model's constants, so errors show here
     {
       rmc::tla::GuardEnv env;
@@ -2667,8 +2687,12 @@ int rmc_model_define_action(rmc_model* m, const char* name, int form, const char
       env.send_helpers = g.send_helpers;
       const std::vector<int> types = form == K_IV ? std::vector<int>{0, 1} : form == K_IJ ? std::vector<int>{0, 0}
                                                                                          : std::vector<int>{0};
-      (void)rmc::tla::compile_guard(*g.mod, g.params, types, g.conjuncts, env, name);
-      (void)rmc::tla::compile_effect(*g.mod, g.params, types, g.effects, env, name);
+      if (kind == K_MSGC) {
+        (void)rmc::tla::compile_handler(*g.mod, g.params, g.conjuncts, env, name);
+      } else {
+        (void)rmc::tla::compile_guard(*g.mod, g.params, types, g.conjuncts, env, name);
+        (void)rmc::tla::compile_effect(*g.mod, g.params, types, g.effects, env, name);
+      }
     }
     m->defined_actions[name] = g;
     return 0;
@@ -3077,7 +3101,8 @@ int rmc_selftest_random_trace(rmc_model* m, uint64_t seed, int steps) {
     uint64_t x = seed * 0x9E3779B97F4A7C15ULL + 1;
     for (int k = 0; k < steps; k++) {
       std::vector<int> en;
-      for (int b = 0; b < M.nfixed + h_nmsg(s[0]); b++) {
+      for (int x = 0; x < nbindings(M, h_nmsg(s[0])); x++) {
+        const int b = binding_at(M, x, h_nmsg(s[0]));
         int err = 0;
         if (host_eval_apply(M, s.data(), b, t.data(), nullptr, nullptr, &err) == 1 && !err) en.push_back(b);
       }
@@ -3128,9 +3153,10 @@ int rmc_selftest_host_bfs(rmc_model* m, uint32_t kmax, uint64_t max_distinct, ui
       uint64_t gl = 0;
       for (size_t p = 0; p < ncur; p++) {
         const uint32_t* S = cur.data() + p * W;
-        int B = M.nfixed + h_nmsg(S[0]);
+        const int B = nbindings(M, h_nmsg(S[0]));
         succ.clear();
-        for (int b = 0; b < B; b++) {
+        for (int x = 0; x < B; x++) {
+          const int b = binding_at(M, x, h_nmsg(S[0]));
           std::vector<uint32_t> t(W, 0);
           int ord = 0, act = 0, err = 0;
           if (host_eval_apply(M, S, b, t.data(), &ord, &act, &err) != 1) continue;

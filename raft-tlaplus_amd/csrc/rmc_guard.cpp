@@ -34,12 +34,30 @@ namespace rmc {
 namespace tla {
 namespace {
 
-enum Ty { T_INT, T_BOOL, T_SRV, T_VAL, T_STATE, T_ACK, T_SET_SRV, T_SET_VAL, T_SET_STATE, T_NIL, T_TRUE, T_FALSE };
+enum Ty { T_INT, T_BOOL, T_SRV, T_VAL, T_STATE, T_ACK, T_SET_SRV, T_SET_VAL, T_SET_STATE, T_NIL, T_TRUE, T_FALSE,
+          // compiled message handlers: a record type (RequestVoteRequest, ...), a term-match model value
+          // (EqualTerm / LessOrEqualTerm), a message's entries sequence (<<>> or one entry)
+          T_MTYPE, T_TMATCH, T_ENTRIES };
 
 const char* ty_name(Ty t) {
   static const char* n[] = {"an integer", "a boolean", "a server", "a value", "a server state", "an acked value",
-                            "a set of servers", "a set of values", "a set of states", "Nil", "TRUE", "FALSE"};
+                            "a set of servers", "a set of values", "a set of states", "Nil", "TRUE", "FALSE",
+                            "a message type", "a term-match value", "a sequence of entries"};
   return n[t];
+}
+
+// The fields of the Raft family's records (Raft.tla:243-505) a compiled
+// handler reads from its bound message: G_MF operand and type.
+bool msg_field_of(const std::string& f, int& mf, Ty& ty) {
+  static const struct { const char* name; int mf; Ty ty; } t[] = {
+      {"mtype", MF_TYPE, T_MTYPE},          {"mterm", MF_TERM, T_INT},           {"msource", MF_SRC, T_SRV},
+      {"mdest", MF_DST, T_SRV},             {"mvoteGranted", MF_GRANTED, T_BOOL}, {"mlastLogIndex", MF_LLI, T_INT},
+      {"mlastLogTerm", MF_LLT, T_INT},      {"mprevLogIndex", MF_PLI, T_INT},    {"mprevLogTerm", MF_PLT, T_INT},
+      {"mentries", MF_NENT, T_ENTRIES},     {"mcommitIndex", MF_COMMIT, T_INT},  {"msuccess", MF_SUCCESS, T_BOOL},
+      {"mmatchIndex", MF_MIDX, T_INT}};
+  for (auto& x : t)
+    if (f == x.name) { mf = x.mf; ty = x.ty; return true; }
+  return false;
 }
 
 struct Compiler;
@@ -47,10 +65,11 @@ struct Compiler;
 // A name in scope: an action parameter (ARG n), a constant of an unrolled
 // quantifier, or a macro (an operator of the module / LET, inlined at use).
 struct Binding {
-  enum K { ARG, CONSTV, MACRO } k = ARG;
+  enum K { ARG, CONSTV, MACRO, MSG } k = ARG;  // MSG: a compiled handler's bound message
   int v = 0;
   Ty ty = T_INT;
   const Def* def = nullptr;  // MACRO: its definition
+  std::weak_ptr<struct Scope> defsc;  // MACRO from a LET: the scope it was defined in (its body's free names)
   // MACRO arguments bound to expressions in the caller's scope
   std::vector<std::pair<std::string, std::pair<NodeP, std::shared_ptr<struct Scope>>>> args;
 };
@@ -170,6 +189,47 @@ struct Compiler {
 
   Ty sub(const Arg& a) { return expr(a.n, a.sc); }
 
+  // Does n denote the handler's bound message (through operator parameters
+  // and parameterless LET definitions)?
+  bool is_msg(const NodeP& n, ScopeP sc, int depth_ = 0) {
+    if (depth_ > 32 || !n || n->kind != N_ID) return false;
+    if (const Binding* b = sc->find(n->s)) {
+      if (b->k == Binding::MSG) return true;
+      if (b->k == Binding::MACRO && b->def && b->def->params.empty())
+        return is_msg(b->def->body, b->defsc.lock() ? b->defsc.lock() : sc, depth_ + 1);
+      return false;
+    }
+    if (const Arg* a = param(n->s)) {
+      std::vector<std::pair<std::string, Arg>> save = params;
+      while (!params.empty() && &params.back().second != a) params.pop_back();
+      params.pop_back();
+      const bool r = is_msg(a->n, a->sc, depth_ + 1);
+      params = save;
+      return r;
+    }
+    return false;
+  }
+  // Does n denote the bound message's mdest (the server a handler's effects act on)?
+  bool is_mdest(const NodeP& n, ScopeP sc, int depth_ = 0) {
+    if (depth_ > 32 || !n) return false;
+    if (n->kind == N_FIELD && n->s == "mdest") return is_msg(n->k[0], sc);
+    if (n->kind != N_ID) return false;
+    if (const Binding* b = sc->find(n->s)) {
+      if (b->k == Binding::MACRO && b->def && b->def->params.empty())
+        return is_mdest(b->def->body, b->defsc.lock() ? b->defsc.lock() : sc, depth_ + 1);
+      return false;
+    }
+    if (const Arg* a = param(n->s)) {
+      std::vector<std::pair<std::string, Arg>> save = params;
+      while (!params.empty() && &params.back().second != a) params.pop_back();
+      params.pop_back();
+      const bool r = is_mdest(a->n, a->sc, depth_ + 1);
+      params = save;
+      return r;
+    }
+    return false;
+  }
+
   Ty bin_int(const NodeP& n, ScopeP sc, uint32_t op) {
     Ty a = concrete(expr(n->k[0], sc), n), b = concrete(expr(n->k[1], sc), n);
     if (a != T_INT || b != T_INT) fail(n, "arithmetic on " + std::string(ty_name(a)) + " and " + ty_name(b));
@@ -177,6 +237,17 @@ struct Compiler {
     return T_INT;
   }
   Ty compare(const NodeP& n, ScopeP sc, const std::string& op) {
+    {  // m.mentries = <<>> (or /=, #): the message carries no entry
+      const bool e0 = n->k[0]->kind == N_TUPLE && n->k[0]->k.empty(), e1 = n->k[1]->kind == N_TUPLE && n->k[1]->k.empty();
+      if (e0 || e1) {
+        if (concrete(expr(e0 ? n->k[1] : n->k[0], sc), n) != T_ENTRIES) fail(n, "<<>> compared with something other than a message's entries");
+        emit(G_CONST, 0);
+        if (op == "=") emit(G_EQ);
+        else if (op == "/=" || op == "#") emit(G_NE);
+        else fail(n, "order comparison with <<>>");
+        return T_BOOL;
+      }
+    }
     // a symbolic operand takes its code from the other side's type
     const size_t mark = code.size();
     Ty a = expr(n->k[0], sc);
@@ -197,6 +268,7 @@ struct Compiler {
     a = concrete(a, n);
     b = concrete(b, n);
     if (a != b && !(a == T_INT && b == T_INT)) fail(n, std::string("comparison of ") + ty_name(a) + " and " + ty_name(b));
+    if (a == T_ENTRIES) fail(n, "comparison of message entries other than with <<>>");
     if ((op == "<" || op == ">" || op == "<=" || op == ">=") && a != T_INT) fail(n, "order comparison of non-integers");
     if (op == "=") emit(G_EQ);
     else if (op == "/=" || op == "#") emit(G_NE);
@@ -343,7 +415,8 @@ struct Compiler {
         if (const Binding* b = sc->find(s)) {
           if (b->k == Binding::ARG) { emit(G_ARG, b->v); return b->ty; }
           if (b->k == Binding::CONSTV) { emit(G_CONST, b->v); return b->ty; }
-          return inline_def(n, b->def, {}, sc);
+          if (b->k == Binding::MSG) fail(n, "the message " + s + " itself as a value (its fields are read as " + s + ".f)");
+          return inline_def(n, b->def, {}, sc, b->defsc.lock());
         }
         if (const Arg* a = param(s)) {
           // evaluate the argument in its own scope, without the parameters bound after it
@@ -357,6 +430,12 @@ struct Compiler {
         if (s == "TRUE") return T_TRUE;
         if (s == "FALSE") return T_FALSE;
         if (s == "Nil") return T_NIL;
+        if (s == "RequestVoteRequest") { emit(G_CONST, RVREQ); return T_MTYPE; }
+        if (s == "RequestVoteResponse") { emit(G_CONST, RVRESP); return T_MTYPE; }
+        if (s == "AppendEntriesRequest") { emit(G_CONST, AEREQ); return T_MTYPE; }
+        if (s == "AppendEntriesResponse") { emit(G_CONST, AERESP); return T_MTYPE; }
+        if (s == "EqualTerm") { emit(G_CONST, 0); return T_TMATCH; }
+        if (s == "LessOrEqualTerm") { emit(G_CONST, 1); return T_TMATCH; }
         if (s == "Follower") { emit(G_CONST, FOLLOWER); return T_STATE; }
         if (s == "Candidate") { emit(G_CONST, CANDIDATE); return T_STATE; }
         if (s == "Leader") { emit(G_CONST, LEADER); return T_STATE; }
@@ -376,13 +455,18 @@ struct Compiler {
       case N_APP: {
         const std::string& s = n->s;
         if (const Binding* b = sc->find(s))
-          if (b->k == Binding::MACRO) return inline_def(n, b->def, n->k, sc);
+          if (b->k == Binding::MACRO) return inline_def(n, b->def, n->k, sc, b->defsc.lock());
         if (!m.find(s) || sc->find(s)) {
           if (s == "Len" && n->k.size() == 1) {
             Arg x;
             if (!log_of(n->k[0], sc, x)) fail(n, "Len of something other than log[x]");
             if (sub(x) != T_SRV) fail(n, "log indexed by a non-server");
             emit(G_LEN);
+            return T_INT;
+          }
+          if (s == "Len" && n->k.size() == 1 && n->k[0]->kind == N_FIELD && n->k[0]->s == "mentries" &&
+              is_msg(n->k[0]->k[0], sc)) {
+            emit(G_MF, MF_NENT);
             return T_INT;
           }
           if (s == "Cardinality" && n->k.size() == 1) {
@@ -398,6 +482,11 @@ struct Compiler {
       case N_FAPP: {
         if (n->k.size() != 2) fail(n, "function application with several arguments");
         const NodeP& f = n->k[0];
+        if (f->kind == N_ID && f->s == "messages" && !sc->find("messages") && !param("messages")) {
+          if (!is_msg(n->k[1], sc)) fail(n, "messages[x] of something other than the handler's message");
+          emit(G_MF, MF_COUNT);
+          return T_INT;
+        }
         if (f->kind == N_ID && !sc->find(f->s) && !param(f->s)) {
           uint32_t op;
           Ty ty;
@@ -424,8 +513,25 @@ struct Compiler {
         }
         fail(n, "this function application (only the state variables' own indexing is compiled)");
       }
-      case N_FIELD: {  // log[x][k].term / .value
+      case N_FIELD: {  // log[x][k].term / .value, and a compiled handler's m.f / m.mentries[1].term / .value
         const NodeP& e = n->k[0];
+        if (is_msg(e, sc)) {
+          int mf;
+          Ty ty;
+          if (!msg_field_of(n->s, mf, ty)) fail(n, "a message has no field " + n->s);
+          emit(G_MF, mf);
+          return ty;
+        }
+        if (e->kind == N_FAPP && e->k.size() == 2 && e->k[0]->kind == N_FIELD && e->k[0]->s == "mentries" &&
+            is_msg(e->k[0]->k[0], sc) && (n->s == "term" || n->s == "value")) {
+          if (e->k[1]->kind != N_NUM || e->k[1]->s != "1") fail(n, "a message entry other than mentries[1]");
+          emit(G_MF, MF_NENT);  // mentries[1] of <<>>: TLC's evaluation error
+          const size_t ok = jump(G_JNZ);
+          emit(G_ERR);
+          patch(ok);
+          emit(G_MF, n->s == "term" ? MF_ETERM : MF_EVALUE);
+          return n->s == "term" ? T_INT : T_VAL;
+        }
         if (e->kind == N_FAPP && e->k.size() == 2 && (n->s == "term" || n->s == "value")) {
           Arg x;
           if (log_of(e->k[0], sc, x)) {
@@ -500,7 +606,12 @@ struct Compiler {
         Ty et = T_SRV;
         bool first = true;
         for (auto& c : n->k) {
-          Ty t = concrete(expr(c, sc), n);
+          Ty t = expr(c, sc);
+          if (t == T_NIL) {  // {Nil, j} (Raft.tla:372): a set of servers with Nil's code (votedFor's Nil)
+            emit(G_CONST, NILS);
+            t = T_SRV;
+          }
+          t = concrete(t, n);
           if (!first && t != et) fail(n, "set literal of mixed types");
           et = t;
           first = false;
@@ -527,6 +638,7 @@ struct Compiler {
           Binding b;
           b.k = Binding::MACRO;
           b.def = &d;
+          b.defsc = s2;
           s2->names[d.name] = b;
         }
         return expr(n->k[0], s2);
@@ -561,13 +673,16 @@ struct Compiler {
     fail(n, "this construct");
   }
 
-  Ty inline_def(const NodeP& at, const Def* d, const std::vector<NodeP>& args, ScopeP sc) {
+  // (defsc: a LET definition's own scope -- TLA+ LET bodies see the names
+  // bound around them, e.g. a handler's message; a module operator sees none)
+  Ty inline_def(const NodeP& at, const Def* d, const std::vector<NodeP>& args, ScopeP sc, ScopeP defsc = nullptr) {
     if (!d->error.empty()) fail(at, "definition " + d->name + " does not parse: " + d->error);
     if (d->params.size() != args.size()) fail(at, "operator " + d->name + " applied to the wrong number of arguments");
     const size_t base = params.size();
     for (size_t q = 0; q < args.size(); q++) params.push_back({d->params[q], Arg{args[q], sc}});
     // the body sees only its parameters (and the module), not the caller's bound names
     auto s2 = std::make_shared<Scope>();
+    s2->up = defsc;
     Ty t = expr(d->body, s2);
     params.resize(base);
     return t;
@@ -601,7 +716,10 @@ void check_depth(const std::vector<uint32_t>& code, const std::string& where, bo
       case G_END:
         if (guard_end && d < 1) throw std::runtime_error(where + ": empty stack at the end");
         continue;
-      case E_END: continue;
+      case E_END: case G_ERR: continue;  // (G_ERR: the program ends with an evaluation error)
+      case G_MF: delta = 1; break;
+      case E_DISCARD: break;
+      case E_REPLY: need = imm == AERESP ? 5 : 4; delta = -need; break;
       case G_CONST: case G_ARG: case G_ECTR: case G_RCTR: delta = 1; break;
       case G_ST: case G_TERM: case G_VOTED: case G_VOTED2: case G_LEN: case G_COMMIT: case G_FSYNC: case G_VOTES:
       case G_ACKED: case G_NEG: case G_NOT: case G_POPC: need = 1; break;
@@ -651,46 +769,38 @@ std::vector<uint32_t> compile_guard(const Module& m, const std::vector<std::stri
 }
 
 
-// An action's EFFECT compiled for effect_vm (rmc_spec.h): the conjuncts that
-// prime a variable, say UNCHANGED, or send messages, over the same typed
-// expression language as the guards (they read the unprimed state).  Server
-// variables may change at the action's own server only ([v EXCEPT ![i] = e],
-// with @), as every action of these specs does; the forms are those of the
-// specs' fixed-binding actions (Raft.tla:226-313): state, currentTerm,
-// votedFor, votesGranted, commitIndex, electionCtr, restartCtr, acked[v],
-// log[i] = Append(@, [term |-> t, value |-> v]), and SendMultipleOnce of a set
-// of RequestVoteRequest records {[...] : j \in S}.  Every VARIABLE must be
-// assigned, left UNCHANGED or (messages) sent to; anything else is refused
-// naming it.
-std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::string>& action_params,
-                                     const std::vector<int>& param_types, const std::vector<NodeP>& effects,
-                                     const GuardEnv& env, const std::string& where) {
-  Compiler c(m, env);
-  c.where = where;
-  auto fail = [&](const NodeP& n, const std::string& what) -> void {
+namespace {
+// The effect conjuncts of a compiled action, shared by compile_effect (a
+// fixed-binding action: its server is its first parameter) and
+// compile_handler (a message handler: its server is the bound message's
+// mdest).  Each item emits effect_vm stores after the expression machine's
+// code for its values; `done` / `kept` track every VARIABLE (assigned,
+// UNCHANGED) for the completeness check.
+struct EffectGen {
+  Compiler& c;
+  const Module& m;
+  const GuardEnv& env;
+  std::string where;
+  std::function<bool(const NodeP&, ScopeP)> own;  // the action's own server?
+  std::string own_name;                            // ... as the text names it (messages)
+  bool handler = false;                            // a message handler (Discard / Reply allowed)
+  std::set<std::string> vars, done, kept;
+  bool sent = false;
+  EffectGen(Compiler& c_, const Module& m_, const GuardEnv& e_, const std::string& w)
+      : c(c_), m(m_), env(e_), where(w), vars(m_.variables.begin(), m_.variables.end()) {}
+
+  [[noreturn]] void fail(const NodeP& n, const std::string& what) {
     throw std::runtime_error("effect of " + where + " (line " + std::to_string(n ? n->line : 0) + "): " + what);
-  };
-  if (env.spec != RAFT && env.spec != FLEX && env.spec != FSYNC)
-    throw std::runtime_error("effect of " + where + ": the effect compiler knows the Raft, FlexibleRaft and RaftFsync "
-                             "layouts only");
-  auto sc = std::make_shared<Scope>();
-  for (size_t q = 0; q < action_params.size(); q++) {
-    Binding b;
-    b.k = Binding::ARG;
-    b.v = (int)q;
-    b.ty = param_types[q] == 1 ? T_VAL : T_SRV;
-    sc->names[action_params[q]] = b;
   }
-  std::set<std::string> vars(m.variables.begin(), m.variables.end()), done, kept;
-  auto mark = [&](const std::string& v, const NodeP& n) {
+  void mark(const std::string& v, const NodeP& n) {
     if (!vars.count(v)) fail(n, v + " is not a variable of the module");
     if (done.count(v)) fail(n, v + " is changed twice");
     if (kept.count(v)) fail(n, v + " is both changed and UNCHANGED");
     done.insert(v);
-  };
+  }
   // UNCHANGED e: variables, tuples of them, and definitions naming them (a
   // variable may be named twice: RaftFsync.tla:116 lists fsyncIndex twice)
-  std::function<void(const NodeP&, int)> unchanged = [&](const NodeP& n, int depth) {
+  void unchanged(const NodeP& n, int depth) {
     if (depth > 16) fail(n, "UNCHANGED nests too deeply");
     if (n->kind == N_TUPLE) { for (auto& k : n->k) unchanged(k, depth + 1); return; }
     if (n->kind == N_ID) {
@@ -703,9 +813,8 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
       if (d && d->params.empty() && d->body) { unchanged(d->body, depth + 1); return; }
     }
     fail(n, "UNCHANGED of something other than variables");
-  };
-  auto is_param0 = [&](const NodeP& n) { return n->kind == N_ID && !action_params.empty() && n->s == action_params[0]; };
-  auto value = [&](const NodeP& e, Ty want) {
+  }
+  void value(const NodeP& e, Ty want, ScopeP sc) {
     if (e->kind == N_SETENUM && e->k.empty() && (want == T_SET_SRV || want == T_SET_VAL || want == T_SET_STATE)) {
       c.emit(G_CONST, 0);  // {} takes the variable's set type
       return;
@@ -716,21 +825,19 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
       t = want;
     }
     if (t != want) fail(e, std::string("the new value is ") + ty_name(t) + ", the variable holds " + ty_name(want));
-  };
+  }
   // [v EXCEPT ![p] = e]: the single path element and its value
-  auto except1 = [&](const NodeP& rhs, const std::string& v, NodeP& path, NodeP& val) {
+  void except1(const NodeP& rhs, const std::string& v, NodeP& path, NodeP& val) {
     if (rhs->kind != N_EXCEPT || rhs->k.size() != 2 || rhs->k[0]->kind != N_ID || rhs->k[0]->s != v ||
         rhs->paths.size() != 1 || rhs->paths[0].size() != 1 || rhs->paths[0][0].field ||
         rhs->paths[0][0].args.size() != 1)
       fail(rhs, v + "' must be [" + v + " EXCEPT ![x] = e]");
     path = rhs->paths[0][0].args[0];
     val = rhs->k[1];
-  };
-  bool sent = false;
-  std::vector<NodeP> items;
-  for (auto& e : effects) c.flatten(e, "/\\", items);
-  for (auto& n : items) {
-    if (n->kind == N_UNARY && n->s == "UNCHANGED") { unchanged(n->k[0], 0); continue; }
+  }
+  // One effect conjunct; false when n is not one (the caller reports it).
+  bool item(const NodeP& n, ScopeP sc) {
+    if (n->kind == N_UNARY && n->s == "UNCHANGED") { unchanged(n->k[0], 0); return true; }
     if (n->kind == N_BIN && n->s == "=" && n->k[0]->kind == N_PRIME && n->k[0]->k[0]->kind == N_ID) {
       const std::string v = n->k[0]->k[0]->s;
       const NodeP& rhs = n->k[1];
@@ -745,12 +852,13 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
       if (store) {
         NodeP path, val;
         except1(rhs, v, path, val);
-        if (!is_param0(path)) fail(path, v + " may change at the action's own server (" + action_params[0] + ") only");
-        c.at = [&c, load, ty]() { c.emit(G_ARG, 0); c.emit(load); return ty; };
-        value(val, ty);
+        if (!own(path, sc)) fail(path, v + " may change at the action's own server (" + own_name + ") only");
+        Compiler& cc = c;
+        c.at = [&cc, load, ty]() { cc.emit(G_ARG, 0); cc.emit(load); return ty; };
+        value(val, ty, sc);
         c.at = nullptr;
         c.emit(store);
-        continue;
+        return true;
       }
       // the leader's rows: [v EXCEPT ![i] = [j \in Server |-> e]] (unrolled over
       // Server) or [v EXCEPT ![i][q] = e]
@@ -765,15 +873,15 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
             rhs->paths[0][0].args.size() != 1 || (rhs->paths[0].size() == 2 && (rhs->paths[0][1].field ||
                                                                                  rhs->paths[0][1].args.size() != 1)))
           fail(rhs, v + "' must be [" + v + " EXCEPT ![i] = [j \\in Server |-> e]] or [" + v + " EXCEPT ![i][j] = e]");
-        if (!is_param0(rhs->paths[0][0].args[0]))
-          fail(rhs->paths[0][0].args[0], v + " may change at the action's own server (" + action_params[0] + ") only");
+        if (!own(rhs->paths[0][0].args[0], sc))
+          fail(rhs->paths[0][0].args[0], v + " may change at the action's own server (" + own_name + ") only");
         const NodeP& val = rhs->k[1];
         if (rhs->paths[0].size() == 2) {  // one entry: ![i][q] = e
           const NodeP& q = rhs->paths[0][1].args[0];
           if (c.concrete(c.expr(q, sc), q) != T_SRV) fail(q, v + " indexed by a non-server");
-          value(val, rty);
+          value(val, rty, sc);
           c.emit(rstore);
-          continue;
+          return true;
         }
         if (val->kind != N_FUNC || val->bounds.size() != 1 || val->bounds[0].vars.size() != 1 || !val->bounds[0].set ||
             val->bounds[0].set->kind != N_ID || val->bounds[0].set->s != "Server")
@@ -795,48 +903,80 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
           if (t != rty) fail(val->k[0], std::string("the new value is ") + ty_name(t) + ", " + v + " holds " + ty_name(rty));
           c.emit(rstore);
         }
-        continue;
+        return true;
       }
       if (v == "electionCtr" || v == "restartCtr") {
-        value(rhs, T_INT);
+        value(rhs, T_INT, sc);
         c.emit(v == "electionCtr" ? E_ECTR : E_RCTR);
-        continue;
+        return true;
       }
       if (v == "acked") {
         NodeP path, val;
         except1(rhs, v, path, val);
         if (c.concrete(c.expr(path, sc), path) != T_VAL) fail(path, "acked indexed by a non-value");
-        value(val, T_ACK);  // (no @ here: the compiler refuses it)
+        value(val, T_ACK, sc);  // (no @ here: the compiler refuses it)
         c.emit(E_ACKED);
-        continue;
+        return true;
       }
       if (v == "log") {
         NodeP path, val;
         except1(rhs, v, path, val);
-        if (!is_param0(path)) fail(path, "log may change at the action's own server only");
+        if (!own(path, sc)) fail(path, "log may change at the action's own server only");
         const bool app = val->kind == N_APP && val->s == "Append" && val->k.size() == 2 && !m.find("Append");
         const NodeP base = app ? val->k[0] : nullptr;
         const bool on_own = base && (base->kind == N_AT || (base->kind == N_FAPP && base->k.size() == 2 &&
                                                             base->k[0]->kind == N_ID && base->k[0]->s == "log" &&
-                                                            is_param0(base->k[1])));
+                                                            own(base->k[1], sc)));
         if (!app || !on_own) fail(val, "log[i]' must be Append(@, entry) or Append(log[i], entry)");
         const NodeP& rec = val->k[1];
         if (rec->kind != N_RECORD || rec->names.size() != 2) fail(rec, "a log entry is [term |-> t, value |-> v]");
         NodeP tv, vv;
         for (size_t q = 0; q < 2; q++) (rec->names[q] == "term" ? tv : vv) = rec->k[q];
         if (!tv || !vv) fail(rec, "a log entry is [term |-> t, value |-> v]");
-        value(tv, T_INT);
-        value(vv, T_VAL);
+        value(tv, T_INT, sc);
+        value(vv, T_VAL, sc);
         c.emit(E_APPEND);
-        continue;
+        return true;
       }
       fail(n, "the effect compiler does not assign " + v + " (it may stay UNCHANGED)");
     }
     // the bag helpers (the lowering checked each is the family's own, by closure
     // hash): a set of RequestVoteRequest records {[...] : j \in S} sent all new
-    // (class 0), or one record sent new (1) or with its count + 1 (2)
-    if (n->kind == N_APP && n->k.size() == 1 && env.send_helpers.count(n->s)) {
+    // (class 0), or one record sent new (1) or with its count + 1 (2); in a
+    // message handler, Discard(m) (3) and Reply(response, m) (4)
+    if (n->kind == N_APP && env.send_helpers.count(n->s)) {
       const int cls = env.send_helpers.at(n->s);
+      if (cls >= 3) {
+        if (!handler) fail(n, n->s + " outside a message handler (no bound message)");
+        if (n->k.size() != (cls == 3 ? 1u : 2u) || !c.is_msg(n->k.back(), sc))
+          fail(n, n->s + " of something other than the handler's message");
+        if (sent) fail(n, "messages are changed twice");
+        sent = true;
+        mark("messages", n);
+        if (cls == 3) {
+          c.emit(E_DISCARD);
+          return true;
+        }
+        const NodeP& rec = n->k[0];
+        if (rec->kind != N_RECORD) fail(rec, "Reply of something other than a record literal");
+        std::map<std::string, NodeP> f;
+        for (size_t q = 0; q < rec->names.size(); q++) f[rec->names[q]] = rec->k[q];
+        const bool rv = f.size() == 5 && f.count("mtype") && f["mtype"]->kind == N_ID &&
+                        f["mtype"]->s == "RequestVoteResponse" && f.count("mterm") && f.count("mvoteGranted") &&
+                        f.count("msource") && f.count("mdest");
+        const bool ae = f.size() == 6 && f.count("mtype") && f["mtype"]->kind == N_ID &&
+                        f["mtype"]->s == "AppendEntriesResponse" && f.count("mterm") && f.count("msuccess") &&
+                        f.count("mmatchIndex") && f.count("msource") && f.count("mdest");
+        if (!rv && !ae) fail(rec, "the handler compiler replies with RequestVoteResponse or AppendEntriesResponse records");
+        auto field = [&](const char* name, Ty t) { value(f[name], t, sc); };
+        field("mterm", T_INT);
+        field(rv ? "mvoteGranted" : "msuccess", T_BOOL);
+        if (ae) field("mmatchIndex", T_INT);
+        field("msource", T_SRV);
+        field("mdest", T_SRV);
+        c.emit(E_REPLY, rv ? RVRESP : AERESP);
+        return true;
+      }
       if (sent) fail(n, "messages are sent twice");
       sent = true;
       mark("messages", n);
@@ -868,7 +1008,7 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
       };
       if (cls != 0) {
         send(sc);
-        continue;
+        return true;
       }
       const std::string jv = S->bounds[0].vars[0];
       // TLC's set {rec : j \in S} holds each distinct record once; one E_RVREQ
@@ -896,15 +1036,225 @@ std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::str
         send(s2);
         c.patch(skip);
       }
-      continue;
+      return true;
     }
-    fail(n, "this effect conjunct (the effect compiler knows v' = ..., UNCHANGED and the module's send helpers)");
+    return false;
   }
-  for (const std::string& v : vars)
-    if (!done.count(v) && !kept.count(v))
-      throw std::runtime_error("effect of " + where + ": " + v + " is neither assigned nor UNCHANGED");
+  // every VARIABLE assigned, UNCHANGED or (messages) sent to
+  void complete() {
+    for (const std::string& v : vars)
+      if (!done.count(v) && !kept.count(v))
+        throw std::runtime_error("effect of " + where + ": " + v + " is neither assigned nor UNCHANGED");
+  }
+};
+}  // namespace
+
+// An action's EFFECT compiled for effect_vm (rmc_spec.h): the conjuncts that
+// prime a variable, say UNCHANGED, or send messages, over the same typed
+// expression language as the guards (they read the unprimed state).  Server
+// variables may change at the action's own server only ([v EXCEPT ![i] = e],
+// with @), as every action of these specs does; the forms are those of the
+// specs' fixed-binding actions (Raft.tla:226-313): state, currentTerm,
+// votedFor, votesGranted, commitIndex, electionCtr, restartCtr, acked[v],
+// log[i] = Append(@, [term |-> t, value |-> v]), and SendMultipleOnce of a set
+// of RequestVoteRequest records {[...] : j \in S}.  Every VARIABLE must be
+// assigned, left UNCHANGED or (messages) sent to; anything else is refused
+// naming it.
+std::vector<uint32_t> compile_effect(const Module& m, const std::vector<std::string>& action_params,
+                                     const std::vector<int>& param_types, const std::vector<NodeP>& effects,
+                                     const GuardEnv& env, const std::string& where) {
+  Compiler c(m, env);
+  c.where = where;
+  if (env.spec != RAFT && env.spec != FLEX && env.spec != FSYNC)
+    throw std::runtime_error("effect of " + where + ": the effect compiler knows the Raft, FlexibleRaft and RaftFsync "
+                             "layouts only");
+  auto sc = std::make_shared<Scope>();
+  for (size_t q = 0; q < action_params.size(); q++) {
+    Binding b;
+    b.k = Binding::ARG;
+    b.v = (int)q;
+    b.ty = param_types[q] == 1 ? T_VAL : T_SRV;
+    sc->names[action_params[q]] = b;
+  }
+  EffectGen g(c, m, env, where);
+  g.own_name = action_params.empty() ? "?" : action_params[0];
+  g.own = [&](const NodeP& n, ScopeP) { return n->kind == N_ID && !action_params.empty() && n->s == action_params[0]; };
+  std::vector<NodeP> items;
+  for (auto& e : effects) c.flatten(e, "/\\", items);
+  for (auto& n : items)
+    if (!g.item(n, sc))
+      g.fail(n, "this effect conjunct (the effect compiler knows v' = ..., UNCHANGED and the module's send helpers)");
+  g.complete();
   c.emit(E_END);
   check_depth(c.code, "effect of " + where);
+  return c.code;
+}
+
+// A message handler compiled whole (K_MSGC): the body of \E m \in DOMAIN
+// messages : body as ONE effect_vm program, its conjuncts in the text's order
+// -- a guard conjunct jumps to the disabled exit when false, an effect
+// conjunct stores into the successor -- so a guard after an effect still
+// disables (the partial successor is dropped).  The effects act on the bound
+// message's mdest (effect_vm's server i, what the reference handlers name
+// LET i == m.mdest, Raft.tla:364, :388, :416): an EXCEPT path must denote
+// m.mdest.  LET definitions are macros; an operator of the module whose body
+// has effects is inlined; a disjunction of effects is taken when it has two
+// branches whose leading guards are complementary (p and ~p, x = y and
+// x # y), each branch's guards before its effects -- the form of
+// Raft.tla:375-376 and :394-397; any other disjunction of effects would give
+// TLC one successor per true branch and is refused.
+std::vector<uint32_t> compile_handler(const Module& m, const std::vector<std::string>& params,
+                                      const std::vector<NodeP>& body, const GuardEnv& env, const std::string& where) {
+  Compiler c(m, env);
+  c.where = where;
+  if (env.spec != RAFT && env.spec != FLEX && env.spec != FSYNC)
+    throw std::runtime_error("handler " + where + ": the handler compiler knows the Raft, FlexibleRaft and RaftFsync "
+                             "layouts only");
+  if (params.size() != 1) throw std::runtime_error("handler " + where + ": binds one message");
+  auto sc = std::make_shared<Scope>();
+  {
+    Binding b;
+    b.k = Binding::MSG;
+    sc->names[params[0]] = b;
+  }
+  EffectGen g(c, m, env, where);
+  g.handler = true;
+  g.own_name = params[0] + ".mdest";
+  g.own = [&c](const NodeP& n, ScopeP s2) { return c.is_mdest(n, s2); };
+  auto fail = [&](const NodeP& n, const std::string& what) -> void { g.fail(n, what); };
+  // does n change the state (a prime, UNCHANGED, a bag helper, or an operator of the module whose body does)?
+  std::function<bool(const NodeP&, int)> effectful = [&](const NodeP& n, int depth) -> bool {
+    if (!n || depth > 64) return false;
+    if (n->kind == N_PRIME) return true;
+    if (n->kind == N_UNARY && n->s == "UNCHANGED") return true;
+    if ((n->kind == N_APP || n->kind == N_ID) && env.send_helpers.count(n->s)) return true;
+    if ((n->kind == N_APP || n->kind == N_ID) && !sc->find(n->s)) {
+      const Def* d = m.find(n->s);
+      if (d && d->error.empty() && d->body && effectful(d->body, depth + 1)) return true;
+    }
+    for (auto& k : n->k)
+      if (effectful(k, depth + 1)) return true;
+    for (auto& d : n->defs)
+      if (effectful(d.body, depth + 1)) return true;
+    return false;
+  };
+  // structural equality (the complementary-guard test)
+  std::function<bool(const NodeP&, const NodeP&)> same = [&](const NodeP& a, const NodeP& b) -> bool {
+    if (!a || !b) return a == b;
+    if (a->kind != b->kind || a->s != b->s || a->k.size() != b->k.size() || a->names != b->names) return false;
+    for (size_t q = 0; q < a->k.size(); q++)
+      if (!same(a->k[q], b->k[q])) return false;
+    return true;
+  };
+  auto negation_of = [&](const NodeP& a, const NodeP& b) {  // b == ~a (or a and b a complementary comparison)
+    if (b->kind == N_UNARY && (b->s == "~" || b->s == "\\lnot" || b->s == "\\neg") && same(a, b->k[0])) return true;
+    const bool ca = a->kind == N_BIN && a->s == "=", cb = b->kind == N_BIN && (b->s == "#" || b->s == "/=");
+    return ca && cb && same(a->k[0], b->k[0]) && same(a->k[1], b->k[1]);
+  };
+  std::vector<size_t> disabled;  // jumps to the disabled exit
+  std::function<void(const NodeP&, ScopeP, std::vector<size_t>&)> stmt;
+  auto guard = [&](const NodeP& n, ScopeP s2, std::vector<size_t>& exits) {
+    const Ty t = c.concrete(c.expr(n, s2), n);
+    if (t != T_BOOL) fail(n, std::string("a guard conjunct is ") + ty_name(t));
+    exits.push_back(c.jump(G_JZ));
+  };
+  stmt = [&](const NodeP& n, ScopeP s2, std::vector<size_t>& exits) {
+    if ((n->kind == N_JUNCT || n->kind == N_BIN) && (n->s == "/\\" || n->s == "\\land")) {
+      std::vector<NodeP> items;
+      c.flatten(n, n->s, items);
+      for (auto& x : items) stmt(x, s2, exits);
+      return;
+    }
+    if (!effectful(n, 0)) { guard(n, s2, exits); return; }
+    if (n->kind == N_LET) {
+      auto s3 = std::make_shared<Scope>();
+      s3->up = s2;
+      for (auto& d : n->defs) {
+        Binding b;
+        b.k = Binding::MACRO;
+        b.def = &d;
+        b.defsc = s3;
+        s3->names[d.name] = b;
+      }
+      stmt(n->k[0], s3, exits);
+      return;
+    }
+    if ((n->kind == N_JUNCT || n->kind == N_BIN) && (n->s == "\\/" || n->s == "\\lor")) {
+      std::vector<NodeP> br;
+      c.flatten(n, n->s, br);
+      if (br.size() != 2) fail(n, "a disjunction of effects with other than two branches");
+      std::vector<NodeP> items[2], guards[2];
+      for (int q = 0; q < 2; q++) {
+        c.flatten(br[q], "/\\", items[q]);
+        bool eff = false;
+        for (auto& x : items[q]) {
+          if (effectful(x, 0)) eff = true;
+          else if (eff) fail(x, "a guard after an effect inside a disjunction of effects");
+          else guards[q].push_back(x);
+        }
+      }
+      if (guards[0].size() != 1 || guards[1].size() != 1 ||
+          !(negation_of(guards[0][0], guards[1][0]) || negation_of(guards[1][0], guards[0][0])))
+        fail(n, "a disjunction of effects whose branches do not start with complementary guards (p and ~p): TLC "
+                "would take every branch whose guard holds");
+      const auto d0 = g.done, k0 = g.kept;
+      const bool s0 = g.sent;
+      std::set<std::string> cover[2], chg[2];
+      bool snt[2];
+      std::vector<size_t> to_next, to_end;
+      for (int q = 0; q < 2; q++) {
+        g.done = d0;
+        g.kept = k0;
+        g.sent = s0;
+        std::vector<size_t>& gx = q == 0 ? to_next : exits;  // branch 0's guard false: try branch 1
+        guard(guards[q][0], s2, gx);
+        for (size_t x = 1; x < items[q].size(); x++)
+          if (!g.item(items[q][x], s2)) fail(items[q][x], "this effect conjunct");
+        chg[q] = g.done;
+        cover[q] = g.done;
+        cover[q].insert(g.kept.begin(), g.kept.end());
+        snt[q] = g.sent;
+        if (q == 0) {
+          to_end.push_back(c.jump(G_JMP));
+          for (size_t x : to_next) c.patch(x);
+        }
+      }
+      for (size_t x : to_end) c.patch(x);
+      for (const std::string& v : g.vars)
+        if (!d0.count(v) && !k0.count(v) && cover[0].count(v) != cover[1].count(v))
+          fail(n, v + " is assigned or UNCHANGED in one branch of the disjunction only");
+      g.done = chg[0];
+      g.done.insert(chg[1].begin(), chg[1].end());
+      g.kept = k0;
+      for (const std::string& v : cover[0])
+        if (cover[1].count(v) && !g.done.count(v)) g.kept.insert(v);
+      g.sent = snt[0] || snt[1];
+      return;
+    }
+    if ((n->kind == N_APP || n->kind == N_ID) && !env.send_helpers.count(n->s) && !s2->find(n->s) &&
+        m.find(n->s)) {  // an operator of the module with effects: inlined
+      const Def* d = m.find(n->s);
+      if (!d->error.empty()) fail(n, "definition " + d->name + " does not parse: " + d->error);
+      const std::vector<NodeP> args = n->kind == N_APP ? n->k : std::vector<NodeP>{};
+      if (d->params.size() != args.size()) fail(n, "operator " + d->name + " applied to the wrong number of arguments");
+      const size_t base = c.params.size();
+      for (size_t q = 0; q < args.size(); q++) c.params.push_back({d->params[q], Arg{args[q], s2}});
+      // the body sees its parameters and the module only (the message through a parameter)
+      stmt(d->body, std::make_shared<Scope>(), exits);
+      c.params.resize(base);
+      return;
+    }
+    if (!g.item(n, s2))
+      fail(n, "this effect conjunct (the handler compiler knows v' = ..., UNCHANGED, Discard, Reply, the send "
+              "helpers, LET and a two-way disjunction of effects)");
+  };
+  for (auto& n : body) stmt(n, sc, disabled);
+  g.complete();
+  c.emit(E_END);
+  for (size_t x : disabled) c.patch(x);  // the disabled exit: no successor
+  c.emit(G_CONST, 0);
+  c.emit(G_END);
+  check_depth(c.code, "handler " + where);
   return c.code;
 }
 

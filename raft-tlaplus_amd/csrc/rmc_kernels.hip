@@ -583,6 +583,20 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           }
         }
       }
+      if constexpr (G) {
+        // compiled message handlers (rmc_guard.cpp compile_handler): every DOMAIN
+        // element, each handler on its own (no live-message prefilter: the
+        // compiled guard alone decides)
+        for (int c = 0; c < cM.nmsgc; c++) {
+          const int q = cM.msgc_q[c];
+          const int off = sMOff[A_C0 + q];
+          for (int k = 0; k < nm; k++)
+            if ((t++ & (bstride - 1)) == w0) {
+              Delta d;
+              if (eval_msgc<SPEC, N>(s, cM, q, k, off + k, d)) record(p, cM.nfixed + MSGC_STRIDE * (1 + q) + k, d);
+            }
+        }
+      }
     }
   }
   __syncthreads();
@@ -1818,18 +1832,20 @@ __global__ __launch_bounds__(SIM_BLOCK) void k_simulate(const uint32_t* __restri
   // the round's counts and its reported failure are then a function of the seed
   for (; steps < depth; steps++) {
     PState<SPEC, N> s{cur};
-    const int B = cM.nfixed + s.nmsg();
+    const int nm = s.nmsg(), B = nbindings(cM, nm);
     int cnt = 0;
-    for (int b = 0; b < B; b++) {
+    for (int x = 0; x < B; x++) {
       Delta d;
-      if (eval_binding<SPEC, N, SPEC != KRAFT>(s, cM, b, d)) cnt++;
+      if (eval_binding<SPEC, N, SPEC != KRAFT>(s, cM, binding_at(cM, x, nm), d)) cnt++;
     }
     if (!cnt) break;  // no successor: the behaviour ends (-deadlock)
     int r = (int)(splitmix(rng) % (unsigned long long)cnt);
     Delta d;
     int b = 0;
-    for (; b < B; b++)
+    for (int x = 0; x < B; x++) {
+      b = binding_at(cM, x, nm);
       if (eval_binding<SPEC, N, SPEC != KRAFT>(s, cM, b, d) && r-- == 0) break;
+    }
     binds[w * depth + steps] = (uint16_t)b;
     if (d.err) {  // an evaluation error in Next (TLC stops with an error)
       atomicMin(&ss->key, (w << 20) | ((unsigned long long)(steps + 1) << 2) | 2ULL);

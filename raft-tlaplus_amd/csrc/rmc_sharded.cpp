@@ -556,7 +556,7 @@ static int check_sharded_impl(rmc_model* m, const rmc_options* opt, Comm& comm, 
   const int W = comm.world;
   const size_t WD = (size_t)M.words;
   res->state_bytes = (uint32_t)(WD * 4);
-  const int maxsucc = M.nfixed + M.kmax;
+  const int maxsucc = max_successors(M);
   const unsigned long long CH = opt->chunk_parents ? opt->chunk_parents : (1ULL << 22);
   const unsigned long long cand_cap = CH * (unsigned long long)std::min(maxsucc, 256);
   const int NL = (int)comm.local.size();

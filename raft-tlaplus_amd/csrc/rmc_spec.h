@@ -80,7 +80,13 @@ constexpr int MAXCOMPILED = 4;
 // handler ranging over DOMAIN messages with one enabled action per element (K_MSG), and an action bound
 // by \E m \in DOMAIN messages that is NOT exclusive with the handlers (K_M: its bindings are fixed
 // bindings, one per message slot k = x, encoded in a fixed binding's (i, jv) as k & 15, k >> 4)
-enum ActKind { K_I = 0, K_IV = 1, K_IJ = 2, K_MSG = 3, K_M = 4 };
+// bindings, one per message slot k = x, encoded in a fixed binding's (i, jv) as k & 15, k >> 4), and a
+// message handler the front end compiles whole (K_MSGC, rmc_guard.cpp compile_handler): evaluated on every
+// DOMAIN element on its own (not assumed exclusive with the library's handlers), its binding for slot k is
+// nfixed + MSGC_STRIDE * (1 + q) + k for compiled action A_C0 + q -- independent of the slot count, so trace
+// records written before a widening keep their meaning
+enum ActKind { K_I = 0, K_IV = 1, K_IJ = 2, K_MSG = 3, K_M = 4, K_MSGC = 5 };
+constexpr int MSGC_STRIDE = 128;
 enum ErrCode {
   E_NONE = 0,
   E_DOMAIN = 1,     // TLC evaluation error: sequence applied outside its domain
@@ -128,8 +134,23 @@ struct Model {
   // action A_C0 + k's effect program in gcode (its guard is at gstart[A_C0 + k])
   int16_t estart[MAXCOMPILED];
   int gany;  // some action has a compiled guard (or is compiled whole)
+  // compiled message handlers (K_MSGC): how many, and each one's compiled-action index q (A_C0 + q)
+  int nmsgc;
+  int8_t msgc_q[MAXCOMPILED];
   uint32_t gcode[MAXGCODE];
 };
+// Bindings a parent with nm DOMAIN elements has, and the idx-th of them: the
+// fixed bindings, one per DOMAIN element for the library's handlers, then one
+// per element for each compiled handler (host loops; the order is immaterial,
+// successors are ordered by their TLC ordinal).
+RMC_HD int nbindings(const Model& M, int nm) { return M.nfixed + nm * (1 + M.nmsgc); }
+RMC_HD int binding_at(const Model& M, int idx, int nm) {
+  if (idx < M.nfixed + nm) return idx;
+  const int r = idx - M.nfixed - nm;
+  return M.nfixed + MSGC_STRIDE * (1 + M.msgc_q[r / nm]) + r % nm;
+}
+// Successors one parent can have at most (the candidate buffers' bound).
+RMC_HD int max_successors(const Model& M) { return M.nfixed + M.kmax * (1 + M.nmsgc); }
 
 // ------------------------------------------------------------- bit helpers
 RMC_HD uint32_t getb(uint32_t w, int pos, int width) { return (w >> pos) & ((1u << width) - 1u); }
@@ -1011,6 +1032,7 @@ enum GOp : uint32_t {
   G_JMP,       // jump imm
   G_POP,
   G_ERR,       // evaluation error
+  G_MF,        // -> field imm of the bound message (compiled message handlers; MF_* below)
   // effect programs only (effect_vm): store the top of the stack into the
   // successor -- server i's (the action's first bound variable) fields, the
   // header's counters and acked, a log entry appended to log[i], a
@@ -1029,10 +1051,37 @@ enum GOp : uint32_t {
   E_PEND,      // j b -> pendingResponse[i][j]' = b
   E_RVREQ,     // term llt lli src dst -> the RequestVoteRequest record, sent new (imm 0: disabled if in
                // DOMAIN) or counted (imm 1: _SendNoRestriction)
+  E_DISCARD,   // Discard(m): the bound message's count - 1 (Raft.tla:164-167; its count > 0 is the guard's)
+  E_REPLY,     // Reply(response, m) (Raft.tla:170-176), imm = response type: RequestVoteResponse
+               // (term granted src dst) or AppendEntriesResponse (term success matchIndex src dst)
   E_END,       // the successor is complete
   G_NUM
 };
 RMC_HD uint32_t g_ins(uint32_t op, int imm = 0) { return op | ((uint32_t)imm << 8); }
+// G_MF fields of a Raft-family record (rmc_spec.h MsgF; the compiler's types in rmc_guard.cpp)
+enum MsgField { MF_TYPE = 0, MF_TERM, MF_SRC, MF_DST, MF_COUNT, MF_GRANTED, MF_LLI, MF_LLT, MF_PLI, MF_PLT, MF_NENT,
+                MF_ETERM, MF_EVALUE, MF_COMMIT, MF_SUCCESS, MF_MIDX, MF_NUM };
+RMC_HD int msg_field(const MsgF& m, int f) {
+  switch (f) {
+    case MF_TYPE: return m.type;
+    case MF_TERM: return m.term;
+    case MF_SRC: return m.src;
+    case MF_DST: return m.dst;
+    case MF_COUNT: return m.count;
+    case MF_GRANTED: return m.granted;
+    case MF_LLI: return m.lli;
+    case MF_LLT: return m.llt;
+    case MF_PLI: return m.pli;
+    case MF_PLT: return m.plt;
+    case MF_NENT: return m.nent;
+    case MF_ETERM: return m.eterm;
+    case MF_EVALUE: return m.evalue;
+    case MF_COMMIT: return m.commit;
+    case MF_SUCCESS: return m.success;
+    case MF_MIDX: return m.midx;
+  }
+  return 0;
+}
 // The stack lives in eight registers, shifted on push and pop (a dynamically
 // indexed array would put it in scratch memory, and a real call would make
 // every kernel that can reach it save its live registers around it: the
@@ -1043,8 +1092,10 @@ RMC_HD uint32_t g_ins(uint32_t op, int imm = 0) { return op | ((uint32_t)imm << 
 // the header, the message ops).  Returns 1 (enabled; d complete at E_END),
 // 0 (disabled: a SendMultipleOnce message already in DOMAIN) or -1 (a TLC
 // evaluation error); a value past the packed layout's field sets d.err.
+// mk: the DOMAIN slot of the bound message of a compiled message handler
+// (G_MF, E_DISCARD, E_REPLY), -1 otherwise.
 template <int SPEC, int N, bool EFF>
-RMC_HD int vm_run(const uint32_t* S, const Model& M, int pc, int i, int jv, Delta& d) {
+RMC_HD int vm_run(const uint32_t* S, const Model& M, int pc, int i, int jv, Delta& d, int mk = -1) {
   int t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0, t6 = 0, t7 = 0;
   const PState<SPEC, N> s{S};
   uint32_t ea = 0, eb = 0, eh = 0;  // effects: server i's words A and B, the header
@@ -1107,6 +1158,10 @@ RMC_HD int vm_run(const uint32_t* S, const Model& M, int pc, int i, int jv, Delt
       case G_JNZ: { const int c_ = t0; GPOP(); if (c_) pc += imm; break; }
       case G_JMP: pc += imm; break;
       case G_POP: GPOP(); break;
+      case G_MF:  // decoded at each use: no record held in registers across the program
+        if (mk < 0) return -1;
+        GPUSH(msg_field(msg_decode<SPEC>(s.msg(mk)), imm));
+        break;
       default:
         if constexpr (EFF) {
           switch (op) {
@@ -1162,6 +1217,34 @@ RMC_HD int vm_run(const uint32_t* S, const Model& M, int pc, int i, int jv, Delt
               }
               break;
             }
+            case E_DISCARD:
+              if (mk < 0 || !(msg_count(s.msg(mk)) > 0)) return 0;
+              op_discard(s, d, mk);
+              break;
+            case E_REPLY: {  // stack: term flag [matchIndex] src dst (dst on top)
+              MsgF r = msg_zero();
+              r.type = imm;
+              r.count = 1;
+              r.src = t1 & 7;
+              r.dst = t0 & 7;
+              GPOP();
+              GPOP();
+              if (imm == AERESP) {
+                r.midx = t0;
+                r.success = t1 & 1;
+                r.term = t2;
+                GPOP(); GPOP(); GPOP();
+              } else {
+                r.granted = t0 & 1;
+                r.term = t1;
+                GPOP(); GPOP();
+              }
+              if (r.term < 0 || r.term > 15) { d.err = E_CAP_TERM; return 1; }
+              if (r.midx < 0 || r.midx > 7) { d.err = E_CAP_FIELD; return 1; }
+              if (mk < 0 || !op_reply(s, d, msg_encode<SPEC>(r), mk)) return 0;
+              if (d.err) return 1;
+              break;
+            }
             case E_END:
               d.w[0] = ea;
               d.w[1] = eb;
@@ -1186,8 +1269,8 @@ RMC_HD int guard_vm(const uint32_t* S, const Model& M, int pc, int i, int jv) {
   return vm_run<SPEC, N, false>(S, M, pc, i, jv, unused);
 }
 template <int SPEC, int N>
-RMC_HD int effect_vm(const PState<SPEC, N>& s, const Model& M, int pc, int i, int jv, Delta& d) {
-  return vm_run<SPEC, N, true>(s.S, M, pc, i, jv, d);
+RMC_HD int effect_vm(const PState<SPEC, N>& s, const Model& M, int pc, int i, int jv, Delta& d, int mk = -1) {
+  return vm_run<SPEC, N, true>(s.S, M, pc, i, jv, d, mk);
 }
 
 template <int SPEC, int N>
@@ -1622,6 +1705,24 @@ RMC_HD bool act_message(const PState<SPEC, N>& s, const Model& M, int k, Delta& 
   return act_message_any<SPEC, N>(s, M, k, d) && ((M.msg_act_mask >> d.act) & 1ULL);
 }
 
+// A compiled message handler (K_MSGC, rmc_guard.cpp compile_handler) on
+// DOMAIN element k: one program -- its guard conjuncts and its effects, in the
+// text's order -- run with i = the message's mdest and jv = its msource (what
+// the reference handlers' LET i == m.mdest, j == m.msource name).
+template <int SPEC, int N>
+RMC_HD bool eval_msgc(const PState<SPEC, N>& s, const Model& M, int q, int k, int ordinal, Delta& d) {
+  d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
+  d.act = A_C0 + q;
+  d.ordinal = ordinal;
+  if (k >= s.nmsg()) return false;
+  uint32_t w = s.msg(k);
+  int sp, dp;
+  msg_srcdst_pos<SPEC>(w, sp, dp);
+  const int e = effect_vm<SPEC, N>(s, M, M.estart[q], (int)((w >> dp) & 7u), (int)((w >> sp) & 7u), d, k);
+  if (e < 0) { d.err = E_DOMAIN; return true; }
+  return e != 0;
+}
+
 // A fixed binding given as (action id, its bound server i, its second bound
 // variable jv) with its TLC ordinal already known: no table lookups, so a lane
 // with its own binding issues no dependent loads before the action's guard.
@@ -1694,6 +1795,12 @@ RMC_HD bool eval_known(const PState<SPEC, N>& s, const Model& M, int b, uint32_t
   if (b < M.nfixed)
     return eval_fixed_id<SPEC, N, G>(s, M, (int)((desc >> 16) & 0xFFu), (int)((desc >> 24) & 15u), (int)(desc >> 28),
                                      ordinal, d);
+  if constexpr (G) {
+    if (b >= M.nfixed + MSGC_STRIDE) {
+      const int r = b - M.nfixed - MSGC_STRIDE;
+      return eval_msgc<SPEC, N>(s, M, r / MSGC_STRIDE, r % MSGC_STRIDE, ordinal, d);
+    }
+  }
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   d.act = -1;
   const bool en = act_message(s, M, b - M.nfixed, d);
@@ -1705,6 +1812,12 @@ RMC_HD bool eval_known(const PState<SPEC, N>& s, const Model& M, int b, uint32_t
 template <int SPEC, int N, bool G = RMC_G_DEFAULT>
 RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta& d) {
   if (b < M.nfixed) return eval_fixed<SPEC, N, G>(s, M, M.fb_act[b], M.fb_x[b], d);
+  if constexpr (G) {
+    if (b >= M.nfixed + MSGC_STRIDE) {
+      const int r = b - M.nfixed - MSGC_STRIDE, q = r / MSGC_STRIDE, k = r % MSGC_STRIDE;
+      return eval_msgc<SPEC, N>(s, M, q, k, M.act_off[M.msg_act_slot[A_C0 + q]] + k, d);
+    }
+  }
   d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0;
   int k = b - M.nfixed;
   d.act = -1;

@@ -1158,6 +1158,65 @@ Lowering lower(const std::string& text, const std::string& next, const std::stri
         continue;
       }
     }
+    if (!k && (L.spec == RAFT || L.spec == FLEX || L.spec == FSYNC) && (dj.form == B_MSG || dj.form == B_M)) {
+      // a message handler compiled whole (rmc_guard.cpp compile_handler): the
+      // bare action's body \E m \in DOMAIN messages : body (Raft.tla:384-401),
+      // or the operator A of \E m \in DOMAIN messages : A(m)
+      const Def* d = m.find(dj.op);
+      GuardSrc gs;
+      if (dj.form == B_MSG) {
+        const NodeP& b = d->body;
+        if (!d->params.empty() || !b || b->kind != N_QUANT || b->s != "\\E" || b->bounds.size() != 1 ||
+            b->bounds[0].vars.size() != 1 || !b->bounds[0].set || b->bounds[0].set->kind != N_UNARY ||
+            b->bounds[0].set->s != "DOMAIN" || b->bounds[0].set->k[0]->kind != N_ID ||
+            b->bounds[0].set->k[0]->s != "messages")
+          throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") is neither a "
+                                   "lowered handler nor of the form \\E m \\in DOMAIN messages : body");
+        gs.params = b->bounds[0].vars;
+        gs.conjuncts = {b->k[0]};
+      } else {
+        if (d->params.size() != 1)
+          throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + "): a handler "
+                                   "bound by \\E m \\in DOMAIN messages takes one parameter");
+        gs.params = d->params;
+        gs.conjuncts = {d->body};
+      }
+      int ncomp = 0;
+      for (const GuardSrc& q : L.guards) ncomp += q.act >= A_C0;
+      if (ncomp >= MAXCOMPILED)
+        throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + "): more than " +
+                                 std::to_string(MAXCOMPILED) + " actions to compile");
+      // the bag helpers it may call are the family's own (by closure hash); a
+      // redefined one is refused where it is used
+      std::map<std::string, int> helpers;
+      std::set<std::string> redefined;
+      for (const Known& q : kKnown)
+        if (q.spec == L.spec && q.role == R_HELPER && m.find(q.name)) {
+          if (hash_of(q.name) == q.hash) helpers[q.name] = q.id;
+          else redefined.insert(q.name);
+        }
+      std::set<std::string> seen;
+      std::function<void(const NodeP&, int)> uses = [&](const NodeP& n, int depth) {
+        if (!n || depth > 64) return;
+        if ((n->kind == N_APP || n->kind == N_ID) && redefined.count(n->s))
+          throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") calls " + n->s +
+                                   ", which is not the " + spec_name(L.spec) + " module's own bag helper");
+        if ((n->kind == N_APP || n->kind == N_ID) && !helpers.count(n->s) && seen.insert(n->s).second)
+          if (const Def* od = m.find(n->s)) uses(od->body, depth + 1);
+        for (auto& c : n->k) uses(c, depth + 1);
+        for (auto& dd : n->defs) uses(dd.body, depth + 1);
+      };
+      for (auto& c : gs.conjuncts) uses(c, 0);
+      gs.send_helpers = helpers;
+      gs.act = A_C0 + ncomp;
+      gs.op = dj.op;
+      gs.kind = K_MSGC;
+      gs.mod = mp;
+      L.guards.push_back(gs);
+      L.actions.push_back({gs.act, gs.kind});
+      L.labels.push_back(dj.op);
+      continue;
+    }
     if (!k)
       throw std::runtime_error("Next disjunct " + dj.op + " (line " + std::to_string(dj.line) + ") computes an action "
                                "the " + spec_name(L.spec) + " lowering does not have (its definition differs from "
@@ -1223,6 +1282,15 @@ GuardSrc parse_action(int spec, const std::string& op, int kind, const std::vect
                            "logVars == " + logv + "\n"
                            "Quorum == {i \\in SUBSET(Server) : Cardinality(i) * 2 > Cardinality(Server)}\n"
                            "LastTerm(xlog) == IF Len(xlog) = 0 THEN 0 ELSE xlog[Len(xlog)].term\n" +
+                           // a message handler's guard helper, restated (Raft.tla:180-186)
+                           std::string(kind == K_MSGC ? "ReceivableMessage(m, mtype, term_match) ==\n"
+                                                        "    /\\ messages[m] > 0\n"
+                                                        "    /\\ m.mtype = mtype\n"
+                                                        "    /\\ \\/ /\\ term_match = EqualTerm\n"
+                                                        "          /\\ m.mterm = currentTerm[m.mdest]\n"
+                                                        "       \\/ /\\ term_match = LessOrEqualTerm\n"
+                                                        "          /\\ m.mterm <= currentTerm[m.mdest]\n"
+                                                      : "") +
                            op + (params.empty() ? "" : "(" + ps + ")") + " ==\n    " + body + "\n====\n";
   auto mod = std::make_shared<Module>(parse_module(text));
   const Def* d = mod->find(op);
@@ -1236,6 +1304,12 @@ GuardSrc parse_action(int spec, const std::string& op, int kind, const std::vect
   g.kind = kind;
   g.mod = mod;
   g.send_helpers = helpers;
+  if (kind == K_MSGC) {  // a message handler: Discard / Reply too, one program in the text's order
+    g.send_helpers["Discard"] = 3;
+    g.send_helpers["Reply"] = 4;
+    g.conjuncts = {d->body};
+    return g;
+  }
   // the send helpers are not defined in the text: mark them as effects for the split
   for (auto& h : helpers) H.effect_ops.insert(h.first);
   if (!H.split(op, g.conjuncts, g.effects)) throw std::runtime_error("action " + op + " changes nothing");

@@ -252,8 +252,9 @@ class Model:
         """Define an action by its TLA+ text for set_next to use by name
         (rmc_model_define_action: compiled whole, guard and effect,
         rmc_guard.cpp compile_effect).  form: "i", "iv" or "ij" (the binding
-        \\E i \\in Server / i \\in Server, v \\in Value / i, j \\in Server)."""
-        f = {"i": 0, "iv": 1, "ij": 2}[form] if isinstance(form, str) else int(form)
+        \\E i \\in Server / i \\in Server, v \\in Value / i, j \\in Server), or "m": a
+        message handler, body of \\E m \\in DOMAIN messages (compile_handler)."""
+        f = {"i": 0, "iv": 1, "ij": 2, "m": 3}[form] if isinstance(form, str) else int(form)
         if isinstance(params, (list, tuple)):
             params = ", ".join(params)
         if lib().rmc_model_define_action(self._h, name.encode(), f, params.encode(), body.encode()) != 0:

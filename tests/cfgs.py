@@ -378,3 +378,106 @@ EFFECTS = [
      ("Restart", "RequestVoteNoSelf") + NEXT_RAFT[2:],
      [("RequestVoteNoSelf", "i", "i", _RV_BODY % "SendMultiple")], 0),
 ]
+
+
+# (name, module, kwargs, Next (names), [(action, "m", "m", TLA+ body)], max_depth):
+# message handlers the TLA+ front end compiles whole (rmc_guard.cpp
+# compile_handler) -- the body of \E m \in DOMAIN messages : body, given as TLA+
+# text (rmc_model_define_action form "m" is the table a module whose Next has
+# such a bare action lowers to).  The Python side of each is
+# make_golden._handler_py()[name].
+def _nx(base, old, new):
+    return tuple(new if d == old else d for d in base)
+
+
+_HRVRESP = """/\\ ReceivableMessage(m, RequestVoteResponse, EqualTerm)
+    /\\ LET i == m.mdest
+           j == m.msource
+       IN
+          /\\ \\/ /\\ m.mvoteGranted
+                /\\ votesGranted' = [votesGranted EXCEPT ![i] = votesGranted[i] \\cup {j}]
+             \\/ /\\ ~m.mvoteGranted
+                /\\ UNCHANGED <<votesGranted>>
+          /\\ Discard(m)
+          /\\ UNCHANGED <<serverVars, votedFor, leaderVars, logVars, auxVars>>"""
+_HRVRESP_ALL = """/\\ ReceivableMessage(m, RequestVoteResponse, EqualTerm)
+    /\\ LET i == m.mdest
+           j == m.msource
+       IN
+          /\\ votesGranted' = [votesGranted EXCEPT ![i] = votesGranted[i] \\cup {j}]
+          /\\ Discard(m)
+          /\\ UNCHANGED <<serverVars, votedFor, leaderVars, logVars, auxVars>>"""
+_HRVREQ_NOLOG = """/\\ ReceivableMessage(m, RequestVoteRequest, LessOrEqualTerm)
+    /\\ LET i     == m.mdest
+           j     == m.msource
+           grant == /\\ m.mterm = currentTerm[i]
+                    /\\ votedFor[i] \\in {Nil, j}
+        IN /\\ m.mterm <= currentTerm[i]
+           /\\ \\/ grant  /\\ votedFor' = [votedFor EXCEPT ![i] = j]
+              \\/ ~grant /\\ UNCHANGED votedFor
+           /\\ Reply([mtype        |-> RequestVoteResponse,
+                     mterm        |-> currentTerm[i],
+                     mvoteGranted |-> grant,
+                     msource      |-> i,
+                     mdest        |-> j],
+                     m)
+           /\\ UNCHANGED <<state, currentTerm, candidateVars, leaderVars, logVars, auxVars>>"""
+_REJAE = """/\\ ReceivableMessage(m, AppendEntriesRequest, LessOrEqualTerm)
+    /\\ LET i     == m.mdest
+           j     == m.msource
+           logOk == \\/ m.mprevLogIndex = 0
+                    \\/ /\\ m.mprevLogIndex > 0
+                       /\\ m.mprevLogIndex <= Len(log[i])
+                       /\\ m.mprevLogTerm = log[i][m.mprevLogIndex].term
+       IN  /\\ %s
+           /\\ Reply([mtype           |-> AppendEntriesResponse,
+                     mterm           |-> currentTerm[i],
+                     msuccess        |-> FALSE,
+                     mmatchIndex     |-> 0,
+                     msource         |-> i,
+                     mdest           |-> j],
+                     m)
+           /\\ UNCHANGED <<state, candidateVars, leaderVars, serverVars, logVars, auxVars>>"""
+_REJAE_REF = _REJAE % """\\/ m.mterm < currentTerm[i]
+              \\/ /\\ m.mterm = currentTerm[i]
+                 /\\ state[i] = Follower
+                 /\\ \\lnot logOk"""
+_REJAE_LENIDX = (_REJAE % """\/ m.mterm < currentTerm[i]
+              \/ /\ m.mterm = currentTerm[i]
+                 /\ state[i] = Follower
+                 /\ \lnot logOk""").replace("mmatchIndex     |-> 0", "mmatchIndex     |-> Len(log[i])")
+_UPDATETERM_STAY = """/\\ m.mterm > currentTerm[m.mdest]
+    /\\ currentTerm'    = [currentTerm EXCEPT ![m.mdest] = m.mterm]
+    /\\ votedFor'       = [votedFor    EXCEPT ![m.mdest] = Nil]
+    /\\ UNCHANGED <<messages, state, candidateVars, leaderVars, logVars, auxVars>>"""
+HANDLERS = [
+    # Raft.tla:386-401 HandleRequestVoteResponse written out: compiled, it checks the built-in space
+    ("raft_hrvresp_text_n3v1e1", "Raft", dict(n=3, v=1, E=1),
+     _nx(NEXT_RAFT, "HandleRequestVoteResponse", "HRVRespText"), [("HRVRespText", "m", "m", _HRVRESP)], 0),
+    # ... tallying every response as a vote (the mvoteGranted test dropped)
+    ("raft_hrvresp_all_n2v1e2", "Raft", dict(n=2, v=1, E=2),
+     _nx(NEXT_RAFT, "HandleRequestVoteResponse", "HRVRespAll"), [("HRVRespAll", "m", "m", _HRVRESP_ALL)], 0),
+    # Raft.tla:360-381 HandleRequestVoteRequest without the log comparison (logOk dropped)
+    ("raft_hrvreq_nolog_n2v1e2", "Raft", dict(n=2, v=1, E=2),
+     _nx(NEXT_RAFT, "HandleRequestVoteRequest", "HRVReqNoLog"), [("HRVReqNoLog", "m", "m", _HRVREQ_NOLOG)], 0),
+    # Raft.tla:412-430 RejectAppendEntriesRequest written out (LogOk inlined)
+    ("raft_rejae_text_n2v2e2", "Raft", dict(n=2, v=2, E=2),
+     _nx(NEXT_RAFT, "RejectAppendEntriesRequest", "RejAEText"), [("RejAEText", "m", "m", _REJAE_REF)], 0),
+    # ... whose rejection carries the follower's log length as mmatchIndex
+    ("raft_rejae_lenidx_n2v2e2", "Raft", dict(n=2, v=2, E=2),
+     _nx(NEXT_RAFT, "RejectAppendEntriesRequest", "RejAELen"), [("RejAELen", "m", "m", _REJAE_LENIDX)], 0),
+    # Raft.tla:348-355 UpdateTerm that does not step down to Follower
+    ("raft_updateterm_stay_n2v1e2", "Raft", dict(n=2, v=1, E=2),
+     _nx(NEXT_RAFT, "UpdateTerm", "UpdateTermStay"), [("UpdateTermStay", "m", "m", _UPDATETERM_STAY)], 0),
+    # two compiled handlers at once, one of them with its reference text
+    ("raft_two_handlers_n2v1e2r1", "Raft", dict(n=2, v=1, E=2, R=1),
+     _nx(_nx(NEXT_RAFT, "HandleRequestVoteResponse", "HRVRespAll"), "RejectAppendEntriesRequest", "RejAEText"),
+     [("HRVRespAll", "m", "m", _HRVRESP_ALL), ("RejAEText", "m", "m", _REJAE_REF)], 0),
+    # FlexibleRaft (Reply refuses a response already in DOMAIN) and RaftFsync
+    ("flex_hrvresp_all_n2v1e2", "FlexibleRaft", dict(n=2, v=1, E=2, ElectionQuorumSize=2, ReplicationQuorumSize=1),
+     _nx(NEXT_RAFT, "HandleRequestVoteResponse", "HRVRespAll"), [("HRVRespAll", "m", "m", _HRVRESP_ALL)], 0),
+    ("fsync_rejae_text_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1),
+     _nx(NEXT_FSYNC, "RejectAppendEntriesRequest", "RejAEText"), [("RejAEText", "m", "m", _REJAE_REF)], 0),
+    ("fsync_hrvreq_nolog_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1),
+     _nx(NEXT_FSYNC, "HandleRequestVoteRequest", "HRVReqNoLog"), [("HRVReqNoLog", "m", "m", _HRVREQ_NOLOG)], 0),
+]

@@ -23,7 +23,7 @@ from oracle import run_c  # noqa: E402
 from oracle.pyoracle import make_spec  # noqa: E402
 from oracle.pyoracle.cfg import parse_cfg  # noqa: E402
 from oracle.pyoracle.tlc import bfs  # noqa: E402
-from cfgs import (EFFECTS, EXTRAS, FLEX_RESTART, FRONTEND, GUARDS, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
+from cfgs import (EFFECTS, EXTRAS, HANDLERS, FLEX_RESTART, FRONTEND, GUARDS, LADDERS, MEDIUM, N5, N5_UNSAFE, ORDER, SMALL, UNSAFE, VARIANT2_MEDIUM,  # noqa: E402
                   VARIANT2_N5, VARIANT2_SMALL, cfg_text)
 
 SHIPPED = [  # the reference's own cfgs, restated in configs/ (same constants)
@@ -444,7 +444,116 @@ def effects():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def _handler_py():
+    """The Python side of every cfgs.HANDLERS message handler (written here by
+    hand from each TLA+ body, iterating DOMAIN messages in TLC's order as the
+    oracle's own handlers do): {case: {name: ("m", f(spec, s))}}."""
+    from oracle.pyoracle.raft import AEREQ, AERESP, EQUAL, FOLLOWER, LEQ, RVREQ, RVRESP
+    from oracle.pyoracle.tlc import NIL, Rec, fset
+
+    def hrvresp_all(sp, s):
+        for m, c in s["messages"]:
+            if not sp.ReceivableMessage(s, m, c, RVRESP, EQUAL):
+                continue
+            i, j = m.mdest, m.msource
+            msgs = sp.Discard(s["messages"], m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            t["votesGranted"] = fset(s["votesGranted"], i, s["votesGranted"][i] | {j})
+            t["messages"] = msgs
+            yield t
+
+    def hrvreq_nolog(sp, s):
+        for m, c in s["messages"]:
+            if not sp.ReceivableMessage(s, m, c, RVREQ, LEQ):
+                continue
+            i, j = m.mdest, m.msource
+            grant = m.mterm == s["currentTerm"][i] and s["votedFor"][i] in (NIL, j)
+            if not m.mterm <= s["currentTerm"][i]:
+                continue
+            msgs = sp.Reply(s["messages"], Rec(mtype=RVRESP, mterm=s["currentTerm"][i], mvoteGranted=grant,
+                                               msource=i, mdest=j), m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            if grant:
+                t["votedFor"] = fset(s["votedFor"], i, j)
+            t["messages"] = msgs
+            yield t
+
+    def rejae_lenidx(sp, s):
+        for m, c in s["messages"]:
+            if not sp.ReceivableMessage(s, m, c, AEREQ, LEQ):
+                continue
+            i, j = m.mdest, m.msource
+            cur = s["currentTerm"][i]
+            if not (m.mterm < cur or (m.mterm == cur and s["state"][i] == FOLLOWER and not sp.LogOk(s, i, m))):
+                continue
+            msgs = sp.Reply(s["messages"], Rec(mtype=AERESP, mterm=cur, msuccess=False,
+                                               mmatchIndex=len(s["log"][i]), msource=i, mdest=j), m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            t["messages"] = msgs
+            yield t
+
+    def updateterm_stay(sp, s):
+        for m, _ in s["messages"]:
+            d = m.mdest
+            if m.mterm > s["currentTerm"][d]:
+                t = dict(s)
+                t["currentTerm"] = fset(s["currentTerm"], d, m.mterm)
+                t["votedFor"] = fset(s["votedFor"], d, NIL)
+                yield t
+
+    ref_hrvresp = ("m", lambda sp, s: sp.HandleRequestVoteResponse(s))
+    ref_rejae = ("m", lambda sp, s: sp.RejectAppendEntriesRequest(s))
+    return {
+        "raft_hrvresp_text_n3v1e1": {"HRVRespText": ref_hrvresp},
+        "raft_hrvresp_all_n2v1e2": {"HRVRespAll": ("m", hrvresp_all)},
+        "raft_hrvreq_nolog_n2v1e2": {"HRVReqNoLog": ("m", hrvreq_nolog)},
+        "raft_rejae_text_n2v2e2": {"RejAEText": ref_rejae},
+        "raft_rejae_lenidx_n2v2e2": {"RejAELen": ("m", rejae_lenidx)},
+        "raft_updateterm_stay_n2v1e2": {"UpdateTermStay": ("m", updateterm_stay)},
+        "raft_two_handlers_n2v1e2r1": {"HRVRespAll": ("m", hrvresp_all), "RejAEText": ref_rejae},
+        "flex_hrvresp_all_n2v1e2": {"HRVRespAll": ("m", hrvresp_all)},
+        "fsync_rejae_text_n2v1e2r1": {"RejAEText": ref_rejae},
+        "fsync_hrvreq_nolog_n2v1e2r1": {"HRVReqNoLog": ("m", hrvreq_nolog)},
+    }
+
+
+def handlers():
+    """--handlers: Next with message handlers the front end compiles whole
+    (cfgs.HANDLERS), by the Python oracle with the same handlers written in
+    Python (_handler_py); the handlers written out from the reference text are
+    also checked against the oracle's own (built-in) space.  Pinned by the
+    Python oracle alone (the C oracle has no configurable actions)."""
+    py = _handler_py()
+    path = os.path.join(HERE, "handlers.json")
+    only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--only=")]
+    out = json.load(open(path)) if only and os.path.exists(path) else {}
+    for name, module, kw, nxt, acts, md in HANDLERS:
+        if only and name not in only[0]:
+            continue
+        txt = cfg_text(module, **kw)
+        cfg = parse_cfg(txt)
+        p = bfs(make_spec(module, cfg, next_order=nxt, defined=py[name]), max_depth=md or None)
+        out[name] = dict(module=module, cfg=txt, next=list(nxt), actions=[list(a) for a in acts], max_depth=md,
+                         generated=p.generated, distinct=p.distinct, depth=p.depth, status=p.status,
+                         violated=getattr(p, "violated", None), levels=[list(x) for x in p.levels],
+                         hidden_same_level=p.hidden_same_level, max_msgs=p.max_msgs,
+                         trace_len=len(p.trace) if getattr(p, "trace", None) else None, pinned_by="pyoracle")
+        print(name, p.generated, p.distinct, p.depth, p.status, getattr(p, "violated", None), p.hidden_same_level,
+              "%.1fs" % p.seconds, flush=True)
+    out = {k: v for k, v in out.items() if k in {e[0] for e in HANDLERS}}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
+    if "--handlers" in sys.argv:
+        return handlers()
     if "--effects" in sys.argv:
         return effects()
     if "--guards" in sys.argv:

@@ -18,6 +18,7 @@ import re
 import pytest
 
 import raftmc
+from cfgs import cfg_text
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 FRONTEND = json.load(open(os.path.join(HERE, "golden", "frontend.json")))
@@ -220,15 +221,35 @@ def test_renamed_helpers_and_module_are_accepted(tmp_path):
 @needs_ref
 def test_changed_action_is_refused_by_name(tmp_path):
     text = ref_text("Raft")
-    # a message handler's effect edited (an edited guard is compiled behind the
-    # library's effect, tests/test_guards.py; a fixed-binding action's new
-    # effect is compiled whole, tests/test_effects.py; a handler over DOMAIN
-    # messages has no compiled form)
-    edited = text.replace("votesGranted[i] \\cup {j}]", "votesGranted[i] \\cup {i}]")
+    # a message handler edited in a way the handler compiler does not take:
+    # AcceptAppendEntriesRequest (Raft.tla:454-485) truncates logs (log' =
+    # new_log, a CASE over TruncateLog); an edited guard is compiled behind the
+    # library's effect (tests/test_guards.py), a fixed-binding action's new
+    # effect compiled whole (tests/test_effects.py), a handler's new body
+    # compiled whole when its effects are the forms compile_handler knows
+    # (tests/test_handlers.py)
+    edited = text.replace("[commitIndex EXCEPT ![i] =\n                                              m.mcommitIndex]",
+                          "[commitIndex EXCEPT ![i] =\n                                              0]")
     assert edited != text
     cfg = open(os.path.join(REF, "standard-raft", "Raft.cfg")).read()
-    with pytest.raises(raftmc.RaftmcError, match="HandleRequestVoteResponse"):
+    with pytest.raises(raftmc.RaftmcError, match="AcceptAppendEntriesRequest"):
         load(tmp_path, edited, cfg)
+
+
+@needs_ref
+def test_changed_handler_is_compiled(tmp_path):
+    """r06: the r05 refusal case -- HandleRequestVoteResponse tallying the
+    voter's destination instead of its source -- now lowers with the handler
+    compiled whole (rmc_guard.cpp compile_handler) and runs on the CPU engine."""
+    text = ref_text("Raft")
+    edited = text.replace("votesGranted[i] \\cup {j}]", "votesGranted[i] \\cup {i}]")
+    assert edited != text
+    cfg = cfg_text("Raft", n=2, v=1, E=2)
+    m = load(tmp_path, edited, cfg)
+    assert m.next()[8] == "HandleRequestVoteResponse"
+    r = m.check_cpu(workers=4)
+    base = raftmc.Model(module="Raft", cfg_text=cfg).check_cpu(workers=4)
+    assert r["status"] == "ok" and r["distinct"] != base["distinct"]
 
 
 @needs_ref

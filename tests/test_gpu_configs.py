@@ -143,3 +143,31 @@ def test_per_shard_device_memory_scales_with_shards():
         r = m.check_logical(W)
         assert (r["distinct"], r["generated"], r["depth"]) == (g["distinct"], g["generated"], g["depth"])
         assert r["device_bytes"] <= bound * single["device_bytes"], (W, r["device_bytes"], single["device_bytes"])
+
+
+# ---- r06: config 5's R-ladder at V = 1, E = 2 (tests/golden/fsync_rladder.json)
+RL = json.load(open(os.path.join(HERE, "golden", "fsync_rladder.json")))
+
+
+def _rmodel(R):
+    return raftmc.Model(module="RaftFsync", cfg_path=os.path.join(ROOT, "configs", "RaftFsync_n3v1e2r%d.cfg" % R))
+
+
+def test_fsync_r3_exhausts_and_its_prefix_equals_the_c_oracle():
+    """RaftFsync_n3v1e2r3 in full on one GPU: the recorded totals, and every
+    one of its first 38 levels equal to the C oracle's own run of them."""
+    r = _rmodel(3).check()
+    g = RL["gpu"]["r3"]
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    ol = RL["oracle_r3_levels"]
+    assert r["levels"][:len(ol)] == ol
+
+
+@pytest.mark.parametrize("R", [4, 7])
+def test_fsync_r_ladder_saturates(R):
+    """Every R >= 3 gives R = 3's 1,179,899,717 distinct states (restartCtr is
+    outside VIEW): the R-ladder cannot be sized to a node."""
+    r = _rmodel(R).check()
+    g = RL["gpu"]["r%d" % R]
+    assert (r["generated"], r["distinct"], r["depth"], r["status"]) == (g["generated"], g["distinct"], g["depth"], "ok")
+    assert r["distinct"] == RL["gpu"]["r3"]["distinct"]

@@ -86,6 +86,13 @@ TARGETS = [
      "profiles/r03/ladder_RaftFsync_n3v2e2r1_hf1.txt", 112),
     ("config 5 scaled: RaftFsync N=3 V=2 E=3 R=1 (configs/RaftFsync_n3v2e3r1.cfg)",
      "profiles/r02/ladder_RaftFsync_n3v2e3r1.txt", 112),
+    # r06: the R-ladder at V=1, E=2 saturates at R=3 (1,179,899,717 distinct for
+    # every R >= 3, profiles/r06/ladder5/); the next RaftFsync rungs are R=0 on
+    # the V and E axes
+    ("config 5 rung: RaftFsync N=3 V=2 E=2 R=0 (configs/RaftFsync_n3v2e2.cfg)",
+     "profiles/r06/ladder5/RaftFsync_n3v2e2.txt", 112),
+    ("config 5 rung: RaftFsync N=3 V=1 E=3 R=0 (configs/RaftFsync_n3v1e3.cfg)",
+     "profiles/r06/ladder5/RaftFsync_n3v1e3.txt", 112),
 ]
 EXTRA = os.environ.get("CAPACITY_EXTRA", "")  # "label|path|row_bytes;..." rungs measured later
 

@@ -76,6 +76,12 @@ GUARDED = {"Restart", "RequestVote", "Timeout", "BecomeLeader", "ClientRequest"}
 HELPERS = {"RAFT": {"SendMultipleOnce": 0, "_SendOnce": 1, "Send": 2, "_SendNoRestriction": 2},
            "FLEX": {"SendMultiple": 0, "Send": 1},
            "FSYNC": {"Send": 1}}
+# ... and the bag helpers a compiled message handler may call (rmc_guard.cpp
+# compile_handler): 3 = Discard(m) (Raft.tla:164-167), 4 = Reply(response,
+# request) (Raft.tla:170-176; FlexibleRaft.tla:148-151 and RaftFsync.tla:149-152
+# refuse a response already in DOMAIN -- rmc_spec.h op_reply)
+for _k in HELPERS:
+    HELPERS[_k].update(Discard=3, Reply=4)
 
 
 def hashes(lib, text):
