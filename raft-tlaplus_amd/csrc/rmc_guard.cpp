@@ -456,6 +456,8 @@ struct Compiler {
         const std::string& s = n->s;
         if (const Binding* b = sc->find(s))
           if (b->k == Binding::MACRO) return inline_def(n, b->def, n->k, sc, b->defsc.lock());
+        int mm = -1;
+        if (!sc->find(s) && n->k.size() == 1 && (mm = minmax_def(m.find(s))) >= 0) return minmax(n, n->k[0], mm, sc);
         if (!m.find(s) || sc->find(s)) {
           if (s == "Len" && n->k.size() == 1) {
             Arg x;
@@ -675,6 +677,47 @@ struct Compiler {
 
   // (defsc: a LET definition's own scope -- TLA+ LET bodies see the names
   // bound around them, e.g. a handler's message; a module operator sees none)
+  // The specs' Min / Max (Raft.tla:190-192: CHOOSE x \in s : \A y \in s : x <= y,
+  // resp. x >= y) -- recognised by that shape, whatever the name: 0 Min, 1 Max,
+  // -1 another definition.
+  static int minmax_def(const Def* d) {
+    if (!d || d->params.size() != 1 || !d->body || d->body->kind != N_CHOOSE) return -1;
+    const Node& c = *d->body;
+    auto is_id = [](const NodeP& n, const std::string& s) { return n && n->kind == N_ID && n->s == s; };
+    if (c.bounds.size() != 1 || c.bounds[0].vars.size() != 1 || !is_id(c.bounds[0].set, d->params[0]) || c.k.size() != 1)
+      return -1;
+    const NodeP& q = c.k[0];
+    if (q->kind != N_QUANT || q->s != "\\A" || q->bounds.size() != 1 || q->bounds[0].vars.size() != 1 ||
+        !is_id(q->bounds[0].set, d->params[0]) || q->k.size() != 1)
+      return -1;
+    const NodeP& b = q->k[0];
+    const std::string& x = c.bounds[0].vars[0];
+    const std::string& y = q->bounds[0].vars[0];
+    if (b->kind != N_BIN || b->k.size() != 2 || x == y) return -1;
+    const bool xy = is_id(b->k[0], x) && is_id(b->k[1], y), yx = is_id(b->k[0], y) && is_id(b->k[1], x);
+    if (!xy && !yx) return -1;
+    const std::string& op = b->s;
+    const bool le = op == "<=" || op == "=<" || op == "\\leq", ge = op == ">=" || op == "\\geq";
+    if (!le && !ge) return -1;
+    return (le == xy) ? 0 : 1;
+  }
+  // Min / Max of a set literal of one or two integers: IF a <= b THEN a ELSE b
+  // (its operands are pure, so each is evaluated again where it is chosen).
+  Ty minmax(const NodeP& at, const NodeP& set, int is_max, ScopeP sc) {
+    if (set->kind != N_SETENUM || set->k.empty() || set->k.size() > 2)
+      fail(at, "Min / Max of something other than a literal of one or two integers");
+    if (concrete(expr(set->k[0], sc), at) != T_INT) fail(at, "Min / Max of a non-integer");
+    if (set->k.size() == 1) return T_INT;
+    if (concrete(expr(set->k[1], sc), at) != T_INT) fail(at, "Min / Max of a non-integer");
+    emit(is_max ? G_LE : G_LT);  // Max: a <= b picks b; Min: a < b picks a
+    const size_t j = jump(is_max ? G_JNZ : G_JZ);
+    expr(set->k[0], sc);
+    const size_t e = jump(G_JMP);
+    patch(j);
+    expr(set->k[1], sc);
+    patch(e);
+    return T_INT;
+  }
   Ty inline_def(const NodeP& at, const Def* d, const std::vector<NodeP>& args, ScopeP sc, ScopeP defsc = nullptr) {
     if (!d->error.empty()) fail(at, "definition " + d->name + " does not parse: " + d->error);
     if (d->params.size() != args.size()) fail(at, "operator " + d->name + " applied to the wrong number of arguments");

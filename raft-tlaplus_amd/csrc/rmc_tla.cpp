@@ -1281,7 +1281,9 @@ GuardSrc parse_action(int spec, const std::string& op, int kind, const std::vect
                            "leaderVars == " + leader + "\n"
                            "logVars == " + logv + "\n"
                            "Quorum == {i \\in SUBSET(Server) : Cardinality(i) * 2 > Cardinality(Server)}\n"
-                           "LastTerm(xlog) == IF Len(xlog) = 0 THEN 0 ELSE xlog[Len(xlog)].term\n" +
+                           "LastTerm(xlog) == IF Len(xlog) = 0 THEN 0 ELSE xlog[Len(xlog)].term\n"
+                           "Min(s) == CHOOSE x \\in s : \\A y \\in s : x <= y\n"
+                           "Max(s) == CHOOSE x \\in s : \\A y \\in s : x >= y\n" +
                            // a message handler's guard helper, restated (Raft.tla:180-186)
                            std::string(kind == K_MSGC ? "ReceivableMessage(m, mtype, term_match) ==\n"
                                                         "    /\\ messages[m] > 0\n"
@@ -1318,12 +1320,14 @@ GuardSrc parse_action(int spec, const std::string& op, int kind, const std::vect
 
 GuardSrc parse_guard(int spec, int act, const std::string& op, const std::vector<std::string>& params,
                      const std::string& expr) {
-  // the family's standard helpers, restated (Raft.tla:123 Quorum, :126 LastTerm)
+  // the family's standard helpers, restated (Raft.tla:123 Quorum, :126 LastTerm, :190-192 Min / Max)
   std::string ps;
   for (size_t q = 0; q < params.size(); q++) ps += (q ? ", " : "") + params[q];
   const std::string text = "---- MODULE GuardText ----\n"
                            "Quorum == {i \\in SUBSET(Server) : Cardinality(i) * 2 > Cardinality(Server)}\n"
                            "LastTerm(xlog) == IF Len(xlog) = 0 THEN 0 ELSE xlog[Len(xlog)].term\n"
+                           "Min(s) == CHOOSE x \\in s : \\A y \\in s : x <= y\n"
+                           "Max(s) == CHOOSE x \\in s : \\A y \\in s : x >= y\n"
                            "GuardOf" + op + (params.empty() ? "" : "(" + ps + ")") + " ==\n    " + expr + "\n====\n";
   auto helpers = std::make_shared<Module>(parse_module(text));
   const Def* d = helpers->find("GuardOf" + op);

@@ -450,6 +450,21 @@ _UPDATETERM_STAY = """/\\ m.mterm > currentTerm[m.mdest]
     /\\ currentTerm'    = [currentTerm EXCEPT ![m.mdest] = m.mterm]
     /\\ votedFor'       = [votedFor    EXCEPT ![m.mdest] = Nil]
     /\\ UNCHANGED <<messages, state, candidateVars, leaderVars, logVars, auxVars>>"""
+_HAERESP = """/\\ ReceivableMessage(m, AppendEntriesResponse, EqualTerm)
+    /\\ LET i     == m.mdest
+           j     == m.msource
+       IN
+          /\\ \\/ /\\ m.msuccess \\* successful
+                /\\ nextIndex'  = [nextIndex  EXCEPT ![i][j] = %s]
+                /\\ matchIndex' = [matchIndex EXCEPT ![i][j] = m.mmatchIndex]
+             \\/ /\\ \\lnot m.msuccess \\* not successful
+                /\\ nextIndex' = [nextIndex EXCEPT ![i][j] =
+                                     Max({nextIndex[i][j] - %d, 1})]
+                /\\ UNCHANGED <<matchIndex>>%s
+          /\\ Discard(m)
+          /\\ UNCHANGED <<serverVars, candidateVars, logVars, auxVars>>"""
+_PEND = """
+          /\\ pendingResponse' = [pendingResponse EXCEPT ![i][j] = FALSE]"""
 HANDLERS = [
     # Raft.tla:386-401 HandleRequestVoteResponse written out: compiled, it checks the built-in space
     ("raft_hrvresp_text_n3v1e1", "Raft", dict(n=3, v=1, E=1),
@@ -480,4 +495,17 @@ HANDLERS = [
      _nx(NEXT_FSYNC, "RejectAppendEntriesRequest", "RejAEText"), [("RejAEText", "m", "m", _REJAE_REF)], 0),
     ("fsync_hrvreq_nolog_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1),
      _nx(NEXT_FSYNC, "HandleRequestVoteRequest", "HRVReqNoLog"), [("HRVReqNoLog", "m", "m", _HRVREQ_NOLOG)], 0),
+    # Raft.tla:490-505 HandleAppendEntriesResponse written out (Max, rows at [i][j] = [mdest][msource])
+    ("raft_haeresp_text_n3v1e1", "Raft", dict(n=3, v=1, E=1),
+     _nx(NEXT_RAFT, "HandleAppendEntriesResponse", "HAERespText"),
+     [("HAERespText", "m", "m", _HAERESP % ("m.mmatchIndex + 1", 1, _PEND))], 0),
+    # ... re-sending the last acknowledged entry: nextIndex = Max({mmatchIndex, 1}) on success, and
+    # backing off by two on a rejection
+    ("raft_haeresp_resend_n2v2e2", "Raft", dict(n=2, v=2, E=2),
+     _nx(NEXT_RAFT, "HandleAppendEntriesResponse", "HAERespResend"),
+     [("HAERespResend", "m", "m", _HAERESP % ("Max({m.mmatchIndex, 1})", 2, _PEND))], 0),
+    # RaftFsync.tla:486-500 (no pendingResponse) written out
+    ("fsync_haeresp_text_n2v1e2r1", "RaftFsync", dict(n=2, v=1, E=2, R=1),
+     _nx(NEXT_FSYNC, "HandleAppendEntriesResponse", "HAERespText"),
+     [("HAERespText", "m", "m", _HAERESP % ("m.mmatchIndex + 1", 1, ""))], 0),
 ]

@@ -325,7 +325,7 @@ def _effect_py():
     """The Python side of every cfgs.EFFECTS action (written here by hand from
     each TLA+ body): {case: {name: (form, f(spec, s, *args))}}."""
     from oracle.pyoracle.raft import CANDIDATE, FOLLOWER, LEADER, RVREQ
-    from oracle.pyoracle.tlc import NIL, Rec, fset
+    from oracle.pyoracle.tlc import NIL, Rec, fset, fset2
 
     def rv(spec, s, i, self_vote, step, mstep=None):
         # RequestVote (Raft.tla:242-257) with the self vote optional, a term step
@@ -449,7 +449,7 @@ def _handler_py():
     hand from each TLA+ body, iterating DOMAIN messages in TLC's order as the
     oracle's own handlers do): {case: {name: ("m", f(spec, s))}}."""
     from oracle.pyoracle.raft import AEREQ, AERESP, EQUAL, FOLLOWER, LEQ, RVREQ, RVRESP
-    from oracle.pyoracle.tlc import NIL, Rec, fset
+    from oracle.pyoracle.tlc import NIL, Rec, fset, fset2
 
     def hrvresp_all(sp, s):
         for m, c in s["messages"]:
@@ -507,7 +507,26 @@ def _handler_py():
                 t["votedFor"] = fset(s["votedFor"], d, NIL)
                 yield t
 
+    def haeresp_resend(sp, s):
+        for m, c in s["messages"]:
+            if not sp.ReceivableMessage(s, m, c, AERESP, EQUAL):
+                continue
+            i, j = m.mdest, m.msource
+            msgs = sp.Discard(s["messages"], m)
+            if msgs is None:
+                continue
+            t = dict(s)
+            if m.msuccess:
+                t["nextIndex"] = fset2(s["nextIndex"], i, j, max(m.mmatchIndex, 1))
+                t["matchIndex"] = fset2(s["matchIndex"], i, j, m.mmatchIndex)
+            else:
+                t["nextIndex"] = fset2(s["nextIndex"], i, j, max(s["nextIndex"][i][j] - 2, 1))
+            t["pendingResponse"] = fset2(s["pendingResponse"], i, j, False)
+            t["messages"] = msgs
+            yield t
+
     ref_hrvresp = ("m", lambda sp, s: sp.HandleRequestVoteResponse(s))
+    ref_haeresp = ("m", lambda sp, s: sp.HandleAppendEntriesResponse(s))
     ref_rejae = ("m", lambda sp, s: sp.RejectAppendEntriesRequest(s))
     return {
         "raft_hrvresp_text_n3v1e1": {"HRVRespText": ref_hrvresp},
@@ -520,6 +539,9 @@ def _handler_py():
         "flex_hrvresp_all_n2v1e2": {"HRVRespAll": ("m", hrvresp_all)},
         "fsync_rejae_text_n2v1e2r1": {"RejAEText": ref_rejae},
         "fsync_hrvreq_nolog_n2v1e2r1": {"HRVReqNoLog": ("m", hrvreq_nolog)},
+        "raft_haeresp_text_n3v1e1": {"HAERespText": ref_haeresp},
+        "raft_haeresp_resend_n2v2e2": {"HAERespResend": ("m", haeresp_resend)},
+        "fsync_haeresp_text_n2v1e2r1": {"HAERespText": ref_haeresp},
     }
 
 

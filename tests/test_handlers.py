@@ -52,11 +52,14 @@ def test_cpu_engine_matches_oracle(name):
     same(model(name).check_cpu(workers=8, max_depth=CASES[name][5]), FIX[name])
 
 
-@pytest.mark.parametrize("name", ["raft_hrvresp_text_n3v1e1", "raft_rejae_text_n2v2e2", "fsync_rejae_text_n2v1e2r1"])
+@pytest.mark.parametrize("name", ["raft_hrvresp_text_n3v1e1", "raft_rejae_text_n2v2e2", "fsync_rejae_text_n2v1e2r1",
+                                  "raft_haeresp_text_n3v1e1", "fsync_haeresp_text_n2v1e2r1"])
 def test_reference_text_compiled_gives_the_builtin_space(name):
-    """The reference's HandleRequestVoteResponse (Raft.tla:386-401) and
-    RejectAppendEntriesRequest (:412-430, RaftFsync.tla's) written out and
-    compiled whole check exactly the library handler's space, level by level."""
+    """The reference's HandleRequestVoteResponse (Raft.tla:386-401),
+    RejectAppendEntriesRequest (:412-430, RaftFsync.tla's) and
+    HandleAppendEntriesResponse (:490-505, RaftFsync.tla:486-500) written out
+    and compiled whole check exactly the library handler's space, level by
+    level."""
     _, module, kw, nxt, acts, md = CASES[name]
     base = raftmc.Model(module=module, cfg_text=FIX[name]["cfg"]).check_cpu(workers=8)
     r = model(name).check_cpu(workers=8)
@@ -121,6 +124,23 @@ def test_refused_handlers_are_named(body, match):
     m = raftmc.Model(module="Raft", cfg_text=_cfg())
     with pytest.raises(raftmc.RaftmcError, match=match):
         m.define_action("Bad", "m", "m", body)
+
+
+def test_min_max_of_a_literal_only():
+    """Min / Max (Raft.tla:190-192) of a one- or two-element literal compile to
+    a compare and select; of any other set they are refused."""
+    m = raftmc.Model(module="Raft", cfg_text=_cfg())
+    with pytest.raises(raftmc.RaftmcError, match="literal of one or two integers"):
+        m.define_action("Bad", "m", "m", """/\\ ReceivableMessage(m, AppendEntriesResponse, EqualTerm)
+    /\\ nextIndex' = [nextIndex EXCEPT ![m.mdest][m.msource] = Max({k \\in 1..3 : k > 1})]
+    /\\ Discard(m)
+    /\\ UNCHANGED <<serverVars, candidateVars, matchIndex, pendingResponse, logVars, auxVars>>""")
+    # a guard through the same code: Min of two terms, Max of one
+    g = raftmc.Model(module="Raft", cfg_text=_cfg())
+    g.set_guard("RequestVote", "i", "Min({currentTerm[i], 1}) = 0 /\\ Max({electionCtr}) < MaxElections")
+    base = raftmc.Model(module="Raft", cfg_text=_cfg())
+    base.set_guard("RequestVote", "i", "currentTerm[i] = 0 /\\ electionCtr < MaxElections")
+    assert g.check_cpu(workers=4)["levels"] == base.check_cpu(workers=4)["levels"]
 
 
 def test_discard_outside_a_handler_is_refused():
