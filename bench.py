@@ -279,8 +279,9 @@ def main():
                        "first_check_note": "the warm-up check of this process, by phase (rmc_check_phases, seconds): "
                                            "hip_init = runtime + device context, buffers = arena allocation and VMM "
                                            "maps, launch_enqueue = host time in launch calls (code-object loading on "
-                                           "a fresh process), table_growth / buffer_growth / widening, kernels = "
-                                           "summed device time",
+                                           "a fresh process), table_growth (.allocate = hipMalloc of each doubled "
+                                           "set, the driver's own time; .fill; .rehash) / buffer_growth / widening, "
+                                           "kernels = summed device time",
                        "hidden_var_collisions": res["hidden_var_collisions"],
                        "fpset_slots": res["hash_capacity"], "state_bytes": S, "fp_bits": args.fp_bits},
             # achieved = B / t_wall with B = 2DS + 8G + 20D per check;

@@ -1405,6 +1405,7 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     return std::chrono::duration<double>(b - a).count();
   };
   double rehash_s = 0, grow_s = 0;
+  double tg_alloc_s = 0, tg_fill_s = 0, tg_rehash_s = 0;  // table growth by step (rmc_check_phases)
 
   // ---- growth: room for `need` entries at <= 0.75 load (0.9 once HBM is full)
   bool full_ok = false;
@@ -1759,6 +1760,9 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
     if (A.table2.bytes >= (1ULL << 30)) A.table2.release();  // large searches need the HBM more than a spare
     grows++;
     rehash_s += secs(tr0, now());
+    tg_alloc_s += secs(tr0, tr1);
+    tg_fill_s += secs(tr1, tr2);
+    tg_rehash_s += secs(tr2, tr3);
     if (opt->verbose)
       fprintf(stderr, "[rmc] fingerprint set grown to 2^%d slots (%.3fs: allocate %.3f, fill %.3f, rehash %.3f, free %.3f)\n",
               __builtin_ctzll(slots), secs(tr0, now()), secs(tr0, tr1), secs(tr1, tr2), secs(tr2, tr3), secs(tr3, now()));
@@ -2515,6 +2519,9 @@ int check_impl(rmc_model* m, const rmc_options* opt_in, rmc_result* res) {
                {"buffers", std::chrono::duration<double>(t_setup - t_model).count()},
                {"launch_enqueue", launch_s},
                {"table_growth", rehash_s},
+               {"table_growth.allocate", tg_alloc_s},  // hipMalloc of the doubled set (the driver's own time)
+               {"table_growth.fill", tg_fill_s},
+               {"table_growth.rehash", tg_rehash_s},
                {"buffer_growth", grow_s},
                {"widening", widen_s},
                {"host_frontier", hf_copy_s},
