@@ -998,8 +998,14 @@ constexpr int MAT_LIST = RMC_MAT_LIST;
 #endif
 constexpr int MAT_T = RMC_MAT_THREADS;
 static_assert(MAT_T % 64 == 0 && MAT_T >= 64, "one thread per tile parent");
+// waves per SIMD the register allocation must allow (0: the compiler's choice)
+#ifdef RMC_MAT_WAVES
+#define RMC_MAT_BOUNDS __launch_bounds__(MAT_T, RMC_MAT_WAVES)
+#else
+#define RMC_MAT_BOUNDS __launch_bounds__(MAT_T)
+#endif
 template <int SPEC, int N, bool G = false>
-__global__ __launch_bounds__(MAT_T) void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
+__global__ RMC_MAT_BOUNDS void k_materialize(const uint32_t* __restrict__ frontier, unsigned long long nparents,
                                                      unsigned long long pbase, const uint32_t* __restrict__ cand_ob,
                                                      const uint16_t* __restrict__ cand_win,
                                                      const uint32_t* __restrict__ par_off,
