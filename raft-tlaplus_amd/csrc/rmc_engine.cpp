@@ -295,6 +295,7 @@ void build_actions(Model& M, const std::vector<std::pair<int, int>>* lowered) {
         M.ord2b[M.act_off[sl] + k] = (uint16_t)(nf + MSGC_STRIDE * (1 + M.act_id[sl] - A_C0) + k);
   }
   if (M.kmax > MSGC_STRIDE) throw std::runtime_error("more message slots than a compiled handler's binding stride");
+  for (int a = 0; a < A_NUM; a++) M.msg_off[a] = (uint16_t)M.act_off[M.msg_act_slot[a]];
   M.bind_words = (M.nfixed + M.kmax + 31) / 32;
   M.ord_words = (off + 31) / 32;
   if (off >= 1024) throw std::runtime_error("ordinal space exceeds 10 bits; lower msg_cap_K");

@@ -56,6 +56,10 @@ constexpr uint32_t OB_LOCAL = 0x4000u;  // sharded search: this shard owns the f
 constexpr uint32_t OB_TDUP = 0x2000u;   // sharded search: repeats an earlier-ranked candidate of its tile (k_tile_dedup)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+// Orders one wave's LDS accesses across lanes: the LDS serves a wave's
+// instructions in order, so it suffices that every earlier LDS write has
+// completed and that the compiler moves no LDS access across this point.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ unsigned long long lanemask_lt() {
   int l = lane_id();
   return l ? (~0ULL >> (64 - l)) : 0ULL;
@@ -129,6 +133,18 @@ constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-succ
 // stages one tile per block synchronously.
 #ifndef RMC_EXPAND_PERSIST
 #define RMC_EXPAND_PERSIST 0
+#endif
+// Phase A (k_expand) and the tile staging of k_materialize issue all of a
+// thread's loads before its first LDS write (stage_rows_batched); 0 = the
+// r01-r06 loop form, kept for the A/B.
+#ifndef RMC_STAGE_BATCH
+#define RMC_STAGE_BATCH 1
+#endif
+// Single-shard k_expand: tile t's candidates start at t x PB x min(maxsucc,
+// 256) instead of a reservation by a returning atomic (a memory round trip on
+// every block's critical path); 0 = the r02-r06 per-XCD counters.
+#ifndef RMC_TILE_SLOTS
+#define RMC_TILE_SLOTS 1
 #endif
 struct ExpandLds {
   int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, off_S2, bytes;
@@ -220,6 +236,37 @@ __device__ __forceinline__ void stage_rows_sync(const uint32_t* __restrict__ fro
     d[1] = v.y;
     d[2] = v.z;
     d[3] = v.w;
+  }
+}
+
+// The same copy with every load of a batch issued before the batch's first
+// LDS write (NT threads, up to U 16 B loads per thread per batch).  Written as
+// a plain loop, hipcc waits for each load (vmcnt(0)) before the next
+// iteration issues its own: one dependent HBM round trip per 16 B step, i.e.
+// three per 64-row tile of the bench workload in k_expand (256 threads) and
+// six in k_materialize (128 threads), all on the block's critical path.
+template <int NT, int U>
+__device__ __forceinline__ void stage_rows_batched(const uint32_t* __restrict__ frontier, unsigned long long p0,
+                                                   int np, int words, int Wp, uint32_t* dst) {
+  const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
+  const int nq = np * (words >> 2);
+  for (int q0 = (int)threadIdx.x; q0 < nq; q0 += NT * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (q0 + u * NT < nq) v[u] = src[q0 + u * NT];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int q = q0 + u * NT;
+      if (q < nq) {
+        const int w = q << 2, p = w / words;
+        uint32_t* d = dst + p * Wp + (w - p * words);
+        d[0] = v[u].x;
+        d[1] = v[u].y;
+        d[2] = v[u].z;
+        d[3] = v[u].w;
+      }
+    }
   }
 }
 
@@ -396,14 +443,35 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     uint32_t* sS = (uint32_t*)lds;
     const unsigned long long p0 = xcd_tile(blockIdx.x, gridDim.x) * PB;
     const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
-    // ---- A: stage the tile (contiguous in HBM) into padded LDS rows
+    // ---- A: stage the tile (contiguous in HBM) into padded LDS rows, and the
+    //      model's binding tables.  Every load of a thread -- table entries
+    //      first, then its rows' 16 B pieces -- is issued before its first
+    //      LDS write: one memory round trip for the phase instead of one per
+    //      16 B step and per table (RMC_STAGE_BATCH=0: the loop form).
+#if RMC_STAGE_BATCH
+    static_assert(MAXFIXED <= 256 && A_NUM <= 256, "one table entry per thread");
+    const uint32_t vdesc = tid < cM.nfixed ? cM.fb_desc[tid] : 0u;
+    const uint32_t vmoff = tid < A_NUM ? (uint32_t)cM.msg_off[tid] : 0u;
+    uint32_t vo2b[4];  // ordinal_limit < 1024
+    // each action slot's fixed bindings (phase B's chunk table, wave 0)
+    const int vfirst = tid < cM.nact ? (int)cM.act_fb_first[tid] : 0, vend = tid < cM.nact ? (int)cM.act_fb_end[tid] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) vo2b[u] = tid + 256 * u < cM.ordinal_limit ? (uint32_t)cM.ord2b[tid + 256 * u] : 0u;
+    stage_rows_batched<256, 4>(frontier, p0, np, words, L.Wp, sS);
+    if (tid < cM.nfixed) sDesc[tid] = vdesc;
+    if (tid < A_NUM) sMOff[tid] = (uint16_t)vmoff;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (tid + 256 * u < cM.ordinal_limit) sO2b[tid + 256 * u] = (uint16_t)vo2b[u];
+#else
     stage_rows_sync(frontier, p0, np, words, L.Wp, sS);
-    for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
-    for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
-    for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
     for (int q = tid; q < cM.nfixed; q += 256) sDesc[q] = cM.fb_desc[q];
     for (int q = tid; q < cM.ordinal_limit; q += 256) sO2b[q] = cM.ord2b[q];
     for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
+#endif
+    for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
+    for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
+    for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
     __syncthreads();
 #endif
   STAMP(0);
@@ -472,7 +540,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       bool g = false;
       if (p < np) {
         PState<SPEC, N> s{sS + p * L.Wp};
-        g = may_enable<SPEC, N, G>(s, cM, b);
+        g = may_enable_d<SPEC, N, G>(s, cM, sDesc[b]);  // the descriptor from LDS, not a vector load per binding
       }
       const unsigned long long m = __ballot(g);
       if (p == 0) sMask[b] = m;
@@ -500,7 +568,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       const int a = tid;
       int c = 0;
       if (a < cM.nact) {
+#if RMC_STAGE_BATCH
+        const int f = vfirst, e = vend;  // loaded in phase A
+#else
         const int f = cM.act_fb_first[a], e = cM.act_fb_end[a];
+#endif
         sAFirst[a] = f;
         sAEnd[a] = e;
         c = ((int)(sBOff[e] - sBOff[f]) + WAVE - 1) / WAVE;
@@ -531,7 +603,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           const int pp = select_bit64(sMask[lo], g - (int)sBOff[lo]);
           PState<SPEC, N> s{sS + pp * L.Wp};
           Delta d;
-          if (eval_fixed<SPEC, N, G>(s, cM, a, cM.fb_x[lo], d)) record(pp, lo, d);
+          // (x from the LDS descriptor: a per-lane cM.fb_x load was a dependent round trip per chunk)
+          if (eval_fixed<SPEC, N, G>(s, cM, a, (int)((sDesc[lo] >> 8) & 0xFFu), d)) record(pp, lo, d);
         }
       }
     }
@@ -626,10 +699,25 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
 #else
       const int seg = sharded ? 0 : (int)(blockIdx.x & (EXPAND_SEGS - 1));  // the block's XCD label
 #endif
-      const unsigned long long seg_cap = sharded ? cand_cap : cand_cap / EXPAND_SEGS;
-      const unsigned long long c = total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL;
-      sG = seg * seg_cap + c;
-      sOver = c + (unsigned long long)total > seg_cap;  // (c itself may be past the segment: no modulo test)
+#if RMC_TILE_SLOTS
+      if (!sharded) {
+        // a fixed slot range per tile (the buffer holds PB x min(maxsucc,
+        // 256) candidates per tile: cand_cap's sizing), so the base needs no
+        // returning atomic -- the tile's count is added for the host
+        // (generated states) by an atomic whose result nobody waits for
+        const unsigned long long tcap = (unsigned long long)PB * (unsigned long long)min(max_successors(cM), 256);
+        const unsigned long long g0 = (p0 / PB) * tcap;
+        if (total) atomicAdd(&counters[16 * seg], (unsigned long long)total);
+        sG = g0;
+        sOver = (unsigned long long)total > tcap || g0 + (unsigned long long)total > cand_cap;
+      } else
+#endif
+      {
+        const unsigned long long seg_cap = sharded ? cand_cap : cand_cap / EXPAND_SEGS;
+        const unsigned long long c = total ? atomicAdd(&counters[16 * seg], (unsigned long long)total) : 0ULL;
+        sG = seg * seg_cap + c;
+        sOver = c + (unsigned long long)total > seg_cap;  // (c itself may be past the segment: no modulo test)
+      }
     }
   }
   __syncthreads();
@@ -901,6 +989,27 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
   const unsigned long long p0 = (bx * MARK_WPB + w) * WAVE;
   const bool active = p0 < nparents;
   const int np = active ? (int)((nparents - p0) < WAVE ? (nparents - p0) : WAVE) : 0;
+#if RMC_STAGE_BATCH
+  // Wave-local throughout: a wave's parents, carries and candidate range are
+  // its own, so no block barrier (LDS ops of one wave complete in order; the
+  // compiler barrier keeps them in program order).  Each lane loads its
+  // parent's offset and count in one round trip; every step's candidate
+  // words are loaded before the binary searches and the table reads.
+  uint32_t my_off = 0u, my_n = 0u;
+  if (lane < np) {
+    my_off = par_off[p0 + lane];
+    my_n = par_n[p0 + lane];
+  }
+  const uint32_t off0 = __shfl(my_off, 0, WAVE);
+  if (lane < np) {
+    sOff[w][lane] = my_off - off0;
+    sCarry[w][lane] = 0;
+    if (lane == np - 1) sOff[w][np] = my_off + my_n - off0;
+  }
+  wave_lds_sync();
+  const int total = active ? (int)sOff[w][np] : 0;
+  const int steps = total;
+#else
   const uint32_t off0 = active ? par_off[p0] : 0u;
   if (lane < np) {
     sOff[w][lane] = par_off[p0 + lane] - off0;
@@ -919,6 +1028,7 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
       steps = steps > qt ? steps : qt;
     }
   }
+#endif
   uint32_t coll = 0;
   const unsigned long long base0 = pbase + p0 + 1;  // ranks count parents from 1
   // MARK_U steps per round: their candidate and table loads are all issued
@@ -927,6 +1037,37 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
     uint32_t obv[MARK_U];
     unsigned long long slv[MARK_U], vv[MARK_U];
     int pv[MARK_U];
+#if RMC_STAGE_BATCH
+    // (the loads are unconditional -- lanes past the range re-read the
+    // range's last candidate, a DUP reads slot 0 -- so no branch splits them
+    // and the compiler issues them back to back)
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int idx = i0 + u * WAVE + lane;
+      const unsigned long long t = (unsigned long long)off0 + (idx < total ? idx : total - 1);
+      obv[u] = cand_ob[t];
+      slv[u] = cand_slot[t];
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      if (i0 + u * WAVE + lane >= total) obv[u] = OB_ERR;
+      if (obv[u] & OB_ERR) slv[u] = CAND_DUP;  // (the slot word is used only without OB_ERR)
+      const unsigned long long sl = (slv[u] & CAND_DUP) ? 0ULL : (slv[u] & CAND_SLOT_MASK);
+      vv[u] = table[ew * sl + (ew >> 1)];
+      if (slv[u] & CAND_DUP) vv[u] = ~0ULL;
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int idx = i0 + u * WAVE + lane;
+      int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
+      if (idx < total)
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if ((int)sOff[w][mid] <= idx) lo = mid; else hi = mid - 1;
+        }
+      pv[u] = lo;
+    }
+#else
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u) {
       const int idx = i0 + u * WAVE + lane;
@@ -949,6 +1090,7 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u)
       vv[u] = (slv[u] & CAND_DUP) ? ~0ULL : table[ew * (slv[u] & CAND_SLOT_MASK) + (ew >> 1)];
+#endif
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u) {
       const int iu = i0 + u * WAVE, idx = iu + lane, p = pv[u];
@@ -970,7 +1112,11 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
           sCarry[w][p] += (uint32_t)__popcll(m & from & to);
         }
       }
+#if RMC_STAGE_BATCH
+      wave_lds_sync();  // the carries are read by other lanes of this wave in the next step
+#else
       __syncthreads();  // the carries are read by other lanes in the next step
+#endif
     }
   }
   if (lane < np) par_win[p0 + lane] = sCarry[w][lane];
@@ -1001,6 +1147,10 @@ static_assert(MAT_T % 64 == 0 && MAT_T >= 64, "one thread per tile parent");
 // waves per SIMD the register allocation must allow (0: the compiler's choice)
 #ifdef RMC_MAT_WAVES
 #define RMC_MAT_BOUNDS __launch_bounds__(MAT_T, RMC_MAT_WAVES)
+#elif RMC_STAGE_BATCH
+// the batched staging's registers take the N <= 3 library instantiation from
+// 95 to 97 VGPRs (4 waves per SIMD); bounded at 5 it allocates 96, no scratch
+#define RMC_MAT_BOUNDS __launch_bounds__(MAT_T, (N <= 3 && !G) ? 5 : 1)
 #else
 #define RMC_MAT_BOUNDS __launch_bounds__(MAT_T)
 #endif
@@ -1029,6 +1179,29 @@ __global__ RMC_MAT_BOUNDS void k_materialize(const uint32_t* __restrict__ fronti
   const unsigned long long p0 = xcd_tile(blockIdx.x, gridDim.x) * PB;
   const int np = (int)((nparents - p0) < (unsigned long long)PB ? (nparents - p0) : PB);
   const uint32_t start = par_off[p0];
+#if RMC_STAGE_BATCH
+  // every load first (binding table, the tile's offsets and positions, its
+  // rows), then the LDS writes: one round trip (stage_rows_batched)
+  constexpr int DU = (MAXFIXED + MAT_T - 1) / MAT_T;
+  uint32_t vdesc[DU];
+#pragma unroll
+  for (int u = 0; u < DU; u++) vdesc[u] = tid + MAT_T * u < cM.nfixed ? cM.fb_desc[tid + MAT_T * u] : 0u;
+  uint32_t voff = 0, vpos = 0, vn = 0;
+  if (tid < np) {
+    voff = par_off[p0 + tid];
+    vpos = par_pos[p0 + tid];
+    vn = par_n[p0 + tid];
+  }
+  stage_rows_batched<MAT_T, 8>(frontier, p0, np, words, Wp, sS);
+#pragma unroll
+  for (int u = 0; u < DU; u++)
+    if (tid + MAT_T * u < cM.nfixed) sDesc[tid + MAT_T * u] = vdesc[u];
+  if (tid < np) {
+    sOff[tid] = voff - start;
+    sPos[tid] = vpos;
+    if (tid == np - 1) sOff[np] = voff + vn - start;
+  }
+#else
   const uint4* src = reinterpret_cast<const uint4*>(frontier + p0 * (unsigned long long)words);
   for (int q = tid; q < np * (words >> 2); q += MAT_T) {
     const int w = q << 2, p = w / words;
@@ -1045,6 +1218,7 @@ __global__ RMC_MAT_BOUNDS void k_materialize(const uint32_t* __restrict__ fronti
     sPos[tid] = par_pos[p0 + tid];
     if (tid == np - 1) sOff[np] = par_off[p0 + tid] + par_n[p0 + tid] - start;
   }
+#endif
   __syncthreads();
   const int total = (int)sOff[np];
   int my_max = 0;  // largest |DOMAIN messages| this thread wrote (reduced per block below)
@@ -1055,6 +1229,44 @@ __global__ RMC_MAT_BOUNDS void k_materialize(const uint32_t* __restrict__ fronti
     if (tid == 0) sCount = 0;
     __syncthreads();
     const int rn = total - r0 < MAT_LIST ? total - r0 : MAT_LIST;
+#if RMC_STAGE_BATCH
+    // MU steps of MAT_T candidates per batch: their win words and ordinal
+    // words are loaded together (the ordinal words of losers too -- the same
+    // lines), then one LDS reservation per wave for the batch's winners
+    constexpr int MU = 4;
+    for (int b0 = 0; b0 < rn; b0 += MAT_T * MU) {  // block-uniform trip count (ballots)
+      uint32_t cw[MU], cob[MU];
+#pragma unroll
+      for (int u = 0; u < MU; u++) {
+        const int idx = b0 + u * MAT_T + tid;
+        cw[u] = 0u;
+        cob[u] = 0u;
+        if (idx < rn) {
+          cw[u] = (uint32_t)cand_win[start + r0 + idx];
+          cob[u] = cand_ob[start + r0 + idx];
+        }
+      }
+      unsigned long long m[MU];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < MU; u++) {
+        m[u] = __ballot(cw[u] != 0u);
+        cnt += __popcll(m[u]);
+      }
+      int base = 0;
+      if (lane == 0 && cnt) base = atomicAdd(&sCount, cnt);
+      base = __shfl(base, 0, WAVE);
+#pragma unroll
+      for (int u = 0; u < MU; u++) {
+        if (cw[u]) {
+          const int at = base + __popcll(m[u] & lanemask_lt());
+          sList[at] = ((cw[u] - 1u) << 16) | (uint32_t)(r0 + b0 + u * MAT_T + tid);
+          sListOb[at] = cob[u];
+        }
+        base += __popcll(m[u]);
+      }
+    }
+#else
     for (int idx = tid; idx < ((rn + MAT_T - 1) / MAT_T) * MAT_T; idx += MAT_T) {
       const uint32_t cw = idx < rn ? (uint32_t)cand_win[start + r0 + idx] : 0u;
       const bool w = cw != 0;
@@ -1068,6 +1280,7 @@ __global__ RMC_MAT_BOUNDS void k_materialize(const uint32_t* __restrict__ fronti
         sListOb[at] = cand_ob[start + r0 + idx];
       }
     }
+#endif
     __syncthreads();
     const int nw = sCount;
     for (int e = tid; e < nw; e += MAT_T) {

@@ -120,6 +120,7 @@ struct Model {
   uint32_t fb_desc[MAXFIXED];
   uint8_t act_fb_first[MAXACT], act_fb_end[MAXACT];  // action slot -> its fixed bindings [first, end)
   int msg_act_slot[A_NUM];                   // action slot of each message action
+  uint16_t msg_off[A_NUM];                   // = act_off[msg_act_slot[a]]: its first ordinal (one load, not a chain)
   unsigned long long msg_act_mask;           // bit a: message action a is a disjunct of this model's Next
   int ordinal_limit;
   int fpw;                    // fingerprint width in 64-bit words (1: 64-bit, 2: 128-bit)
@@ -1832,8 +1833,7 @@ RMC_HD bool eval_binding(const PState<SPEC, N>& s, const Model& M, int b, Delta&
 // eval_binding returns false without an error, so k_expand evaluates only the
 // (parent, binding) pairs that pass it.
 template <int SPEC, int N, bool G = RMC_G_DEFAULT>
-RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
-  const uint32_t desc = M.fb_desc[b];
+RMC_HD bool may_enable_d(const PState<SPEC, N>& s, const Model& M, uint32_t desc) {  // desc = M.fb_desc[b]
   const int i = (int)((desc >> 24) & 15u), jv = (int)(desc >> 28);
   {
     const int act = (int)((desc >> 16) & 0xFFu);
@@ -1872,6 +1872,10 @@ RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
     case A_SENDPULL: return st == FOLLOWER && i != jv && a_voted(a) == jv;
   }
   return true;
+}
+template <int SPEC, int N, bool G = RMC_G_DEFAULT>
+RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
+  return may_enable_d<SPEC, N, G>(s, M, M.fb_desc[b]);
 }
 
 // Write parent + delta as a packed row of M.words words (a multiple of 4),
