@@ -30,6 +30,11 @@ constexpr unsigned long long EMPTY = ~0ULL;
 // hidden << 47 | slot
 constexpr unsigned long long CAND_DUP = 1ULL << 63;
 constexpr unsigned long long CAND_SLOT_MASK = (1ULL << 47) - 1;
+// k_expand's tile dedup: CAND_REF | hidden << 47 | the candidate index of the
+// same tile round's representative, which inserted the fingerprint (slots
+// are below 2^46, so bit 46 is free in a slot word)
+constexpr unsigned long long CAND_REF = 1ULL << 46;
+constexpr unsigned long long CAND_REF_MASK = CAND_REF - 1;
 constexpr int VAL_RANK_SHIFT = 16;   // val = rank << 16 | hidden
 constexpr int VAL_FLOOR_SHIFT = 26;  // floor = (global index + 1) << 26 (rank << 16 with ordinal 0)
 

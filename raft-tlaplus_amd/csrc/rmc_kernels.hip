@@ -119,10 +119,18 @@ struct Tile {
 };
 
 // Dynamic LDS layout of k_expand (bytes; the launch computes the same).
-constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
-#ifdef RMC_TILE_DEDUP
-constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-successor round
+[[maybe_unused]] constexpr int LIVE_WORDS = 4;  // message bitmask words per parent (kmax <= 124)
+// Phase C's tile-local dedup of the HBM inserts (single shard, 64-bit
+// fingerprints; see k_expand).  Measured and not the default (r06, bench
+// workload, CLI, three interleaved rounds, profiles/r06/ab_tile_dedup.txt):
+// it cuts the inserts from 6.75e9 to 4.23e9 and the memory-side atomics from
+// 9.30e9 to 5.05e9 per check (2.7 per new state; RMC_FPSTATS,
+// profiles/r06/fpstats_tile_dedup.txt), yet k_expand takes 710 ms against
+// 662 -- the atomics are not what bounds it; the round's barrier is.
+#ifndef RMC_TILE_DEDUP
+#define RMC_TILE_DEDUP 0
 #endif
+[[maybe_unused]] constexpr int DEDUP = 256;  // LDS slots of one 256-successor round's table (+ its 256 fingerprints)
 // Persistent k_expand (-DRMC_EXPAND_PERSIST=1, measured and rejected in r05):
 // a grid of resident blocks walks the tiles, and each block stages tile t+G's
 // parent rows into a second LDS buffer by LDS-DMA while tile t runs phases
@@ -146,19 +154,64 @@ constexpr int DEDUP = 256;     // phase C: LDS fingerprint table of one 256-succ
 #ifndef RMC_TILE_SLOTS
 #define RMC_TILE_SLOTS 1
 #endif
+// RMC_LDS_TRIM: the per-parent live-message mask holds (kmax + 31) / 32
+// words instead of LIVE_WORDS, and the tile prefix sBase is 16-bit (a tile
+// has at most 64 x 812 candidates): on the bench workload 20.4 KB per block
+// instead of 21.1 KB, so eight blocks fit a CU's 160 KB of LDS, not seven.
+#ifndef RMC_LDS_TRIM
+#define RMC_LDS_TRIM 1
+#endif
+#if RMC_LDS_TRIM
+typedef uint16_t base_t;
+#else
+typedef uint32_t base_t;
+#endif
+// RMC_ACT_MAJOR: phase C's lanes take the tile's successors grouped by
+// action (action slot, then parent, then ordinal) instead of parent-major, so
+// a wave runs one or two actions' code in eval_known instead of every action
+// its 64 lanes happen to mix.  Each lane still stores its candidate at its
+// TLC-order position in the tile's range, so the candidate layout and every
+// later kernel are unchanged.  Phase B counts each (action slot, parent)
+// pair's successors (16-bit halves of LDS words), and wave 1 turns the counts
+// into a flattened prefix beside wave 0's reservation (no extra barrier).
+// Measured and not the default (r06, bench workload, CLI, three interleaved
+// rounds, profiles/r06/ab_act_major.txt): k_expand 685-686 ms against
+// 661 parent-major -- the lookup (a search over nact x 64 prefixes, a rank
+// below the action's first ordinal) and the scattered candidate stores cost
+// more than the divergence they remove.
+#ifndef RMC_ACT_MAJOR
+#define RMC_ACT_MAJOR 0
+#endif
+#if RMC_ACT_MAJOR && (!RMC_STAGE_BATCH || RMC_EXPAND_PERSIST)
+#error "RMC_ACT_MAJOR stages its tables in the batched one-tile phase A (RMC_STAGE_BATCH=1, RMC_EXPAND_PERSIST=0)"
+#endif
 struct ExpandLds {
-  int Wp, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, off_S2, bytes;
+  int Wp, lw, off_AP, off_Ms, off_Mask, off_Ord, off_Base, off_BOff, off_Live, off_Desc, off_O2b, off_MOff, off_Hash, off_S2, bytes;
 };
-__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes, int nfixed, int nord) {
+__host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int msbytes, int nfixed, int nord, int kmax,
+                                                int nact) {
   ExpandLds L;
+#if RMC_LDS_TRIM
+  L.lw = (kmax + 31) >> 5;
+  if (L.lw < 1) L.lw = 1;
+#else
+  (void)kmax;
+  L.lw = LIVE_WORDS;
+#endif
   L.Wp = words | 1;  // odd row stride: lane-per-parent LDS reads are bank-conflict free
   int o = (PB * L.Wp * 4 + 7) & ~7;
   L.off_Ms = o;  // per-parent message sums (MsgSums<N>, 8 B aligned)
   o += PB * msbytes;
+  L.off_AP = o;  // RMC_ACT_MAJOR: per (action slot, parent) successor counts, then their prefix (u16)
+#if RMC_ACT_MAJOR
+  o += ((nact * PB + 2) * 2 + 7) & ~7;
+#else
+  (void)nact;
+#endif
   L.off_Ord = o;  // per parent: bitmask over TLC ordinals of its enabled bindings
   o += PB * ordw * 4;
   L.off_Base = o;  // exclusive prefix over the tile's parents of their successor counts
-  o += (PB + 1) * 4;
+  o += ((PB + 1) * (int)sizeof(base_t) + 3) & ~3;
   // the model's binding tables, staged once per block: a lane's own binding
   // then costs LDS reads instead of dependent vector loads of __constant__ data
   L.off_Desc = o;  // fixed binding -> descriptor (Model::fb_desc)
@@ -175,9 +228,9 @@ __host__ __device__ inline ExpandLds expand_lds(int PB, int words, int ordw, int
   L.off_BOff = o;  // exclusive prefix over fixed bindings of the passing pairs
   o += (nfixed + 1) * 4;
   L.off_Live = o;  // per parent: bitmask over DOMAIN messages that can enable an action (msg_live)
-  o += PB * LIVE_WORDS * 4;
-#ifdef RMC_TILE_DEDUP
-  const int hash_end = L.off_Hash + DEDUP * 12;
+  o += PB * L.lw * 4;
+#if RMC_TILE_DEDUP
+  const int hash_end = L.off_Hash + DEDUP * 12;  // DEDUP u32 slots + 256 u64 fingerprints
   o = o > hash_end ? o : hash_end;
 #endif
   o = (o + 15) & ~15;
@@ -362,21 +415,26 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   __shared__ unsigned long long sG;
   __shared__ int sOver;
   __shared__ int sAFirst[MAXACT], sAEnd[MAXACT], sAChunk[MAXACT + 1];
+#if RMC_ACT_MAJOR
+  __shared__ uint16_t sAOff[MAXACT + 1];  // action slot -> its first ordinal (Model::act_off), + ordinal_limit
+  __shared__ uint8_t sMSlot[A_NUM];       // message action id -> its action slot (Model::msg_act_slot)
+#endif
   using MS = typename SumsOf<N, FPW>::T;
   // the tile's LDS arrays (the same layout in both kernel forms)
 #define RMC_EXPAND_LDS_ARRAYS                                                                         \
   const int words = cM.words, ordw = cM.ord_words;                                                     \
-  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS), cM.nfixed, cM.ordinal_limit);      \
+  const ExpandLds L = expand_lds(PB, words, ordw, (int)sizeof(MS), cM.nfixed, cM.ordinal_limit, cM.kmax, cM.nact); \
   MS* sMS = (MS*)(lds + L.off_Ms);                                                                     \
   uint32_t* sOrd = (uint32_t*)(lds + L.off_Ord);                                                       \
-  uint32_t* sBase = (uint32_t*)(lds + L.off_Base);                                                     \
+  base_t* sBase = (base_t*)(lds + L.off_Base);                                                         \
   uint32_t* sLive = (uint32_t*)(lds + L.off_Live);                                                     \
   unsigned long long* sMask = (unsigned long long*)(lds + L.off_Mask);                                 \
   uint32_t* sBOff = (uint32_t*)(lds + L.off_BOff);                                                     \
   uint32_t* sDesc = (uint32_t*)(lds + L.off_Desc);                                                     \
   uint16_t* sO2b = (uint16_t*)(lds + L.off_O2b);                                                       \
   uint16_t* sMOff = (uint16_t*)(lds + L.off_MOff);                                                     \
-  (void)sMS, (void)sOrd, (void)sBase, (void)sLive, (void)sMask, (void)sBOff, (void)sDesc, (void)sO2b, (void)sMOff;
+  uint16_t* sAP = (uint16_t*)(lds + L.off_AP);                                                          \
+  (void)sMS, (void)sOrd, (void)sBase, (void)sLive, (void)sMask, (void)sBOff, (void)sDesc, (void)sO2b, (void)sMOff, (void)sAP;
 #ifdef RMC_STAMPS
   unsigned long long t_prev = clock64();
 #endif
@@ -433,7 +491,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
                        (uint32_t*)(lds + (buf ? 0 : L.off_S2)));
     }
     for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
-    for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
+    for (int q = tid; q < PB * L.lw; q += 256) sLive[q] = 0;
     for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
     __syncthreads();
 #else
@@ -455,11 +513,20 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     uint32_t vo2b[4];  // ordinal_limit < 1024
     // each action slot's fixed bindings (phase B's chunk table, wave 0)
     const int vfirst = tid < cM.nact ? (int)cM.act_fb_first[tid] : 0, vend = tid < cM.nact ? (int)cM.act_fb_end[tid] : 0;
+#if RMC_ACT_MAJOR
+    const int vaoff = tid < cM.nact ? cM.act_off[tid] : cM.ordinal_limit;
+    const int vmslot = tid < A_NUM ? cM.msg_act_slot[tid] : 0;
+#endif
 #pragma unroll
     for (int u = 0; u < 4; u++) vo2b[u] = tid + 256 * u < cM.ordinal_limit ? (uint32_t)cM.ord2b[tid + 256 * u] : 0u;
     stage_rows_batched<256, 4>(frontier, p0, np, words, L.Wp, sS);
     if (tid < cM.nfixed) sDesc[tid] = vdesc;
     if (tid < A_NUM) sMOff[tid] = (uint16_t)vmoff;
+#if RMC_ACT_MAJOR
+    if (tid <= cM.nact) sAOff[tid] = (uint16_t)vaoff;
+    if (tid < A_NUM) sMSlot[tid] = (uint8_t)vmslot;
+    for (int q = tid; q < (cM.nact * PB + 2) / 2; q += 256) ((uint32_t*)sAP)[q] = 0;
+#endif
 #pragma unroll
     for (int u = 0; u < 4; u++)
       if (tid + 256 * u < cM.ordinal_limit) sO2b[tid + 256 * u] = (uint16_t)vo2b[u];
@@ -470,7 +537,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     for (int q = tid; q < A_NUM; q += 256) sMOff[q] = (uint16_t)cM.act_off[cM.msg_act_slot[q]];
 #endif
     for (int q = tid; q < PB * ordw; q += 256) sOrd[q] = 0;
-    for (int q = tid; q < PB * LIVE_WORDS; q += 256) sLive[q] = 0;
+    for (int q = tid; q < PB * L.lw; q += 256) sLive[q] = 0;
     for (int q = tid; q < PB * (int)(sizeof(MS) / 4); q += 256) ((uint32_t*)sMS)[q] = 0;
     __syncthreads();
 #endif
@@ -497,7 +564,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       for (int k = tid / PB; k < nm; k += bstride) {
         int src, dst;
         const uint32_t w = s.msg(k);
-        if (msg_live<SPEC, N>(s, w)) atomicOr(&sLive[p * LIVE_WORDS + (k >> 5)], 1u << (k & 31));
+        if (msg_live<SPEC, N>(s, w)) atomicOr(&sLive[p * L.lw + (k >> 5)], 1u << (k & 31));
         const uint64_t u = msg_u<SPEC>(w, src, dst);
         MsgSums<N>& m1 = sums1<N>(sMS[p]);
         atomicAdd(&m1.sig[src], (uint32_t)u);
@@ -513,7 +580,12 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     STAMP(15);  // message sums done (diagnostic build: phase B split)
     // eval_one: one (parent pp, binding b) pair; enabled -> the ordinal bit,
     // errors and message-capacity overflow flagged
-    auto record = [&](int pp, int b, const Delta& d) {
+    auto record = [&](int pp, int b, const Delta& d, int slot) {
+#if RMC_ACT_MAJOR
+      atomicAdd((uint32_t*)sAP + ((slot * PB + pp) >> 1), 1u << (16 * (pp & 1)));
+#else
+      (void)slot;
+#endif
       if (d.err) {
         if (d.err == E_DOMAIN) atomicMin(&st->err_key, order_key(pbase + p0 + pp, d.ordinal, b));
         else atomicOr(&st->cap_flags, 1u << d.err);
@@ -604,7 +676,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           PState<SPEC, N> s{sS + pp * L.Wp};
           Delta d;
           // (x from the LDS descriptor: a per-lane cM.fb_x load was a dependent round trip per chunk)
-          if (eval_fixed<SPEC, N, G>(s, cM, a, (int)((sDesc[lo] >> 8) & 0xFFu), d)) record(pp, lo, d);
+          if (eval_fixed<SPEC, N, G>(s, cM, a, (int)((sDesc[lo] >> 8) & 0xFFu), d)) record(pp, lo, d, a);
         }
       }
     }
@@ -641,8 +713,8 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
 #endif
       // the parent's live messages, every 4th one per wave
       int t = 0;
-      for (int q = 0; q < LIVE_WORDS; q++) {
-        uint32_t x = sLive[p * LIVE_WORDS + q];
+      for (int q = 0; q < L.lw; q++) {
+        uint32_t x = sLive[p * L.lw + q];
         while (x) {
           const int k = 32 * q + __ffs(x) - 1;
           x &= x - 1u;
@@ -651,7 +723,11 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
             d.srv = -1; d.nops = 0; d.hdr = s.hdr(); d.err = 0; d.act = -1;
             if (act_message<SPEC, N>(s, cM, k, d)) {
               d.ordinal = sMOff[d.act] + k;
-              record(p, cM.nfixed + k, d);
+#if RMC_ACT_MAJOR
+              record(p, cM.nfixed + k, d, sMSlot[d.act]);
+#else
+              record(p, cM.nfixed + k, d, 0);
+#endif
             }
           }
         }
@@ -666,7 +742,12 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           for (int k = 0; k < nm; k++)
             if ((t++ & (bstride - 1)) == w0) {
               Delta d;
-              if (eval_msgc<SPEC, N>(s, cM, q, k, off + k, d)) record(p, cM.nfixed + MSGC_STRIDE * (1 + q) + k, d);
+#if RMC_ACT_MAJOR
+              if (eval_msgc<SPEC, N>(s, cM, q, k, off + k, d))
+                record(p, cM.nfixed + MSGC_STRIDE * (1 + q) + k, d, sMSlot[A_C0 + q]);
+#else
+              if (eval_msgc<SPEC, N>(s, cM, q, k, off + k, d)) record(p, cM.nfixed + MSGC_STRIDE * (1 + q) + k, d, 0);
+#endif
             }
         }
       }
@@ -685,7 +766,7 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       int y = __shfl_up(incl, o, WAVE);
       if (tid >= o) incl += y;
     }
-    if (tid < PB) sBase[tid + 1] = (uint32_t)incl;
+    if (tid < PB) sBase[tid + 1] = (base_t)incl;
     if (tid == 0) sBase[0] = 0;
     int total = __shfl(incl, 63, WAVE);
     // one reservation per tile.  The single-shard search spreads them over 8
@@ -720,6 +801,30 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       }
     }
   }
+#if RMC_ACT_MAJOR
+  if (tid >= 64 && tid < 128) {  // wave 1, beside wave 0's reservation: the flattened
+    // exclusive prefix over (action slot, parent) of phase B's counts, in place;
+    // sAP[nact * PB] = the tile's total
+    const int l = tid - 64;
+    unsigned carry = 0;
+    for (int a = 0; a < cM.nact; a++) {
+      const unsigned c = sAP[a * PB + l];
+      unsigned incl = c;
+#pragma unroll
+      for (int o = 1; o < WAVE; o <<= 1) {
+        const unsigned y = __shfl_up(incl, o, WAVE);
+        if (l >= o) incl += y;
+      }
+      sAP[a * PB + l] = (uint16_t)(carry + incl - c);
+      carry += __shfl(incl, WAVE - 1, WAVE);
+    }
+    if (l == 0) sAP[cM.nact * PB] = (uint16_t)carry;
+  }
+#endif
+#if RMC_TILE_DEDUP
+  // phase C's dedup table for round 0 (its bytes are phase B's, dead now)
+  if (FPW == 1 && !sharded) ((uint32_t*)(lds + L.off_Hash))[tid] = ~0u;
+#endif
   __syncthreads();
   const int total = (int)sBase[np];
   const unsigned long long gbase = sG;
@@ -771,33 +876,36 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   //      candidate gbase + idx, so a wave's candidate stores are contiguous
   //      (binding-major enumeration scattered them: one 32 B write request per
   //      8 B store, ~0.7 GB of extra HBM writes per launch on the bench cfg).
-#ifdef RMC_TILE_DEDUP
-  // Measured and not the default (r03, bench workload, CLI): k_expand 933 ms
-  // per check with the tile dedup vs 918 ms without -- the LDS table's three
-  // barriers per 256-successor round cost more than the HBM probes it saves.
+#if RMC_TILE_DEDUP
+  // Tile-local dedup of the inserts (single shard, 64-bit fingerprints).
+  // Phase C's successors come in rounds of 256 (lane = tid).  Successors of
+  // the same round with the same fingerprint (commuting actions of sibling
+  // parents) send ONE insert to the HBM set: the lowest round index, which is
+  // the lowest TLC rank, since candidates are numbered in TLC order.  The
+  // others could never lower that entry's minimum.  They store CAND_REF |
+  // hidden << 47 | the representative's candidate index, and k_mark_tiles
+  // reads the entry through it (never a winner; hidden collisions are
+  // counted as if they had inserted).  The LDS table: DEDUP u32 slots, each
+  // holding the lowest round index of its key (~0 = empty), plus the round's
+  // fingerprints by index for the key compare.  Unlike the r03 form (three
+  // barriers per round; the others waited for their representative's insert
+  // to learn its slot), one barrier per round, and no lane waits on another's
+  // HBM insert.  Round 0's table is cleared before the reservation barrier.
   if constexpr (FPW == 1) {
-    if (!sharded) {
-      // Tile-local dedup first.  A BFS level's duplicates are same-level ones
-      // (0.7% of the bench workload's successors are of an earlier level),
-      // and 37% of all successors repeat a fingerprint another successor of
-      // the SAME 64-parent tile produced (commuting actions of sibling
-      // parents; CPU census).  Per round of 256 successors
-      // an LDS table keeps each fingerprint's first successor in TLC order
-      // (the lowest idx: candidates are in TLC order), and only that
-      // representative touches the HBM set -- it carries the tile's lowest
-      // rank, so the others could never lower the entry's min.  They share
-      // its slot: k_mark's win test and hidden-variable collision count read
-      // the entry exactly as if they had inserted.
-      unsigned long long* sHK = (unsigned long long*)(lds + L.off_Hash);
-      uint32_t* sHR = (uint32_t*)(lds + L.off_Hash + DEDUP * 8);
+    if (!sharded && !diag) {
+      uint32_t* sDT = (uint32_t*)(lds + L.off_Hash);
+      unsigned long long* sDF = (unsigned long long*)(lds + L.off_Hash + DEDUP * 4);
       for (int r0 = 0; r0 < total; r0 += 256) {
-        sHK[tid] = EMPTY;
-        sHR[tid] = 0xFFFFFFFFu;
-        __syncthreads();
+        if (r0) {  // the previous round is done with the table
+          __syncthreads();
+          sDT[tid] = ~0u;
+          __syncthreads();
+        }
         const int idx = r0 + tid;
         const bool act = idx < total;
-        uint32_t obw = OB_ERR;  // the candidate's ordinal/binding word (the Delta is dead after the fp)
+        uint32_t obw = OB_ERR;
         unsigned long long fp = 0, val = 0;
+        int h = 0;
         if (act) {
           int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
           while (lo < hi) {
@@ -811,40 +919,37 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
           Delta d;
           eval_known<SPEC, N, G>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
           obw = ((uint32_t)d.ordinal << 16) | (uint32_t)b | (d.err ? OB_ERR : 0u);
-          if (diag == 2) fp = (unsigned long long)d.hdr ^ d.w[0] ^ d.opc[0];  // the delta only
-          else if (!d.err) {
+          if (!d.err) {
             const unsigned long long pg = pbase + p0 + p;
             val = ((((pg + 1) << 10) | (unsigned long long)d.ordinal) << VAL_RANK_SHIFT) |
                   (unsigned long long)hidden_of<SPEC>(d.hdr);
             fp = delta_fp_sums<SPEC, N>(s, cM, d, sums1<N>(sMS[p]));
+            sDF[tid] = fp;  // before the claim below: a lane that finds tid in a slot reads it
+            asm volatile("" ::: "memory");
+            h = (int)((fp ^ (fp >> 31)) & (DEDUP - 1));
+            for (;;) {  // at most 256 keys in DEDUP slots: a slot is always found
+              const uint32_t v = atomicCAS(&sDT[h], ~0u, (uint32_t)tid);
+              if (v == ~0u) break;
+              if (sDF[v] == fp) {
+                atomicMin(&sDT[h], (uint32_t)tid);
+                break;
+              }
+              h = (h + 1) & (DEDUP - 1);
+            }
           }
         }
-        const bool ok = act && !(obw & OB_ERR) && diag != 2;
-        int h = 0;
-        if (ok) {
-          h = (int)((fp ^ (fp >> 32)) & (DEDUP - 1));
-          for (;;) {  // at most 256 keys in DEDUP slots: a slot is always found
-            const unsigned long long prev = atomicCAS(&sHK[h], EMPTY, fp);
-            if (prev == EMPTY || prev == fp) break;
-            h = (h + 1) & (DEDUP - 1);
-          }
-          atomicMin(&sHR[h], (uint32_t)tid);
-        }
         __syncthreads();
-        const bool rep = ok && sHR[h] == (uint32_t)tid;
-        unsigned long long raw = EMPTY;
-        if (rep) {
-          raw = diag == 1 ? (fp & CAND_SLOT_MASK) : fpset_insert(table, mask, fp, val, floor, st);
-          sHK[h] = raw;  // keys are not read again this round: the slot in their place
+        unsigned long long slot = CAND_DUP;
+        if (act && !(obw & OB_ERR)) {
+          const uint32_t rep = sDT[h];
+          if (rep == (uint32_t)tid) slot = cand_word(fpset_insert(table, mask, fp, val, floor, st), val);
+          else slot = CAND_REF | ((val & 0xFFFFULL) << 47) | (gbase + (unsigned long long)(r0 + (int)rep));
         }
-        __syncthreads();
-        if (ok && !rep) raw = sHK[h];
         if (act) {
           const unsigned long long t = gbase + (unsigned long long)idx;
-          cand_slot[t] = diag == 2 ? fp : ok ? cand_word(raw, val) : CAND_DUP;
+          cand_slot[t] = slot;
           cand_ob[t] = obw;
         }
-        __syncthreads();  // the next round resets the table
       }
       STAMP(3);
       continue;
@@ -858,6 +963,19 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
   // check, yet k_expand took 1,019 ms instead of 824: the LDS table costs
   // more than the HBM operations it saves.  profiles/r04/ab_wave_dedup_r04w.txt)
   for (int idx = tid; idx < total; idx += 256) {
+#if RMC_ACT_MAJOR
+    // lane idx -> (action slot a, parent p, its j-th successor of that action):
+    // the last flattened entry whose prefix is <= idx (it has a successor)
+    int lo = 0, hi = cM.nact * PB - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int)sAP[mid] <= idx) lo = mid; else hi = mid - 1;
+    }
+    const int p = lo & (PB - 1), a = lo / PB;
+    const int r = rank_below(sOrd + p * ordw, sAOff[a]) + (idx - (int)sAP[lo]);  // its rank among p's successors
+    const int ord = select_bit(sOrd + p * ordw, r);
+    const int pos = (int)sBase[p] + r;  // its TLC-order position in the tile
+#else
     int lo = 0, hi = np - 1;  // parent p: sBase[p] <= idx < sBase[p+1]
     while (lo < hi) {
       int mid = (lo + hi + 1) >> 1;
@@ -865,11 +983,13 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
     }
     const int p = lo;
     const int ord = select_bit(sOrd + p * ordw, idx - (int)sBase[p]);
+    const int pos = idx;
+#endif
     const int b = sO2b[ord];
     PState<SPEC, N> s{sS + p * L.Wp};
     Delta d;
     eval_known<SPEC, N, G>(s, cM, b, b < cM.nfixed ? sDesc[b] : 0u, ord, d);
-    const unsigned long long t = gbase + (unsigned long long)idx;
+    const unsigned long long t = gbase + (unsigned long long)pos;
     const unsigned long long pg = pbase + p0 + p;
     unsigned long long slot = CAND_DUP;
     uint32_t local = 0;
@@ -944,8 +1064,11 @@ __global__ __launch_bounds__(256) void k_mark(unsigned long long nparents, unsig
       const uint32_t t = t0 + u;
       ob[u] = t < off + n ? cand_ob[t] : OB_ERR;
       sl[u] = (ob[u] & OB_ERR) ? CAND_DUP : cand_slot[t];
+      unsigned long long w = sl[u];
+      if (!(w & CAND_DUP) && (w & CAND_REF)) w = cand_slot[w & CAND_REF_MASK];  // tile-dedup reference
+      if (w & CAND_DUP) sl[u] = CAND_DUP;
       // entry = ew words, value in the word after the key (ew 2: fp, val; ew 4: fp.a, fp.b, val, -)
-      v[u] = (sl[u] & CAND_DUP) ? ~0ULL : table[ew * (sl[u] & CAND_SLOT_MASK) + (ew >> 1)];
+      v[u] = (w & CAND_DUP) ? ~0ULL : table[ew * (w & CAND_SLOT_MASK) + (ew >> 1)];
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -1048,13 +1171,26 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
       obv[u] = cand_ob[t];
       slv[u] = cand_slot[t];
     }
+    // a tile-dedup reference (CAND_REF) reads the entry through its
+    // representative's word (same tile: an L2 hit); its own rank and hidden
+    // bits then make it a loser and count its collision (fpset_won)
+    unsigned long long rw[MARK_U];
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u) {
       if (i0 + u * WAVE + lane >= total) obv[u] = OB_ERR;
       if (obv[u] & OB_ERR) slv[u] = CAND_DUP;  // (the slot word is used only without OB_ERR)
-      const unsigned long long sl = (slv[u] & CAND_DUP) ? 0ULL : (slv[u] & CAND_SLOT_MASK);
+      const bool ref = !(slv[u] & CAND_DUP) && (slv[u] & CAND_REF);
+      rw[u] = cand_slot[ref ? (slv[u] & CAND_REF_MASK) : (unsigned long long)off0];
+      if (!ref) rw[u] = slv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const unsigned long long sl = (rw[u] & CAND_DUP) ? 0ULL : (rw[u] & CAND_SLOT_MASK);
       vv[u] = table[ew * sl + (ew >> 1)];
-      if (slv[u] & CAND_DUP) vv[u] = ~0ULL;
+      if (rw[u] & CAND_DUP) {
+        vv[u] = ~0ULL;
+        slv[u] = CAND_DUP;  // (a representative whose insert failed: the chunk is redone)
+      }
     }
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u) {
@@ -1088,8 +1224,12 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
       }
     }
 #pragma unroll
-    for (int u = 0; u < MARK_U; ++u)
-      vv[u] = (slv[u] & CAND_DUP) ? ~0ULL : table[ew * (slv[u] & CAND_SLOT_MASK) + (ew >> 1)];
+    for (int u = 0; u < MARK_U; ++u) {
+      unsigned long long w = slv[u];
+      if (!(w & CAND_DUP) && (w & CAND_REF)) w = cand_slot[w & CAND_REF_MASK];  // tile-dedup reference
+      if (w & CAND_DUP) slv[u] = CAND_DUP;
+      vv[u] = (w & CAND_DUP) ? ~0ULL : table[ew * (w & CAND_SLOT_MASK) + (ew >> 1)];
+    }
 #endif
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u) {
@@ -1313,16 +1453,25 @@ __global__ RMC_MAT_BOUNDS void k_materialize(const uint32_t* __restrict__ fronti
         tp = tr_parent + out_base_global + dst;
         tb = tr_bind + out_base_global + dst;
       }
+      // All three point into device memory; typed so, the stores are global_*
+      // rather than flat_* (a pointer read from `pieces` is generic).  A flat
+      // store counts in lgkmcnt too, so every LDS wait after one also waited
+      // for the store to reach memory: the row's 16 B stores went out one
+      // HBM write round trip apart.  (A generic -> global -> generic cast
+      // round trip is folded away; the pointers must stay global-typed.)
+      gu32* go = (gu32*)o;
+      __attribute__((address_space(1))) unsigned long long* gtp = (__attribute__((address_space(1))) unsigned long long*)tp;
+      __attribute__((address_space(1))) uint16_t* gtb = (__attribute__((address_space(1))) uint16_t*)tb;
       int nn = 0;
-      int err = apply_delta<SPEC, N>(s, cM, d, o, &nn);
+      int err = apply_delta<SPEC, N, gu32*>(s, cM, d, go, &nn);
       if (err) atomicOr(&st->cap_flags, 1u << err);
       my_max = nn > my_max ? nn : my_max;
 #ifdef RMC_ROWSTATS
       my_words += (unsigned long long)((1 + 4 * N + nn + 3) & ~3);
 #endif
       const unsigned long long pg = pbase + p0 + p;
-      *tp = pg;
-      *tb = (uint16_t)b;
+      *gtp = pg;
+      *gtb = (uint16_t)b;
       // invariants read only the header and the server words: check them on
       // the parent + delta in place (SuccView), not on the row written to HBM
       const SuccView<SPEC, N> ns(s, d);
@@ -1362,7 +1511,12 @@ __global__ __launch_bounds__(256) void k_owner_count(const unsigned long long* _
   if (threadIdx.x < W) h[threadIdx.x] = 0;
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n && !(cand_ob[t] & (OB_ERR | OB_LOCAL | OB_TDUP))) atomicAdd(&h[fp_owner(cand_fp[t], W)], 1u);
+  if (t < n) {
+    uint32_t ob = cand_ob[t];
+    unsigned long long fp = cand_fp[t];  // loaded beside ob (used only for a remote candidate)
+    asm volatile("" : "+v"(ob), "+v"(fp));  // both loads issued before the branch (hipcc would sink fp's past it)
+    if (!(ob & (OB_ERR | OB_LOCAL | OB_TDUP))) atomicAdd(&h[fp_owner(fp, W)], 1u);
+  }
   __syncthreads();
   if (threadIdx.x < W) blk_counts[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
@@ -1457,16 +1611,22 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
   __syncthreads();
   unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  if (cand_ob[t] & (OB_ERR | OB_LOCAL | OB_TDUP)) {
+  // the candidate's three words loaded together (fp and val are used only
+  // for a remote candidate; the lines are read anyway)
+  uint32_t ob = cand_ob[t];
+  unsigned long long fp = cand_fp[t], val = cand_val[t];
+  asm volatile("" : "+v"(ob), "+v"(fp), "+v"(val));  // all three issued before the branch (hipcc would sink two)
+  if (ob & (OB_ERR | OB_LOCAL | OB_TDUP)) {
     perm[t] = 0xFFFFFFFFu;
     return;
   }
-  unsigned long long fp = cand_fp[t];
   const int o = fp_owner(fp, W);
   unsigned pos = atomicAdd(&h[o], 1u);
-  unsigned long long* dst = reinterpret_cast<unsigned long long*>(db[o] + 16ULL * pos);
+  // a device address (another shard's receive buffer, or send): global stores
+  __attribute__((address_space(1))) unsigned long long* dst =
+      reinterpret_cast<__attribute__((address_space(1))) unsigned long long*>(db[o] + 16ULL * pos);
   dst[0] = fp;
-  dst[1] = cand_val[t];
+  dst[1] = val;
   perm[t] = pos;
 }
 
@@ -1480,30 +1640,70 @@ __global__ __launch_bounds__(256) void k_insert_recv(const unsigned long long* _
                                                      unsigned long long floor,
                                                      unsigned long long* __restrict__ recv_slot, DevStatus* st) {
   // RECV_U records per thread (consecutive records on consecutive threads of
-  // each step, for the L2 locality of a parent's duplicates): their first
-  // probe groups are loaded together, then inserted in record order
+  // each step, for the L2 locality of a parent's duplicates).  Three batched
+  // memory steps: every record loaded (unconditionally: lanes past n re-read
+  // the last record, so no branch splits the batch and hipcc issues the
+  // loads back to back), every first probe group loaded, every CAS a group
+  // left to do issued; only a CAS lost to another key (rare) falls back to
+  // the probe loop.  (The r04 form loaded the records and ran the CAS of
+  // each record after the previous one's had returned: eight dependent
+  // round trips per thread.)
   constexpr int U = RECV_U;
+  if (n == 0) return;
   const unsigned long long j0 = (unsigned long long)blockIdx.x * blockDim.x * U + threadIdx.x;
-  unsigned long long fp[U], v[U];
+  unsigned long long fp[U], v[U], slot[U], prev[U];
   ulonglong2 e[U][4];
-  bool ld[U];
+  bool ld[U], cas[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
-    if (j < n) {
-      fp[u] = recv[2 * j];
-      v[u] = recv[2 * j + 1];
+    const unsigned long long jc = j < n ? j : n - 1;
+    fp[u] = recv[2 * jc];
+    v[u] = recv[2 * jc + 1];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) ld[u] = fpset_group_load(table, mask, fp[u], e[u]);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
+    slot[u] = EMPTY;
+    cas[u] = false;
+    if (j >= n) continue;
+    unsigned long long s0 = fp_slot(fp[u], mask);
+    if (ld[u]) {
+      int k = 4;
+      unsigned long long kv = 0;
+      bool found = false;
+#pragma unroll
+      for (int q = 3; q >= 0; q--)
+        if (e[u][q].x == fp[u] || e[u][q].x == EMPTY) { k = q; kv = e[u][q].y; found = e[u][q].x == fp[u]; }
+      if (found) {  // decided by the group: an earlier level's copy needs nothing, a same-level one its min
+        s0 = (s0 + (unsigned long long)k) & mask;
+        if (kv >= floor && v[u] < kv) atomicMin(table + 2 * s0 + 1, v[u]);
+        slot[u] = s0;
+        continue;
+      }
+      if (k < 4) {  // the first EMPTY of the group: claim it
+        slot[u] = (s0 + (unsigned long long)k) & mask;
+        cas[u] = true;
+      }
     }
   }
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
-    ld[u] = j < n && fpset_group_load(table, mask, fp[u], e[u]);
-  }
+  for (int u = 0; u < U; u++)
+    if (cas[u]) prev[u] = atomicCAS(table + 2 * slot[u], EMPTY, fp[u]);
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
-    if (j < n) recv_slot[j] = cand_word(fpset_insert_loaded(table, mask, fp[u], v[u], floor, st, e[u], ld[u]), v[u]);
+    if (j >= n) continue;
+    if (cas[u] && (prev[u] == EMPTY || prev[u] == fp[u])) {
+      atomicMin(table + 2 * slot[u] + 1, v[u]);  // claimed, or claimed since the load: the min (as fpset_insert)
+    } else if (slot[u] == EMPTY || cas[u]) {
+      // no group (table end), four other keys, or the slot went to another
+      // key since the load: the probe loop from the group's start
+      slot[u] = fpset_insert_loaded(table, mask, fp[u], v[u], floor, st, e[u], ld[u] && !cas[u]);
+    }
+    recv_slot[j] = cand_word(slot[u], v[u]);
   }
 }
 
@@ -1529,14 +1729,19 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
     __syncthreads();
   }
   const unsigned long long j0 = (unsigned long long)blockIdx.x * blockDim.x * U + threadIdx.x;
-  unsigned long long rs[U], tv[U];
+  unsigned long long rs[U], tv[U], mv[U];
+  // every record's slot word and value first (unconditional: lanes past n
+  // re-read the last record), then every table read (a DUP reads slot 0)
+  if (n == 0) return;
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const unsigned long long j = j0 + (unsigned long long)u * blockDim.x;
-    rs[u] = j < n ? recv_slot[j] : CAND_DUP;
+    const unsigned long long jc = j < n ? j : n - 1;
+    rs[u] = recv_slot[jc];
+    mv[u] = recv[2 * jc + 1];
   }
 #pragma unroll
-  for (int u = 0; u < U; u++) tv[u] = (rs[u] & CAND_DUP) ? 0ULL : table[2 * (rs[u] & CAND_SLOT_MASK) + 1];
+  for (int u = 0; u < U; u++) tv[u] = table[2 * ((rs[u] & CAND_DUP) ? 0ULL : (rs[u] & CAND_SLOT_MASK)) + 1];
   unsigned int wins = 0, colls = 0;
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -1544,7 +1749,7 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
     if (j >= n) continue;
     bool w = false, c = false;
     if (!(rs[u] & CAND_DUP)) {
-      const unsigned long long mine = recv[2 * j + 1];
+      const unsigned long long mine = mv[u];
       w = fpset_won(tv[u], mine >> VAL_RANK_SHIFT, floor, mine, c);
       colls += c;
     }
@@ -1557,7 +1762,7 @@ __global__ __launch_bounds__(256) void k_mark_recv(const unsigned long long* __r
         const int mid = (lo + hi + 1) >> 1;
         if (srs[mid] <= j) lo = mid; else hi = mid - 1;
       }
-      *reinterpret_cast<uint8_t*>(sfb[lo] + j) = fl;
+      *reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(sfb[lo] + j) = fl;  // global, not flat (no lgkm wait)
     } else {
       flag[j] = fl;
     }
@@ -1598,28 +1803,54 @@ __global__ __launch_bounds__(256) void k_mark_gen(unsigned long long nparents, u
     const uint32_t off = par_off[p], n = par_n[p];
     uint32_t cnt = 0;
     const unsigned long long base = (pbase + p + 1) << 10;
-    constexpr int U = 8;  // independent reads issued together, as in k_mark
+    constexpr int U = 8;
+    // A candidate's decision is a chain of up to four dependent reads (its
+    // ob word; then its slot word, value or record position; then the table
+    // entry, the owner's flag or a tile representative's position; then
+    // that one's flag).  Each stage is read for all U candidates of a step
+    // before the next stage starts, every load unconditional (an unused
+    // stage reads index 0 / the step's first candidate), so a step costs four
+    // round trips instead of up to four per candidate.
     for (uint32_t t0 = off; t0 < off + n; t0 += U) {
-      uint32_t ob[U];
+      uint32_t ob[U], pq[U], pt[U];
+      uint8_t fb[U], fb2[U];
       bool w[U];
-      unsigned long long v[U], mine[U];
+      unsigned long long v[U], mine[U], cv[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const uint32_t t = t0 + u;
-        ob[u] = t < off + n ? cand_ob[t] : OB_ERR;
+        const uint32_t t = t0 + u < off + n ? t0 + u : off + n - 1;
+        ob[u] = cand_ob[t];
+        mine[u] = cand_fp[t];
+        cv[u] = cand_val[t];
+        pq[u] = perm[t];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (t0 + u >= off + n) ob[u] = OB_ERR;
+        const bool local = (ob[u] & (OB_ERR | OB_LOCAL)) == OB_LOCAL;
+        if (local && (mine[u] & CAND_DUP)) ob[u] |= OB_ERR;  // the insert failed: the round was redone
+        const bool loc = (ob[u] & (OB_ERR | OB_LOCAL)) == OB_LOCAL, tdup = !(ob[u] & (OB_ERR | OB_LOCAL)) && (ob[u] & OB_TDUP);
+        const bool remote = !(ob[u] & (OB_ERR | OB_LOCAL | OB_TDUP));
+        v[u] = table[2 * (loc && !moved ? (mine[u] & CAND_SLOT_MASK) : 0ULL) + 1];
+        fb[u] = flag_back[remote ? pq[u] : 0u];
+        pt[u] = perm[tdup ? (uint32_t)cv[u] : 0u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const bool tdup = !(ob[u] & (OB_ERR | OB_LOCAL)) && (ob[u] & OB_TDUP);
+        fb2[u] = flag_back[tdup ? pt[u] : 0u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
         w[u] = false;
-        v[u] = mine[u] = 0;
         if (ob[u] & OB_ERR) continue;
         if (ob[u] & OB_LOCAL) {
-          mine[u] = cand_fp[t];  // hidden << 47 | slot, or CAND_DUP (the insert failed: the round was redone)
-          if (mine[u] & CAND_DUP) { ob[u] |= OB_ERR; continue; }
-          v[u] = moved ? fpset_value(table, mask, cand_val[t]) : table[2 * (mine[u] & CAND_SLOT_MASK) + 1];
+          if (moved) v[u] = fpset_value(table, mask, cv[u]);  // the set was rehashed since the insert
           mine[u] >>= 47;
         } else if (ob[u] & OB_TDUP) {  // loses to its tile's representative; collides when that did
-          coll += flag_back[perm[(uint32_t)cand_val[t]]] == 2 ? 1u : 0u;
+          coll += fb2[u] == 2 ? 1u : 0u;
         } else {
-          const uint32_t q = perm[t];
-          w[u] = flag_back[q] == 1;
+          w[u] = fb[u] == 1;
         }
       }
 #pragma unroll
@@ -1709,7 +1940,7 @@ struct Launch {
     unsigned long long blocks = (a.nparents + PB - 1) / PB;
     const Model& M = *a.model;
     ExpandLds L = expand_lds(PB, M.words, M.ord_words, (int)sizeof(typename SumsOf<N, FPW>::T), M.nfixed,
-                             M.ordinal_limit);
+                             M.ordinal_limit, M.kmax, M.nact);
 #if RMC_EXPAND_PERSIST
     {  // resident blocks only: as many as the CUs hold at this LDS size
       static int cached_bytes = -1, cached_grid = 0;

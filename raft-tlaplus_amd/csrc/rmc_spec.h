@@ -1883,8 +1883,26 @@ RMC_HD bool may_enable(const PState<SPEC, N>& s, const Model& M, int b) {
 // most MAXOPS) are sorted in registers and merged into the parent's message
 // list (with its in-place count changes); the row leaves through a 4-word
 // register window, 16 B per store on the device.  Rows are 16 B aligned.
-template <int SPEC, int N>
-RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d, uint32_t* out, int* nmsg_out = nullptr) {
+// The 16 B row stores of apply_delta: through a generic pointer (host rows,
+// k_simulate's LDS rows) or a global one (k_materialize: global_store, not
+// flat_store -- a flat store counts in lgkmcnt too, so each later LDS wait
+// would also wait for the store to reach HBM).
+RMC_HD void row_store4(uint32_t* o, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *reinterpret_cast<uint4*>(o) = make_uint4(b0, b1, b2, b3);
+#else
+  o[0] = b0; o[1] = b1; o[2] = b2; o[3] = b3;
+#endif
+}
+#if defined(__HIPCC__)
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));  // a builtin vector: assignable in any address space
+__device__ inline void row_store4(gu32* o, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  *reinterpret_cast<__attribute__((address_space(1))) u32x4_t*>(o) = u32x4_t{b0, b1, b2, b3};
+}
+#endif
+template <int SPEC, int N, class OutP = uint32_t*>
+RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d, OutP out, int* nmsg_out = nullptr) {
   constexpr uint32_t NONE = 0xFFFFFFFFu;  // never a message word (mdest would be 7)
   uint32_t ins[MAXOPS];
 #pragma unroll
@@ -1908,7 +1926,7 @@ RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d,
   if (nn > M.kmax) return E_CAP_MSG;
   uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
   int cnt = 0;
-  uint32_t* o = out;
+  OutP o = out;
 #if defined(__HIP_DEVICE_COMPILE__)
   // device rows end after their last message: the 16 B stores past it (the
   // zero padding up to M.kmax slots) are masked off -- every reader stops at
@@ -1924,9 +1942,9 @@ RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d,
     b3 = w;
     if (++cnt == 4) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      if ((int)(o - out) < used) *reinterpret_cast<uint4*>(o) = make_uint4(b0, b1, b2, b3);
+      if ((int)(o - out) < used) row_store4(o, b0, b1, b2, b3);
 #else
-      o[0] = b0; o[1] = b1; o[2] = b2; o[3] = b3;
+      row_store4(o, b0, b1, b2, b3);
 #endif
       o += 4;
       cnt = 0;
