@@ -1912,12 +1912,143 @@ void launch_mark_recv(const unsigned long long* recv, const unsigned long long* 
   hipLaunchKernelGGL(k_mark_recv, dim3((unsigned)((n + 256 * RECV_U - 1) / (256 * RECV_U))), dim3(256), 0, s, recv,
                      recv_slot, n, table, floor, flag, newcount, st, fbase, rseg, W);
 }
+// k_mark_gen's work with k_mark_tiles's shape: a wave per k_expand tile (the
+// tile's candidates are one contiguous range in the sharded layout too), its
+// lanes over 64 candidates per step, four steps per round.  Each stage of a
+// candidate's decision chain (ob / slot word / value / record position, then
+// the table entry / the owner's flag / a tile representative's position,
+// then that one's flag) is loaded for all four steps before the next stage,
+// every load unconditional.  Ranks by ballot inside each parent's segment,
+// as k_mark_tiles.  Measured and not the default (r06, 8 logical shards,
+// kernel trace of one CLI check, profiles/r06/s3/kernels_logical8_gen_tiles.txt):
+// 362 ms per check against 105 ms for the thread-per-parent k_mark_gen with
+// its stages batched (kernels_logical8_cli.txt); the cause is not
+// understood -- both read the same bytes, and this form is coalesced.
+#ifndef RMC_MARK_GEN_TILES
+#define RMC_MARK_GEN_TILES 0
+#endif
+__global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_gen_tiles(
+    unsigned long long nparents, unsigned long long pbase, const uint32_t* __restrict__ par_off,
+    const uint32_t* __restrict__ par_n, const uint32_t* __restrict__ cand_ob,
+    const unsigned long long* __restrict__ cand_fp, const unsigned long long* __restrict__ cand_val,
+    const uint32_t* __restrict__ perm, const uint8_t* __restrict__ flag_back,
+    const unsigned long long* __restrict__ table, unsigned long long mask, unsigned long long floor, int moved,
+    uint16_t* __restrict__ cand_win, uint32_t* __restrict__ par_win, unsigned long long* __restrict__ newcount,
+    DevStatus* st) {
+  __shared__ uint32_t sOff[MARK_WPB][WAVE + 1], sCarry[MARK_WPB][WAVE];
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const unsigned long long p0 = ((unsigned long long)blockIdx.x * MARK_WPB + w) * WAVE;
+  const bool active = p0 < nparents;
+  const int np = active ? (int)((nparents - p0) < WAVE ? (nparents - p0) : WAVE) : 0;
+  uint32_t my_off = 0u, my_n = 0u;
+  if (lane < np) {
+    my_off = par_off[p0 + lane];
+    my_n = par_n[p0 + lane];
+  }
+  const uint32_t off0 = __shfl(my_off, 0, WAVE);
+  if (lane < np) {
+    sOff[w][lane] = my_off - off0;
+    sCarry[w][lane] = 0;
+    if (lane == np - 1) sOff[w][np] = my_off + my_n - off0;
+  }
+  wave_lds_sync();
+  const int total = active ? (int)sOff[w][np] : 0;
+  uint32_t coll = 0, nloc = 0;
+  const unsigned long long base0 = pbase + p0 + 1;  // ranks count parents from 1
+  for (int i0 = 0; i0 < total; i0 += MARK_U * WAVE) {
+    uint32_t ob[MARK_U], pq[MARK_U], pt[MARK_U];
+    unsigned long long mine[MARK_U], cv[MARK_U], v[MARK_U];
+    uint8_t fb[MARK_U], fb2[MARK_U];
+    int pv[MARK_U];
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int idx = i0 + u * WAVE + lane;
+      const unsigned long long t = (unsigned long long)off0 + (idx < total ? idx : total - 1);
+      ob[u] = cand_ob[t];
+      mine[u] = cand_fp[t];
+      cv[u] = cand_val[t];
+      pq[u] = perm[t];
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      if (i0 + u * WAVE + lane >= total) ob[u] = OB_ERR;
+      if ((ob[u] & (OB_ERR | OB_LOCAL)) == OB_LOCAL && (mine[u] & CAND_DUP)) ob[u] |= OB_ERR;  // its round was redone
+      const bool loc = (ob[u] & (OB_ERR | OB_LOCAL)) == OB_LOCAL;
+      const bool tdup = !(ob[u] & (OB_ERR | OB_LOCAL)) && (ob[u] & OB_TDUP);
+      const bool remote = !(ob[u] & (OB_ERR | OB_LOCAL | OB_TDUP));
+      v[u] = table[2 * (loc && !moved ? (mine[u] & CAND_SLOT_MASK) : 0ULL) + 1];
+      fb[u] = flag_back[remote ? pq[u] : 0u];
+      pt[u] = perm[tdup ? (uint32_t)cv[u] : 0u];
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const bool tdup = !(ob[u] & (OB_ERR | OB_LOCAL)) && (ob[u] & OB_TDUP);
+      fb2[u] = flag_back[tdup ? pt[u] : 0u];
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int idx = i0 + u * WAVE + lane;
+      int lo = 0, hi = np - 1;  // parent p: sOff[p] <= idx < sOff[p+1]
+      if (idx < total)
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if ((int)sOff[w][mid] <= idx) lo = mid; else hi = mid - 1;
+        }
+      pv[u] = lo;
+    }
+#pragma unroll
+    for (int u = 0; u < MARK_U; ++u) {
+      const int iu = i0 + u * WAVE, idx = iu + lane, p = pv[u];
+      bool win = false;
+      if (!(ob[u] & OB_ERR)) {
+        if (ob[u] & OB_LOCAL) {
+          if (moved) v[u] = fpset_value(table, mask, cv[u]);  // the set was rehashed since the insert
+          bool c = false;
+          win = fpset_won(v[u], ((base0 + p) << 10) | (ob[u] >> 16), floor, mine[u] >> 47, c);
+          coll += c ? 1u : 0u;
+          nloc += win ? 1u : 0u;
+        } else if (ob[u] & OB_TDUP) {  // loses to its tile's representative; collides when that did
+          coll += fb2[u] == 2 ? 1u : 0u;
+        } else {
+          win = fb[u] == 1;
+        }
+      }
+      const unsigned long long m = __ballot(win);
+      if (idx < total) {
+        const int first = (int)sOff[w][p] - iu;
+        const int endl = (int)sOff[w][p + 1] - iu;
+        const unsigned long long from = first > 0 ? ~((1ULL << first) - 1ULL) : ~0ULL;
+        const uint32_t r = sCarry[w][p] + (uint32_t)__popcll(m & lanemask_lt() & from);
+        cand_win[(unsigned long long)off0 + idx] = win ? (uint16_t)(r + 1u) : (uint16_t)0;
+        if (lane == (endl < WAVE ? endl : WAVE) - 1) {
+          const unsigned long long to = endl < WAVE ? ((1ULL << endl) - 1ULL) : ~0ULL;
+          sCarry[w][p] += (uint32_t)__popcll(m & from & to);
+        }
+      }
+      wave_lds_sync();  // the carries are read by other lanes of this wave in the next step
+    }
+  }
+  if (lane < np) par_win[p0 + lane] = sCarry[w][lane];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    coll += __shfl_xor(coll, o, WAVE);
+    nloc += __shfl_xor(nloc, o, WAVE);
+  }
+  if (lane == 0 && coll) atomicAdd(&st->hidden_coll, (unsigned long long)coll);
+  if (lane == 0 && nloc) atomicAdd(newcount, (unsigned long long)nloc);
+}
 void launch_mark_gen(const LevelArgs& a, int moved, const uint32_t* perm, const uint8_t* flag_back,
                      unsigned long long* newcount, hipStream_t s) {
   if (!a.nparents) return;
+#if RMC_MARK_GEN_TILES
+  hipLaunchKernelGGL(k_mark_gen_tiles, dim3((unsigned)((a.nparents + MARK_WPB * WAVE - 1) / (MARK_WPB * WAVE))),
+                     dim3(MARK_WPB * WAVE), 0, s, a.nparents, a.pbase, a.par_off, a.par_n, a.cand_ob, a.cand_slot,
+                     a.cand_val, perm, flag_back, a.table, a.mask, a.floor, moved, a.cand_win, a.par_win, newcount, a.st);
+#else
   hipLaunchKernelGGL(k_mark_gen, dim3((unsigned)((a.nparents + 255) / 256)), dim3(256), 0, s, a.nparents, a.pbase,
                      a.par_off, a.par_n, a.cand_ob, a.cand_slot, a.cand_val, perm, flag_back, a.table, a.mask, a.floor,
                      moved, a.cand_win, a.par_win, newcount, a.st);
+#endif
 }
 int host_fp_owner(unsigned long long fp, int W) { return fp_owner(fp, W); }
 

@@ -102,7 +102,16 @@ enum ErrCode {
 };
 constexpr int NILS = 7;
 constexpr int MAXN = 7, MAXV = 4, MAXLOG = 5, MAXOPS = 7, MAXPERM = 120, MAXACT = 16, MAXFIXED = 192;
-constexpr int MAXGCODE = 512;  // words of compiled guard code (Model::gcode)
+constexpr int MAXGCODE = 512;
+// apply_delta on the device: the merge stops at the wave's largest message
+// count and reads the parent's messages four per LDS round trip.  Measured
+// and not the default (r06, bench workload, CLI, three interleaved rounds,
+// profiles/r06/ab_merge_batch.txt): k_materialize 242-244 ms against 240-241
+// for the loop form (M.kmax steps, one dependent read per step) -- the
+// merge's LDS chain is not what bounds k_materialize.
+#ifndef RMC_MERGE_BATCH
+#define RMC_MERGE_BATCH 0
+#endif  // words of compiled guard code (Model::gcode)
 
 struct Model {
   int spec, N, V, E, R, EQ, RQ, lfae, lfiq, ffbr;
@@ -1975,6 +1984,43 @@ RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d,
       if (q < d.nops && d.opk[q] == kk) w = d.opc[q];
     return w;
   };
+#if defined(__HIP_DEVICE_COMPILE__) && RMC_MERGE_BATCH
+  // Device rows: the merge runs to the wave's largest message count, not to
+  // M.kmax (the steps past a lane's own count emit zeros its masked stores
+  // drop; the emitted word count is rounded up to whole 16 B stores, and
+  // M.words is a multiple of 4, so it stays <= M.kmax), and it reads the
+  // parent's messages four at a time: each block of four steps consumes at
+  // most four of them, so their LDS loads are issued together at the
+  // block's start instead of one dependent load per step.  (The wave-wide
+  // max may read an inactive lane's stale count: it is clamped to M.kmax,
+  // and every lane of the wave computes the same value.)
+  int jmax = nn;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int y = __shfl_xor(jmax, o, 64);
+    jmax = y > jmax ? y : jmax;
+  }
+  jmax = jmax < M.kmax ? jmax : M.kmax;
+  const int head = 1 + 4 * N, steps = ((head + jmax + 3) & ~3) - head;
+#pragma unroll 1
+  for (int j0 = 0; j0 < steps; j0 += 4) {
+    uint32_t m[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) m[u] = pmsg(k + u);
+    int kk = 0;  // messages of m[] consumed so far (<= u at step u)
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (j0 + u >= steps) break;
+      const uint32_t wp = kk == 0 ? m[0] : kk == 1 ? m[1] : kk == 2 ? m[2] : m[3];
+      const bool take_ins = ins[0] < wp;
+      const uint32_t w = take_ins ? ins[0] : wp;
+      emit(w == NONE ? 0u : w);
+      if (take_ins) (void)pop_ins();
+      else kk++;
+    }
+    k += kk;
+  }
+#else
   uint32_t wp = pmsg(0);
 #pragma unroll 1
   for (int j = 0; j < M.kmax; j++) {
@@ -1988,6 +2034,7 @@ RMC_HD int apply_delta(const PState<SPEC, N>& s, const Model& M, const Delta& d,
       wp = pmsg(k);
     }
   }
+#endif
   return E_NONE;
 }
 
