@@ -635,7 +635,15 @@ __global__ __launch_bounds__(256, (N >= 5 ? (FPW == 2 ? 2 : 3) : N == 4 ? (FPW =
       }
       if (tid == 0) sBOff[cM.nfixed] = carry;
     }
+#if RMC_STAGE_BATCH
+    // the chunk table below is wave 0's too: its sBOff reads need only this
+    // wave's writes done (one block barrier fewer per tile: k_expand 657-658
+    // vs 662-665 ms per check, profiles/r06/ab_phase_b_barriers.txt; building
+    // the table in every wave to drop the next barrier too measured 662-664)
+    if (tid < WAVE) wave_lds_sync();
+#else
     __syncthreads();
+#endif
     if (tid < WAVE) {  // per action slot (lane): its first wave-sized chunk of passing pairs
       const int a = tid;
       int c = 0;
@@ -1179,9 +1187,13 @@ __global__ __launch_bounds__(MARK_WPB * WAVE) void k_mark_tiles(unsigned long lo
     for (int u = 0; u < MARK_U; ++u) {
       if (i0 + u * WAVE + lane >= total) obv[u] = OB_ERR;
       if (obv[u] & OB_ERR) slv[u] = CAND_DUP;  // (the slot word is used only without OB_ERR)
+#if RMC_TILE_DEDUP
       const bool ref = !(slv[u] & CAND_DUP) && (slv[u] & CAND_REF);
       rw[u] = cand_slot[ref ? (slv[u] & CAND_REF_MASK) : (unsigned long long)off0];
       if (!ref) rw[u] = slv[u];
+#else
+      rw[u] = slv[u];  // (no references without the tile dedup: no extra load)
+#endif
     }
 #pragma unroll
     for (int u = 0; u < MARK_U; ++u) {
